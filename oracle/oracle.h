@@ -1,0 +1,162 @@
+/*
+ * oracle.h -- CPU restatement of the Mbed TLS 4.1.0 record-protection path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in mbedtls_amd/ links, loads or calls
+ * this code; only tests/, __graft_entry__.smoke() (as the checker) and the
+ * cpu_baseline leg of bench.py use it.
+ *
+ * What it restates (reference = /root/reference, Mbed TLS 4.1.0):
+ *   - record framing of library/ssl_msg.c:
+ *       ssl_compute_padding_length        ssl_msg.c:431-435
+ *       ssl_build_inner_plaintext         ssl_msg.c:466-491
+ *       ssl_parse_inner_plaintext         ssl_msg.c:496-514
+ *       ssl_extract_add_data_from_record  ssl_msg.c:568-735 (non-CID branch)
+ *       ssl_transform_aead_dynamic_iv_is_explicit ssl_msg.c:739-743
+ *       ssl_build_record_nonce            ssl_msg.c:768-781
+ *       mbedtls_ssl_encrypt_buf (AEAD)    ssl_msg.c:784-1078
+ *       mbedtls_ssl_decrypt_buf (AEAD)    ssl_msg.c:1270-1433, 1803-1818
+ *   - transform population (ivlen / fixed_ivlen / taglen / minlen):
+ *       TLS 1.3: library/ssl_tls13_keys.c:974-998
+ *       TLS 1.2: library/ssl_tls.c:7768-7797
+ *   - PSA error mapping: library/ssl_tls.c:2157-2166
+ *
+ * The AEAD arithmetic itself lives in the TF-PSA-Crypto submodule, which is
+ * NOT vendored in /root/reference (.gitmodules:4-6; the directory is empty).
+ * It is restated here from the published standards it implements:
+ *   - AES: FIPS-197 (S-box derived from the GF(2^8) inverse + affine map)
+ *   - GCM: NIST SP 800-38D (GHASH with 4-bit Shoup tables, the Mbed TLS
+ *     builtin design class, ChangeLog:439-441)
+ *   - ChaCha20 / Poly1305 / AEAD: RFC 8439 sections 2.3, 2.5, 2.8
+ *
+ * Pinning: see oracle/README.md.  The AES-128-GCM TLS 1.3 record path is
+ * pinned by the reference's own 4 KATs (tests/suites/test_suite_ssl.data:
+ * 2776-2834).  AES-256-GCM and ChaCha20-Poly1305 have no record KAT in the
+ * reference; they are pinned by standards vectors (SP 800-38D test cases,
+ * RFC 8439 2.8.2) and a differential check against OpenSSL libcrypto.
+ */
+#ifndef TLSREC_ORACLE_H
+#define TLSREC_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes: the values of include/mbedtls/ssl.h:40-125 and the PSA codes
+ * they alias (MBEDTLS_ERR_SSL_BAD_INPUT_DATA = PSA_ERROR_INVALID_ARGUMENT
+ * = -135, MBEDTLS_ERR_SSL_BUFFER_TOO_SMALL = PSA_ERROR_BUFFER_TOO_SMALL = -138). */
+#define ORC_ERR_SSL_BAD_INPUT_DATA     (-135)
+#define ORC_ERR_SSL_BUFFER_TOO_SMALL   (-138)
+#define ORC_ERR_SSL_INVALID_MAC        (-0x7180)
+#define ORC_ERR_SSL_INVALID_RECORD     (-0x7200)
+#define ORC_ERR_SSL_INTERNAL_ERROR     (-0x6C00)
+#define ORC_ERR_SSL_FEATURE_UNAVAILABLE (-0x7080)
+
+#define ORC_VERSION_TLS1_2 0x0303
+#define ORC_VERSION_TLS1_3 0x0304
+
+#define ORC_CIPHER_AES_128_GCM        1
+#define ORC_CIPHER_AES_256_GCM        2
+#define ORC_CIPHER_CHACHA20_POLY1305  3
+
+#define ORC_OUT_CONTENT_LEN 16384     /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
+
+/* ---- primitives ------------------------------------------------------- */
+typedef struct {
+    uint32_t rk[60];
+    int nr;
+} orc_aes_ctx;
+
+int  orc_aes_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits);
+void orc_aes_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t out[16]);
+const uint8_t *orc_aes_sbox(void);
+
+typedef struct {
+    orc_aes_ctx aes;
+    uint64_t hl[16], hh[16];   /* Shoup 4-bit table of n*H */
+    uint8_t h[16];
+} orc_gcm_ctx;
+
+int  orc_gcm_setkey(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits);
+void orc_ghash_mult(const orc_gcm_ctx *ctx, const uint8_t x[16], uint8_t out[16]);
+/* one-shot GCM with a 12-byte IV; tag_len <= 16 */
+void orc_gcm_encrypt(const orc_gcm_ctx *ctx, const uint8_t iv[12],
+                     const uint8_t *aad, size_t aad_len,
+                     const uint8_t *in, size_t len, uint8_t *out,
+                     uint8_t *tag, size_t tag_len);
+/* returns 0 or ORC_ERR_SSL_INVALID_MAC */
+int  orc_gcm_decrypt(const orc_gcm_ctx *ctx, const uint8_t iv[12],
+                     const uint8_t *aad, size_t aad_len,
+                     const uint8_t *in, size_t len, uint8_t *out,
+                     const uint8_t *tag, size_t tag_len);
+/* GHASH over (aad, ct) with the length block, raw (no E(J0) mask) */
+void orc_ghash(const orc_gcm_ctx *ctx, const uint8_t *aad, size_t aad_len,
+               const uint8_t *ct, size_t ct_len, uint8_t out[16]);
+void orc_gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
+
+void orc_chacha20_block(const uint8_t key[32], uint32_t counter,
+                        const uint8_t nonce[12], uint8_t out[64]);
+void orc_chacha20_xor(const uint8_t key[32], uint32_t counter,
+                      const uint8_t nonce[12], const uint8_t *in,
+                      uint8_t *out, size_t len);
+void orc_poly1305(const uint8_t key[32], const uint8_t *msg, size_t len,
+                  uint8_t tag[16]);
+void orc_chachapoly_encrypt(const uint8_t key[32], const uint8_t nonce[12],
+                            const uint8_t *aad, size_t aad_len,
+                            const uint8_t *in, size_t len, uint8_t *out,
+                            uint8_t tag[16]);
+int  orc_chachapoly_decrypt(const uint8_t key[32], const uint8_t nonce[12],
+                            const uint8_t *aad, size_t aad_len,
+                            const uint8_t *in, size_t len, uint8_t *out,
+                            const uint8_t tag[16]);
+
+/* ---- record layer ------------------------------------------------------ */
+
+/* Mirror of the AEAD-relevant fields of struct mbedtls_ssl_transform
+ * (library/ssl_misc.h:1073-1120) with raw keys in place of PSA key ids. */
+typedef struct {
+    size_t minlen, ivlen, fixed_ivlen, maclen, taglen;
+    uint8_t iv_enc[16], iv_dec[16];
+    int tls_version;
+    int cipher;
+    size_t keylen;
+    uint8_t key_enc[32], key_dec[32];
+    orc_gcm_ctx gcm_enc, gcm_dec;   /* expanded GCM state */
+    size_t granularity;             /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY */
+} orc_transform;
+
+/* Mirror of mbedtls_record (library/ssl_misc.h:1163-1188), non-CID. */
+typedef struct {
+    uint8_t ctr[8];
+    uint8_t type;
+    uint8_t ver[2];
+    uint8_t *buf;
+    size_t buf_len;
+    size_t data_offset;
+    size_t data_len;
+} orc_record;
+
+/* Populate a transform as ssl_tls13_keys.c:922-1042 / ssl_tls.c:7639-7979
+ * (AEAD branch) would.  granularity = 16 for the default config. */
+int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
+                        const uint8_t *key_enc, const uint8_t *key_dec,
+                        const uint8_t *iv_enc, const uint8_t *iv_dec,
+                        size_t granularity);
+
+int orc_encrypt_buf(const orc_transform *t, orc_record *rec);
+int orc_decrypt_buf(const orc_transform *t, orc_record *rec);
+
+/* ---- CPU baseline batch driver (bench.py cpu_baseline leg) ------------- */
+/* Decrypt (dir=0) or encrypt (dir=1) `n` TLS records laid out at a fixed
+ * stride, all under one transform, with record i using seq = seq0 + i, on
+ * `threads` pthreads.  Returns elapsed seconds (CLOCK_MONOTONIC) or < 0. */
+double orc_bench_records(const orc_transform *t, int dir, uint8_t *arena,
+                         size_t stride, size_t data_len, uint64_t n,
+                         uint64_t seq0, int threads, int32_t *status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

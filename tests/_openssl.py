@@ -1,0 +1,108 @@
+"""Independent AEAD cross-check through OpenSSL libcrypto (ctypes, EVP API).
+
+Used only by tests and the golden-vector generator to cross-validate the CPU
+restatement in oracle/ for AES-256-GCM and ChaCha20-Poly1305, for which the
+reference ships no record-level KAT.  Returns None when the
+library is not present.
+"""
+from __future__ import annotations
+
+import ctypes
+import ctypes.util
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        for name in ("libcrypto.so.3", ctypes.util.find_library("crypto")):
+            if not name:
+                continue
+            try:
+                _lib = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+        if _lib is None:
+            return None
+        L = _lib
+        L.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
+        L.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
+        for f in ("EVP_aes_128_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305"):
+            getattr(L, f).restype = ctypes.c_void_p
+        L.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_char_p, ctypes.c_char_p]
+        L.EVP_DecryptInit_ex.argtypes = L.EVP_EncryptInit_ex.argtypes
+        L.EVP_CIPHER_CTX_ctrl.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        upd = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+               ctypes.c_char_p, ctypes.c_int]
+        L.EVP_EncryptUpdate.argtypes = upd
+        L.EVP_DecryptUpdate.argtypes = upd
+        L.EVP_EncryptFinal_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.EVP_DecryptFinal_ex.argtypes = L.EVP_EncryptFinal_ex.argtypes
+    return _lib
+
+
+EVP_CTRL_AEAD_SET_IVLEN = 0x9
+EVP_CTRL_AEAD_GET_TAG = 0x10
+EVP_CTRL_AEAD_SET_TAG = 0x11
+
+
+def _cipher(name: str, keylen: int):
+    L = lib()
+    if name == "gcm":
+        return L.EVP_aes_128_gcm() if keylen == 16 else L.EVP_aes_256_gcm()
+    return L.EVP_chacha20_poly1305()
+
+
+def seal(name: str, key: bytes, nonce: bytes, aad: bytes, pt: bytes):
+    L = lib()
+    ctx = L.EVP_CIPHER_CTX_new()
+    try:
+        c = _cipher(name, len(key))
+        assert L.EVP_EncryptInit_ex(ctx, c, None, None, None) == 1
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_IVLEN, len(nonce), None) == 1
+        assert L.EVP_EncryptInit_ex(ctx, None, None, key, nonce) == 1
+        n = ctypes.c_int(0)
+        if aad:
+            assert L.EVP_EncryptUpdate(ctx, None, ctypes.byref(n), aad, len(aad)) == 1
+        out = ctypes.create_string_buffer(len(pt) + 32)
+        total = 0
+        if pt:
+            assert L.EVP_EncryptUpdate(ctx, out, ctypes.byref(n), pt, len(pt)) == 1
+            total = n.value
+        assert L.EVP_EncryptFinal_ex(ctx, ctypes.byref(out, total), ctypes.byref(n)) == 1
+        total += n.value
+        tag = ctypes.create_string_buffer(16)
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, 16, tag) == 1
+        return out.raw[:total], tag.raw
+    finally:
+        L.EVP_CIPHER_CTX_free(ctx)
+
+
+def open_(name: str, key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes):
+    """Returns plaintext bytes, or None when the tag does not verify."""
+    L = lib()
+    ctx = L.EVP_CIPHER_CTX_new()
+    try:
+        c = _cipher(name, len(key))
+        assert L.EVP_DecryptInit_ex(ctx, c, None, None, None) == 1
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_IVLEN, len(nonce), None) == 1
+        assert L.EVP_DecryptInit_ex(ctx, None, None, key, nonce) == 1
+        n = ctypes.c_int(0)
+        if aad:
+            assert L.EVP_DecryptUpdate(ctx, None, ctypes.byref(n), aad, len(aad)) == 1
+        out = ctypes.create_string_buffer(len(ct) + 32)
+        total = 0
+        if ct:
+            assert L.EVP_DecryptUpdate(ctx, out, ctypes.byref(n), ct, len(ct)) == 1
+            total = n.value
+        tbuf = ctypes.create_string_buffer(bytes(tag), 16)
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_TAG, 16, tbuf) == 1
+        ok = L.EVP_DecryptFinal_ex(ctx, ctypes.byref(out, total), ctypes.byref(n))
+        if ok != 1:
+            return None
+        return out.raw[:total]
+    finally:
+        L.EVP_CIPHER_CTX_free(ctx)
