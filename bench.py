@@ -1,0 +1,297 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident TLS record AEAD throughput on MI355X.
+
+Default workload = BASELINE.json configs[1]: TLS 1.3 AES-256-GCM *decrypt* of
+2^20 records x 16 KiB (16383 B content + 1 B type = 16384 B inner plaintext,
+16400 B ciphertext+tag) under one key, inputs resident in HBM.  One step = one
+tlsrec_batch_decrypt call over the whole batch (one kernel launch).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+
+Multi-GPU (driver): torchrun ... bench.py --gpus N.  Records shard by
+contiguous range (2^20 per rank, weak scaling); the only collective is the
+RCCL broadcast of the key table from rank 0 (plus the max-time reduction).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "TLS records/sec + GiB/s AEAD throughput (device-resident), 16 KiB records"
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 0x7115EC0DE
+
+CONFIGS = {
+    # name: (cipher, tls, direction, content bytes, records, keys, workload text)
+    "c2": ("AES-256-GCM", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
+           "AES-256-GCM decrypt, 1M x 16 KiB TLS 1.3 application-data records, single key"),
+    "c3": ("CHACHA20-POLY1305", "TLS1.3", "encrypt", 1400, 1 << 20, 1,
+           "ChaCha20-Poly1305 encrypt, 1M x 1.4 KiB TLS 1.3 records, single key"),
+    "c4": ("MIX", "TLS1.3", "decrypt", 16383, 1 << 22, 1 << 16,
+           "64K keys x 64 records, AES-256-GCM + ChaCha20-Poly1305 interleaved, 16 KiB"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of the CPU sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", type=int, default=64, help="records spot-checked against the oracle")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def inner_len(content, tls):
+    if tls == "TLS1.3":
+        return content + 1 + (16 - (content + 1) % 16) % 16
+    return content
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import mbedtls_amd as M
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    cname, tls, direction, content, n_default, nkeys, workload = CONFIGS[args.config]
+    n = args.records or n_default
+    ver = M.VERSION_TLS1_3 if tls == "TLS1.3" else M.VERSION_TLS1_2
+    inner = inner_len(content, tls)
+    wire = inner + 16
+    stride = (wire + 15) // 16 * 16
+    ciphers = {"AES-256-GCM": [M.CIPHER_AES_256_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
+               "MIX": [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]}[cname]
+    nkeys = min(nkeys, n)
+
+    # ---- key table: generated on rank 0, broadcast over RCCL (xGMI) -------------
+    from tests.prng import prng_array
+    km = np.zeros(nkeys, dtype=M.KEY_MATERIAL)
+    if rank == 0:
+        raw = prng_array(SEED, nkeys * 48).reshape(nkeys, 48)
+        km["cipher"] = np.array([ciphers[i % len(ciphers)] for i in range(nkeys)], dtype=np.uint8)
+        km["tls_minor"] = 4 if ver == M.VERSION_TLS1_3 else 3
+        km["fixed_ivlen"] = 12
+        km["taglen"] = 16
+        km["key"] = raw[:, :32]
+        km["iv"][:, :12] = raw[:, 32:44]
+    keys_dev = torch.from_numpy(km.view(np.uint8).copy()).to(dev)
+    if world > 1:
+        dist.broadcast(keys_dev, src=0)
+    kt = M.KeyTable(nkeys)
+    kt.load(keys_dev)
+
+    # ---- synthetic records (this rank's shard) ---------------------------------
+    shard0 = rank * n
+    arena = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev)
+    recs = M.records(n)
+    recs["buf_off"] = np.arange(n, dtype=np.uint64) * stride
+    recs["buf_len"] = stride
+    recs["data_offset"] = 0
+    recs["data_len"] = content
+    if nkeys == 1:
+        recs["slot"] = 0
+    else:   # round-robin over keys, then grouped by key so a workgroup shares its key
+        recs["slot"] = np.sort(np.arange(n, dtype=np.uint64) % nkeys).astype(np.uint32)
+    seq = np.arange(shard0, shard0 + n, dtype=np.uint64)
+    recs["ctr"] = M.seq_bytes(seq)
+    recs["type"] = 23
+    recs["ver"] = (3, 3)
+    recs_dev = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+    res_dev = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    sample = list(range(0, n, max(1, n // max(1, args.verify))))[:args.verify]
+    pt_sample = {i: arena[i * stride:i * stride + content].cpu().numpy().copy() for i in sample}
+
+    if direction == "decrypt":
+        # produce the ciphertexts with the (separately verified) encrypt kernel
+        M.batch_encrypt(kt, recs_dev, res_dev, n, arena, arena, lanes=args.lanes)
+        torch.cuda.synchronize()
+        enc_status = res_dev.view(torch.int32)[0::4]
+        assert int((enc_status != 0).sum()) == 0, "encrypt of the synthetic batch failed"
+        dec = recs.copy()
+        dec["data_len"] = wire
+        in_recs = torch.from_numpy(dec.view(np.uint8).copy()).to(dev)
+        in_arena, out_arena = arena, torch.empty_like(arena)
+        run = lambda: M.batch_decrypt(kt, in_recs, res_dev, n, in_arena, out_arena, lanes=args.lanes)  # noqa: E731
+    else:
+        in_recs = recs_dev
+        in_arena, out_arena = arena, torch.empty_like(arena)
+        run = lambda: M.batch_encrypt(kt, in_recs, res_dev, n, in_arena, out_arena, lanes=args.lanes)  # noqa: E731
+
+    # ---- warmup, then K timed steps -----------------------------------------
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        run()
+        b.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+
+    # ---- correctness of what was timed ----------------------------------------
+    st = res_dev.view(torch.int32)[0::4]
+    bad = int((st != 0).sum())
+    lens = res_dev.view(torch.int32)[2::4]
+    if direction == "decrypt":
+        bad += int((lens != content).sum())
+        for i in sample:
+            got = out_arena[i * stride:i * stride + content].cpu().numpy()
+            bad += int(not np.array_equal(got, pt_sample[i]))
+    bad_t = torch.tensor([bad], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(bad_t)
+    bad = int(bad_t.item())
+
+    # oracle spot check of the bytes (rank 0, sample): the ciphertext the
+    # GPU produced must equal the CPU restatement's for the same inputs
+    oracle_ok = None
+    if rank == 0 and args.verify:
+        import oracle as O
+        oc = {M.CIPHER_AES_256_GCM: O.AES_256_GCM, M.CIPHER_CHACHA20_POLY1305: O.CHACHA20_POLY1305}
+        oracle_ok = True
+        src = arena if direction == "decrypt" else out_arena
+        for i in sample[:16]:
+            s = int(recs["slot"][i])
+            k = km[s] if rank == 0 else None
+            ot = O.Transform(O.TLS1_3 if ver == M.VERSION_TLS1_3 else O.TLS1_2, oc[int(k["cipher"])],
+                             bytes(k["key"]), bytes(k["key"]), bytes(k["iv"]), bytes(k["iv"]))
+            buf = bytearray(stride)
+            buf[:content] = pt_sample[i].tobytes()
+            orec = O.Record(ctr=bytes(recs["ctr"][i]), type=23, ver=b"\x03\x03", buf=buf,
+                            data_offset=0, data_len=content)
+            assert ot.encrypt_buf(orec) == 0
+            got = src[i * stride:i * stride + wire].cpu().numpy().tobytes()
+            oracle_ok &= got == orec.data()
+
+    # ---- roofline of the dominant kernel --------------------------------------
+    # algorithmic bytes per record: ciphertext+tag (or content) read, inner
+    # plaintext (or ciphertext+tag) written, 40 B descriptor read, 16 B result
+    if direction == "decrypt":
+        alg_per_rec = wire + inner + 40 + 16
+    else:
+        alg_per_rec = content + wire + 40 + 16
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    achieved = alg_per_rec * n / kern_avg_s / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("records") == n:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    steps_s = wall / args.steps
+    payload_total = float(n) * inner * world
+    value = payload_total / steps_s / 2**30
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(cname, ver, content, inner, wire, stride, km, args.cpu_seconds, direction)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(steps_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 keys/nonces, uniform random payload; decrypt inputs made by the verified encrypt kernel)",
+        "config": {"workload": workload, "config": args.config, "records_per_gpu": n,
+                   "record_inner_bytes": inner, "record_wire_bytes": wire, "keys": nkeys,
+                   "lanes_per_record": args.lanes or "auto", "parallelism": f"shard{world}"},
+        "records_per_s": round(n * world / steps_s, 1),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_record": alg_per_rec, "kernel_ms_avg": round(kern_avg_s * 1e3, 4)},
+        "cpu_baseline": cpu,
+        "check": {"bad_records": bad, "oracle_sample_ok": oracle_ok},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, direction):
+    """oracle/ (the CPU restatement, kind 'port') timed on this host's cores on
+    a bounded sample of the same workload."""
+    import oracle as O
+    cipher = O.CHACHA20_POLY1305 if cname == "CHACHA20-POLY1305" else O.AES_256_GCM
+    k = km[0]
+    t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"]), bytes(k["key"]),
+                    bytes(k["iv"]), bytes(k["iv"]))
+    threads = min(16, os.cpu_count() or 1)
+    from tests.prng import prng_array
+    n = 256
+    while True:
+        arena = np.zeros(n * stride, dtype=np.uint8)
+        payload = prng_array(SEED ^ 0xC0FFEE, n * content).reshape(n, content)
+        arena.reshape(n, stride)[:, :content] = payload
+        if direction == "decrypt":
+            st = np.zeros(n, dtype=np.int32)
+            t.bench(1, arena, stride, content, n, 0, threads, st)     # seal (untimed)
+            assert (st == 0).all()
+            el = t.bench(0, arena, stride, wire, n, 0, threads, st)
+            assert (st == 0).all()
+        else:
+            st = np.zeros(n, dtype=np.int32)
+            el = t.bench(1, arena, stride, content, n, 0, threads, st)
+            assert (st == 0).all()
+        if el >= target_s or n >= (1 << 18):
+            break
+        n = int(n * max(2.0, min(8.0, target_s / max(el, 1e-3))))
+    gib = n * inner / el / 2**30
+    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} records x {inner} B inner plaintext, {direction}, oracle/liboracle.so "
+                      f"(table AES + 4-bit Shoup GHASH / ChaCha20 + 44-bit-limb Poly1305), {el:.2f} s wall on {threads} threads"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * tlsrec.h -- C ABI of the MI355X TLS record-protection engine (libtlsrec.so).
+ *
+ * Drop-in boundary for the AEAD record path of Mbed TLS 4.1.0:
+ *
+ *   reference (internal, library/ssl_misc.h:1724-1732)     this library
+ *   ---------------------------------------------------    ----------------------
+ *   int mbedtls_ssl_encrypt_buf(ssl, transform, rec)       tlsrec_encrypt_buf
+ *       library/ssl_msg.c:784-1268
+ *   int mbedtls_ssl_decrypt_buf(ssl, transform, rec)       tlsrec_decrypt_buf
+ *       library/ssl_msg.c:1270-1834
+ *   struct mbedtls_ssl_transform (ssl_misc.h:1073-1120)    tlsrec_transform
+ *   mbedtls_record               (ssl_misc.h:1163-1188)    tlsrec_record
+ *   mbedtls_ssl_tls13_populate_transform                   tlsrec_transform_setup
+ *       (library/ssl_tls13_keys.c:922-1042) and the AEAD
+ *       branch of ssl_tls12_populate_transform
+ *       (library/ssl_tls.c:7768-7797)
+ *   mbedtls_ssl_transform_free (ssl_msg.c:6084-6099)       tlsrec_transform_free
+ *   psa_aead_encrypt / psa_aead_decrypt (TF-PSA-Crypto,    the HIP kernels behind
+ *       called at ssl_msg.c:1043 and :1412)                 every entry point
+ *
+ * plus a device-resident batch extension (tlsrec_batch_encrypt/decrypt) that
+ * applies the same per-record semantics to many records already in HBM, and a
+ * key table (tlsrec_keytab_*) that holds per-connection keys on the GPU.
+ *
+ * Semantics and error codes are those of the reference: 0 on success or a
+ * negative MBEDTLS_ERR_SSL_* value (include/mbedtls/ssl.h:40-125); the record
+ * is transformed in place and its data_offset / data_len / type are updated
+ * exactly as the reference updates them.  Only the AEAD suites are supported
+ * (AES-128-GCM, AES-256-GCM, ChaCha20-Poly1305; TLS 1.2 and 1.3, no CID).
+ *
+ * Every entry point that touches record data runs on the GPU; there is no CPU
+ * fallback.  Without a usable HIP device they return
+ * TLSREC_ERR_SSL_HW_ACCEL_FAILED (MBEDTLS_ERR_SSL_HW_ACCEL_FAILED).
+ */
+#ifndef TLSREC_H
+#define TLSREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants (values of include/mbedtls/ssl.h) ---------------------- */
+#define TLSREC_ERR_SSL_BAD_INPUT_DATA        (-135)    /* PSA_ERROR_INVALID_ARGUMENT, ssl.h:40 */
+#define TLSREC_ERR_SSL_BUFFER_TOO_SMALL      (-138)    /* PSA_ERROR_BUFFER_TOO_SMALL, ssl.h:125 */
+#define TLSREC_ERR_SSL_ALLOC_FAILED          (-141)    /* PSA_ERROR_INSUFFICIENT_MEMORY, ssl.h:101 */
+#define TLSREC_ERR_SSL_FEATURE_UNAVAILABLE   (-0x7080) /* ssl.h:38 */
+#define TLSREC_ERR_SSL_INVALID_MAC           (-0x7180) /* ssl.h:42 */
+#define TLSREC_ERR_SSL_INVALID_RECORD        (-0x7200) /* ssl.h:44 */
+#define TLSREC_ERR_SSL_HW_ACCEL_FAILED       (-0x7F80) /* ssl.h:103 */
+#define TLSREC_ERR_SSL_INTERNAL_ERROR        (-0x6C00) /* ssl.h:117 */
+
+#define TLSREC_VERSION_TLS1_2   0x0303   /* MBEDTLS_SSL_VERSION_TLS1_2 */
+#define TLSREC_VERSION_TLS1_3   0x0304   /* MBEDTLS_SSL_VERSION_TLS1_3 */
+
+#define TLSREC_CIPHER_AES_128_GCM        1
+#define TLSREC_CIPHER_AES_256_GCM        2
+#define TLSREC_CIPHER_CHACHA20_POLY1305  3
+
+#define TLSREC_MSG_APPLICATION_DATA  23      /* ssl.h:527 */
+#define TLSREC_OUT_CONTENT_LEN       16384   /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
+#define TLSREC_PADDING_GRANULARITY   16      /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY, ssl.h:432 */
+
+/* ---- single-record API (host buffers) --------------------------------- */
+
+/* AEAD fields of struct mbedtls_ssl_transform, with raw key bytes and
+ * device key-table slots in place of the PSA key ids psa_key_enc/dec. */
+typedef struct tlsrec_transform {
+    size_t minlen;           /* min. ciphertext length */
+    size_t ivlen;            /* 12 */
+    size_t fixed_ivlen;      /* 12, or 4 for TLS 1.2 GCM */
+    size_t maclen;           /* 0 for AEAD */
+    size_t taglen;           /* 16 */
+    unsigned char iv_enc[16];
+    unsigned char iv_dec[16];
+    int tls_version;         /* TLSREC_VERSION_* */
+    int cipher;              /* TLSREC_CIPHER_* */
+    size_t keylen;           /* 16 or 32 */
+    unsigned char key_enc[32];
+    unsigned char key_dec[32];
+    int32_t slot_enc;        /* device key slots (engine key table), -1 = none */
+    int32_t slot_dec;
+    uint32_t granularity;    /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY (16) */
+} tlsrec_transform;
+
+/* mbedtls_record without the CID fields. */
+typedef struct tlsrec_record {
+    uint8_t ctr[8];          /* implicit sequence number, big endian */
+    uint8_t type;            /* record content type */
+    uint8_t ver[2];          /* version as on the wire */
+    unsigned char *buf;      /* host buffer enclosing the record content */
+    size_t buf_len;
+    size_t data_offset;
+    size_t data_len;
+} tlsrec_record;
+
+/* Populate `t` like mbedtls_ssl_tls13_populate_transform (TLS 1.3) or the
+ * AEAD branch of ssl_tls12_populate_transform (TLS 1.2) and import both keys
+ * into the engine's device key table.  iv_* point at 12 bytes (TLS 1.3,
+ * ChaChaPoly) or at least fixed_ivlen bytes (TLS 1.2 GCM: 4). */
+int tlsrec_transform_setup(tlsrec_transform *t, int tls_version, int cipher,
+                           const unsigned char *key_enc, const unsigned char *key_dec,
+                           const unsigned char *iv_enc, const unsigned char *iv_dec);
+/* As tlsrec_transform_setup with an explicit TLS 1.3 padding granularity
+ * (the reference's compile-time MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY;
+ * its record KATs are generated with 1). */
+int tlsrec_transform_setup_ex(tlsrec_transform *t, int tls_version, int cipher,
+                              const unsigned char *key_enc, const unsigned char *key_dec,
+                              const unsigned char *iv_enc, const unsigned char *iv_dec,
+                              unsigned granularity);
+/* Release the key slots and zeroize the transform. */
+void tlsrec_transform_free(tlsrec_transform *t);
+
+/* Same contract as mbedtls_ssl_encrypt_buf / mbedtls_ssl_decrypt_buf;
+ * `ssl` is accepted for signature parity and only used for debugging in the
+ * reference, it may be NULL. */
+int tlsrec_encrypt_buf(void *ssl, tlsrec_transform *t, tlsrec_record *rec);
+int tlsrec_decrypt_buf(const void *ssl, tlsrec_transform *t, tlsrec_record *rec);
+
+/* ---- device key table -------------------------------------------------- */
+
+/* One direction of one connection: the raw material a handshake produces
+ * (what the RCCL broadcast carries).  64 bytes. */
+typedef struct tlsrec_key_material {
+    uint8_t cipher;          /* TLSREC_CIPHER_* */
+    uint8_t tls_minor;       /* 3 = TLS 1.2, 4 = TLS 1.3 */
+    uint8_t fixed_ivlen;     /* 12, or 4 for TLS 1.2 GCM */
+    uint8_t taglen;          /* 16 */
+    uint8_t granularity;     /* TLS 1.3 padding granularity, 0 = 16 (ssl.h:432) */
+    uint8_t reserved[11];
+    uint8_t iv[16];          /* static IV, first fixed_ivlen bytes used */
+    uint8_t key[32];         /* 16 or 32 bytes used */
+} tlsrec_key_material;
+
+typedef struct tlsrec_keytab tlsrec_keytab;
+
+/* Device table of `capacity` slots on the current HIP device. */
+int tlsrec_keytab_create(tlsrec_keytab **kt, uint32_t capacity);
+/* Load `count` slots starting at `first` from `keys` (host memory, or device
+ * memory when keys_on_device != 0) and expand them on the GPU (AES key
+ * schedule, H = E_K(0), GHASH tables).  Enqueued on `stream` (hipStream_t,
+ * NULL = default stream). */
+int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t count,
+                       const tlsrec_key_material *keys, int keys_on_device,
+                       void *stream);
+uint32_t tlsrec_keytab_capacity(const tlsrec_keytab *kt);
+void tlsrec_keytab_free(tlsrec_keytab *kt);
+
+/* ---- device-resident batch API ----------------------------------------- */
+
+/* mbedtls_record with offsets into a device arena (40 bytes). */
+typedef struct tlsrec_batch_rec {
+    uint64_t buf_off;        /* rec->buf = arena + buf_off */
+    uint32_t buf_len;
+    uint32_t data_offset;
+    uint32_t data_len;
+    uint32_t slot;           /* key-table slot = the transform direction */
+    uint8_t  ctr[8];         /* sequence number, big endian */
+    uint8_t  type;
+    uint8_t  ver[2];
+    uint8_t  reserved[5];
+} tlsrec_batch_rec;
+
+/* The fields of the record after the call, plus its status (16 bytes). */
+typedef struct tlsrec_batch_res {
+    int32_t  status;         /* 0 or MBEDTLS_ERR_SSL_* */
+    uint32_t data_offset;
+    uint32_t data_len;
+    uint8_t  type;
+    uint8_t  reserved[3];
+} tlsrec_batch_res;
+
+/* Protect / unprotect `n` records.  `recs` and `res` are device arrays; the
+ * record buffers live in `in_arena`; results are written to the same offsets
+ * of `out_arena` (== in_arena for the reference's in-place behaviour).
+ * lanes_per_record: 0 = auto, else 8/16/32/64 lanes of a wavefront share one
+ * record.  Asynchronous on `stream`; per-record status lands in `res`. */
+int tlsrec_batch_encrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
+                         tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
+                         uint8_t *out_arena, uint32_t lanes_per_record, void *stream);
+int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
+                         tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
+                         uint8_t *out_arena, uint32_t lanes_per_record, void *stream);
+
+/* Host-only: run the record-framing checks of encrypt_buf / decrypt_buf
+ * (everything decided before the AEAD, tlsrec_frame.h) for one batch record
+ * under `km`.  Returns 1 if the record proceeds to the AEAD (aead_pos /
+ * aead_len filled), 0 if it stops early (`early` holds the status and the
+ * record fields the reference would leave).  Needs no GPU. */
+int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_batch_rec *rec,
+                       tlsrec_batch_res *early, uint32_t *aead_pos, uint32_t *aead_len);
+
+/* ---- engine ------------------------------------------------------------- */
+/* 0 if a gfx950 device is usable, else TLSREC_ERR_SSL_HW_ACCEL_FAILED. */
+int tlsrec_device_check(void);
+/* Library build string (kernel variants, arch). */
+const char *tlsrec_version_string(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TLSREC_H */

@@ -1,0 +1,24 @@
+"""mbedtls_amd -- MI355X TLS record-layer AEAD engine.
+
+A drop-in for the record encrypt/decrypt path of Mbed TLS 4.1.0
+(``mbedtls_ssl_encrypt_buf`` / ``mbedtls_ssl_decrypt_buf``, library/ssl_msg.c)
+with hand-written gfx950 kernels for AES-128/256-GCM and ChaCha20-Poly1305.
+The C ABI is include/tlsrec.h; this package is its Python binding.
+"""
+from ._abi import (CIPHER_AES_128_GCM, CIPHER_AES_256_GCM, CIPHER_CHACHA20_POLY1305,  # noqa: F401
+                   ERR_SSL_BAD_INPUT_DATA, ERR_SSL_BUFFER_TOO_SMALL, ERR_SSL_FEATURE_UNAVAILABLE,
+                   ERR_SSL_HW_ACCEL_FAILED, ERR_SSL_INTERNAL_ERROR, ERR_SSL_INVALID_MAC,
+                   ERR_SSL_INVALID_RECORD, MSG_APPLICATION_DATA, VERSION_TLS1_2, VERSION_TLS1_3,
+                   BATCH_REC, BATCH_RES, KEY_MATERIAL, load)
+from .batch import (KeyTable, batch_decrypt, batch_encrypt, frame_check, key_material,  # noqa: F401
+                    records, results, seq_bytes)
+from .record import Record, Transform, decrypt_buf, encrypt_buf  # noqa: F401
+
+
+def device_ok() -> bool:
+    """True when a gfx950 device is usable by libtlsrec."""
+    return load().tlsrec_device_check() == 0
+
+
+def version() -> str:
+    return load().tlsrec_version_string().decode()

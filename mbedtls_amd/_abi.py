@@ -1,0 +1,104 @@
+"""ctypes binding of include/tlsrec.h (the C ABI of libtlsrec.so).
+
+This is the same binding a maintainer would add to a Python caller of the
+reference record path; it loads the in-tree HIP library
+and raises if it is missing -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libtlsrec.so")
+
+# ---- constants (include/tlsrec.h, values of include/mbedtls/ssl.h) ----------
+ERR_SSL_BAD_INPUT_DATA = -135
+ERR_SSL_BUFFER_TOO_SMALL = -138
+ERR_SSL_ALLOC_FAILED = -141
+ERR_SSL_FEATURE_UNAVAILABLE = -0x7080
+ERR_SSL_INVALID_MAC = -0x7180
+ERR_SSL_INVALID_RECORD = -0x7200
+ERR_SSL_HW_ACCEL_FAILED = -0x7F80
+ERR_SSL_INTERNAL_ERROR = -0x6C00
+
+VERSION_TLS1_2 = 0x0303
+VERSION_TLS1_3 = 0x0304
+CIPHER_AES_128_GCM = 1
+CIPHER_AES_256_GCM = 2
+CIPHER_CHACHA20_POLY1305 = 3
+MSG_APPLICATION_DATA = 23
+
+# ---- layouts -----------------------------------------------------------------
+KEY_MATERIAL = np.dtype([("cipher", "u1"), ("tls_minor", "u1"), ("fixed_ivlen", "u1"),
+                         ("taglen", "u1"), ("granularity", "u1"), ("reserved", "u1", 11),
+                         ("iv", "u1", 16), ("key", "u1", 32)])
+BATCH_REC = np.dtype([("buf_off", "<u8"), ("buf_len", "<u4"), ("data_offset", "<u4"),
+                      ("data_len", "<u4"), ("slot", "<u4"), ("ctr", "u1", 8), ("type", "u1"),
+                      ("ver", "u1", 2), ("reserved", "u1", 5)])
+BATCH_RES = np.dtype([("status", "<i4"), ("data_offset", "<u4"), ("data_len", "<u4"),
+                      ("type", "u1"), ("reserved", "u1", 3)])
+assert KEY_MATERIAL.itemsize == 64 and BATCH_REC.itemsize == 40 and BATCH_RES.itemsize == 16
+
+
+class CTransform(ctypes.Structure):
+    _fields_ = [("minlen", ctypes.c_size_t), ("ivlen", ctypes.c_size_t),
+                ("fixed_ivlen", ctypes.c_size_t), ("maclen", ctypes.c_size_t),
+                ("taglen", ctypes.c_size_t), ("iv_enc", ctypes.c_ubyte * 16),
+                ("iv_dec", ctypes.c_ubyte * 16), ("tls_version", ctypes.c_int),
+                ("cipher", ctypes.c_int), ("keylen", ctypes.c_size_t),
+                ("key_enc", ctypes.c_ubyte * 32), ("key_dec", ctypes.c_ubyte * 32),
+                ("slot_enc", ctypes.c_int32), ("slot_dec", ctypes.c_int32),
+                ("granularity", ctypes.c_uint32)]
+
+
+class CRecord(ctypes.Structure):
+    _fields_ = [("ctr", ctypes.c_ubyte * 8), ("type", ctypes.c_ubyte), ("ver", ctypes.c_ubyte * 2),
+                ("buf", ctypes.c_void_p), ("buf_len", ctypes.c_size_t),
+                ("data_offset", ctypes.c_size_t), ("data_len", ctypes.c_size_t)]
+
+
+# every function include/tlsrec.h declares, with its signature
+_VP, _U32, _INT = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+SIGNATURES = {
+    "tlsrec_transform_setup": (_INT, [_VP, _INT, _INT, _VP, _VP, _VP, _VP]),
+    "tlsrec_transform_setup_ex": (_INT, [_VP, _INT, _INT, _VP, _VP, _VP, _VP, ctypes.c_uint]),
+    "tlsrec_transform_free": (None, [_VP]),
+    "tlsrec_encrypt_buf": (_INT, [_VP, _VP, _VP]),
+    "tlsrec_decrypt_buf": (_INT, [_VP, _VP, _VP]),
+    "tlsrec_keytab_create": (_INT, [ctypes.POINTER(_VP), _U32]),
+    "tlsrec_keytab_load": (_INT, [_VP, _U32, _U32, _VP, _INT, _VP]),
+    "tlsrec_keytab_capacity": (_U32, [_VP]),
+    "tlsrec_keytab_free": (None, [_VP]),
+    "tlsrec_batch_encrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
+    "tlsrec_batch_decrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
+    "tlsrec_frame_check": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP]),
+    "tlsrec_device_check": (_INT, []),
+    "tlsrec_version_string": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load():
+    """Load libtlsrec.so (HIP runtime linked).  torch, when importable, is
+    imported first so that the process uses a single libamdhip64."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (shares its HIP runtime with us)
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -m mbedtls_amd.build` "
+                          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L

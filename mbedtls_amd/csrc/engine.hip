@@ -1,0 +1,308 @@
+/*
+ * engine.hip -- host side of the device engine: key tables, batch launches,
+ * and the staging used by the single-record entry points.
+ *
+ * Everything here is plain HIP runtime C++ behind the extern "C" ABI of
+ * include/tlsrec.h.  No torch types, no CPU crypto: a record is only ever
+ * transformed by the kernels in kernels.hip.
+ */
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "tlsrec.h"
+#include "tlsrec_internal.h"
+
+using namespace tlsrec;
+
+struct tlsrec_keytab {
+    uint32_t capacity;
+    int device;
+    SlotState *d_slots;
+    uint4 *d_ghtab;
+    tlsrec_key_material *d_stage;
+    uint8_t *h_cipher;        /* host mirror of each slot's cipher */
+    uint32_t cipher_mask;     /* 1 << TLSREC_CIPHER_* of every loaded slot */
+};
+
+static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED; }
+
+extern "C" int tlsrec_device_check(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    return 0;
+}
+
+extern "C" const char *tlsrec_version_string(void)
+{
+    return "tlsrec 0.1 gfx950: aes-gcm(L=4/8/16/64, T-tables in LDS, GHASH 4-bit position tables) "
+           "chacha20-poly1305(L=1/2/4/8, 26-bit limbs)";
+}
+
+extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
+{
+    if (out == NULL || capacity == 0) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    *out = NULL;
+    if (tlsrec_device_check() != 0) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    tlsrec_keytab *kt = (tlsrec_keytab *) calloc(1, sizeof(*kt));
+    if (!kt) return TLSREC_ERR_SSL_ALLOC_FAILED;
+    kt->capacity = capacity;
+    hipGetDevice(&kt->device);
+    kt->h_cipher = (uint8_t *) calloc(capacity, 1);
+    if (!kt->h_cipher ||
+        hipMalloc((void **) &kt->d_slots, sizeof(SlotState) * (size_t) capacity) != hipSuccess ||
+        hipMalloc((void **) &kt->d_ghtab, sizeof(uint4) * (size_t) KEY_TABLE_WORDS * capacity) != hipSuccess ||
+        hipMalloc((void **) &kt->d_stage, sizeof(tlsrec_key_material) * (size_t) capacity) != hipSuccess) {
+        tlsrec_keytab_free(kt);
+        return TLSREC_ERR_SSL_ALLOC_FAILED;
+    }
+    if (hipMemset(kt->d_slots, 0, sizeof(SlotState) * (size_t) capacity) != hipSuccess) {
+        tlsrec_keytab_free(kt);
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    *out = kt;
+    return 0;
+}
+
+extern "C" uint32_t tlsrec_keytab_capacity(const tlsrec_keytab *kt) { return kt ? kt->capacity : 0; }
+
+extern "C" void tlsrec_keytab_free(tlsrec_keytab *kt)
+{
+    if (!kt) return;
+    if (kt->d_slots) {
+        /* zeroize key material (ssl_msg.c:6084-6099 zeroizes transforms) */
+        hipMemset(kt->d_slots, 0, sizeof(SlotState) * (size_t) kt->capacity);
+        hipMemset(kt->d_ghtab, 0, sizeof(uint4) * (size_t) KEY_TABLE_WORDS * kt->capacity);
+        hipDeviceSynchronize();
+    }
+    hipFree(kt->d_slots);
+    hipFree(kt->d_ghtab);
+    hipFree(kt->d_stage);
+    free(kt->h_cipher);
+    free(kt);
+}
+
+static int check_material(const tlsrec_key_material *k)
+{
+    if (k->cipher < TLSREC_CIPHER_AES_128_GCM || k->cipher > TLSREC_CIPHER_CHACHA20_POLY1305)
+        return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
+    if (k->tls_minor != 3 && k->tls_minor != 4) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (k->taglen != 16) return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
+    if (k->fixed_ivlen != 12 && k->fixed_ivlen != 4) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    return 0;
+}
+
+extern "C" int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t count,
+                                  const tlsrec_key_material *keys, int keys_on_device, void *stream)
+{
+    if (!kt || !keys || first > kt->capacity || count > kt->capacity - first) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (count == 0) return 0;
+    hipStream_t st = (hipStream_t) stream;
+    tlsrec_key_material *host = NULL;
+    if (keys_on_device) {
+        host = (tlsrec_key_material *) malloc(sizeof(*host) * count);
+        if (!host) return TLSREC_ERR_SSL_ALLOC_FAILED;
+        if (hipMemcpyAsync(host, keys, sizeof(*host) * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            free(host);
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
+    }
+    const tlsrec_key_material *hk = keys_on_device ? host : keys;
+    for (uint32_t i = 0; i < count; i++) {
+        int r = check_material(&hk[i]);
+        if (r) {
+            free(host);
+            return r;
+        }
+    }
+    for (uint32_t i = 0; i < count; i++) {
+        kt->h_cipher[first + i] = hk[i].cipher;
+        kt->cipher_mask |= 1u << hk[i].cipher;
+    }
+    free(host);
+    const tlsrec_key_material *src = keys;
+    if (!keys_on_device) {
+        if (hipMemcpyAsync(kt->d_stage + first, keys, sizeof(*keys) * count, hipMemcpyHostToDevice, st) != hipSuccess)
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        /* the staging copy must land before the host buffer may be reused */
+        if (hipStreamSynchronize(st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        src = kt->d_stage + first;
+    }
+    return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, src, first, count, st));
+}
+
+static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t target_wgs)
+{
+    uint64_t want = (n + (uint64_t) waves_per_wg * target_wgs - 1) / ((uint64_t) waves_per_wg * target_wgs);
+    if (want < R) want = R;
+    want = (want + R - 1) / R * R;
+    if (want > 64) want = 64;
+    return (uint32_t) want;
+}
+
+static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
+                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec)
+{
+    if (!kt || (!recs && n) || (!res && n)) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t) stream;
+    int cu = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, kt->device) == hipSuccess && prop.multiProcessorCount > 0)
+            cu = prop.multiProcessorCount;
+    }
+    for (int cipher = TLSREC_CIPHER_AES_128_GCM; cipher <= TLSREC_CIPHER_AES_256_GCM; cipher++) {
+        if (!(kt->cipher_mask & (1u << cipher))) continue;
+        int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes : 8;
+        GcmArgs a;
+        a.slots = kt->d_slots;
+        a.ghtab = kt->d_ghtab;
+        a.recs = recs;
+        a.res = res;
+        a.n = n;
+        a.in = in;
+        a.out = out;
+        a.rpw = pick_rpw(n, GCM_WAVES, 64 / L, (uint32_t) cu);
+        a.capacity = kt->capacity;
+        a.cipher = (uint32_t) cipher;
+        uint64_t per_wg = (uint64_t) GCM_WAVES * a.rpw;
+        uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
+        int nr = cipher == TLSREC_CIPHER_AES_128_GCM ? 10 : 14;
+        if (tlsrec__launch_gcm(&a, dec, L, nr, grid, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305)) {
+        int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;
+        CpArgs a;
+        a.slots = kt->d_slots;
+        a.recs = recs;
+        a.res = res;
+        a.n = n;
+        a.in = in;
+        a.out = out;
+        a.rpw = pick_rpw(n, CP_WAVES, 64 / L, (uint32_t) cu * 4);
+        a.capacity = kt->capacity;
+        uint64_t per_wg = (uint64_t) CP_WAVES * a.rpw;
+        uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
+        if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    return 0;
+}
+
+extern "C" int tlsrec_batch_encrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                    uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
+                                    uint32_t lanes_per_record, void *stream)
+{
+    return batch(kt, recs, res, n, in_arena, out_arena, lanes_per_record, stream, 0);
+}
+
+extern "C" int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                    uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
+                                    uint32_t lanes_per_record, void *stream)
+{
+    return batch(kt, recs, res, n, in_arena, out_arena, lanes_per_record, stream, 1);
+}
+
+/* ======================================================================
+ * Engine used by the single-record API (tlsrec_host.c): a process-wide key
+ * table with a slot allocator and a device staging area.
+ * ==================================================================== */
+#define TLSREC_ENGINE_SLOTS 4096
+
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static tlsrec_keytab *g_kt = NULL;
+static uint8_t g_used[TLSREC_ENGINE_SLOTS];
+static hipStream_t g_stream = NULL;
+static uint8_t *g_dbuf = NULL;
+static size_t g_dbuf_len = 0;
+static void *g_dmeta = NULL;
+
+static int engine_init_locked(void)
+{
+    if (g_kt) return 0;
+    int r = tlsrec_keytab_create(&g_kt, TLSREC_ENGINE_SLOTS);
+    if (r) return r;
+    if (hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&g_dmeta, 64) != hipSuccess) {
+        tlsrec_keytab_free(g_kt);
+        g_kt = NULL;
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    return 0;
+}
+
+extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
+{
+    pthread_mutex_lock(&g_mu);
+    int r = engine_init_locked();
+    int slot = -1;
+    if (r == 0) {
+        for (int i = 0; i < TLSREC_ENGINE_SLOTS; i++)
+            if (!g_used[i]) { slot = i; break; }
+        if (slot < 0) r = TLSREC_ERR_SSL_ALLOC_FAILED;
+    }
+    if (r == 0) {
+        r = tlsrec_keytab_load(g_kt, (uint32_t) slot, 1, km, 0, g_stream);
+        if (r == 0 && hipStreamSynchronize(g_stream) != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) g_used[slot] = 1;
+    }
+    pthread_mutex_unlock(&g_mu);
+    return r ? r : slot;
+}
+
+extern "C" void tlsrec__engine_slot_free(int slot)
+{
+    if (slot < 0 || slot >= TLSREC_ENGINE_SLOTS) return;
+    pthread_mutex_lock(&g_mu);
+    if (g_kt && g_used[slot]) {
+        hipMemsetAsync(g_kt->d_slots + slot, 0, sizeof(SlotState), g_stream);
+        hipMemsetAsync(g_kt->d_ghtab + (size_t) slot * KEY_TABLE_WORDS, 0, sizeof(uint4) * KEY_TABLE_WORDS,
+                       g_stream);
+        hipStreamSynchronize(g_stream);
+        g_used[slot] = 0;
+    }
+    pthread_mutex_unlock(&g_mu);
+}
+
+/* Run one record through the batch kernels: host buffer -> device -> host. */
+extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
+                                  tlsrec_batch_res *out)
+{
+    pthread_mutex_lock(&g_mu);
+    int r = engine_init_locked();
+    if (r == 0 && g_dbuf_len < buf_len + 16) {
+        hipFree(g_dbuf);
+        g_dbuf = NULL;
+        g_dbuf_len = 0;
+        size_t want = buf_len + 16 > 65536 ? buf_len + 16 : 65536;
+        if (hipMalloc((void **) &g_dbuf, want) != hipSuccess) r = TLSREC_ERR_SSL_ALLOC_FAILED;
+        else g_dbuf_len = want;
+    }
+    if (r == 0) {
+        tlsrec_batch_rec d = *rec;
+        d.buf_off = 0;
+        tlsrec_batch_rec *d_rec = (tlsrec_batch_rec *) g_dmeta;
+        tlsrec_batch_res *d_res = (tlsrec_batch_res *) ((uint8_t *) g_dmeta + 48);
+        hipError_t e = hipSuccess;
+        if (buf_len) e = hipMemcpyAsync(g_dbuf, buf, buf_len, hipMemcpyHostToDevice, g_stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_rec, &d, sizeof(d), hipMemcpyHostToDevice, g_stream);
+        if (e == hipSuccess) {
+            r = batch(g_kt, d_rec, d_res, 1, g_dbuf, g_dbuf, 0, g_stream, dec);
+            if (r == 0 && buf_len) e = hipMemcpyAsync(buf, g_dbuf, buf_len, hipMemcpyDeviceToHost, g_stream);
+            if (r == 0 && e == hipSuccess) e = hipMemcpyAsync(out, d_res, sizeof(*out), hipMemcpyDeviceToHost, g_stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
+        }
+        if (e != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}

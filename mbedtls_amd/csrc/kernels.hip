@@ -1,0 +1,767 @@
+/*
+ * kernels.hip -- gfx950 kernels of the TLS record engine.
+ *
+ *   tlsrec_keysetup_kernel   per key slot: AES key schedule, H = E_K(0),
+ *                            H^(2^i) and their GHASH position tables.
+ *   tlsrec_gcm_kernel        AES-128/256-GCM record protect / unprotect,
+ *                            the psa_aead_encrypt/decrypt calls of
+ *                            ssl_msg.c:1043 and :1412 fused with the record
+ *                            framing around them.
+ *   tlsrec_chachapoly_kernel ChaCha20-Poly1305 likewise.
+ *
+ * Work decomposition: a wavefront owns a chunk of up to 64
+ * records.  A pre-pass gives each lane one record's one-off block (E_K(J0)
+ * for GCM, the Poly1305 key block for ChaCha20-Poly1305).  Then L lanes
+ * (L = 8 for GCM: 8 x 16 B = one 128-B line per record per step) walk one
+ * record; GHASH / Poly1305 are evaluated as L interleaved Horner chains with
+ * a uniform multiplier H^L / r^(4L), combined at the end by a log2(L) tree.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tlsrec.h"
+#include "tlsrec_device.h"
+#include "tlsrec_frame.h"
+#include "tlsrec_internal.h"
+
+namespace tlsrec {
+
+/* ======================================================================
+ * Key setup
+ * ==================================================================== */
+__device__ inline void aes_key_expand(const uint8_t *key, int nk, uint32_t *rk)
+{
+    const int nr = nk + 6, total = 4 * (nr + 1);
+    for (int i = 0; i < nk; i++) {
+        rk[i] = (uint32_t) key[4 * i] | ((uint32_t) key[4 * i + 1] << 8) |
+                ((uint32_t) key[4 * i + 2] << 16) | ((uint32_t) key[4 * i + 3] << 24);
+    }
+    uint32_t rcon = 1;
+    for (int i = nk; i < total; i++) {
+        uint32_t t = rk[i - 1];
+        if (i % nk == 0) {
+            t = (t >> 8) | (t << 24);
+            t = (uint32_t) kSbox.v[t & 0xff] | ((uint32_t) kSbox.v[(t >> 8) & 0xff] << 8) |
+                ((uint32_t) kSbox.v[(t >> 16) & 0xff] << 16) | ((uint32_t) kSbox.v[t >> 24] << 24);
+            t ^= rcon;
+            rcon = xtime8(rcon);
+        } else if (nk > 6 && i % nk == 4) {
+            t = (uint32_t) kSbox.v[t & 0xff] | ((uint32_t) kSbox.v[(t >> 8) & 0xff] << 8) |
+                ((uint32_t) kSbox.v[(t >> 16) & 0xff] << 16) | ((uint32_t) kSbox.v[t >> 24] << 24);
+        }
+        rk[i] = rk[i - nk] ^ t;
+    }
+}
+
+/* byte-oriented AES (one lane; only used for H = E_K(0^128)) */
+__device__ inline void aes_encrypt_bytes(const uint32_t *rk, int nr, uint8_t st[16])
+{
+    for (int i = 0; i < 16; i++) st[i] ^= (uint8_t) (rk[i / 4] >> (8 * (i % 4)));
+    for (int r = 1; r <= nr; r++) {
+        uint8_t t[16];
+        for (int c = 0; c < 4; c++)
+            for (int row = 0; row < 4; row++) t[4 * c + row] = kSbox.v[st[4 * ((c + row) & 3) + row]];
+        if (r != nr) {
+            for (int c = 0; c < 4; c++) {
+                uint32_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+                uint32_t all = a0 ^ a1 ^ a2 ^ a3;
+                t[4 * c + 0] = (uint8_t) (a0 ^ all ^ xtime8(a0 ^ a1));
+                t[4 * c + 1] = (uint8_t) (a1 ^ all ^ xtime8(a1 ^ a2));
+                t[4 * c + 2] = (uint8_t) (a2 ^ all ^ xtime8(a2 ^ a3));
+                t[4 * c + 3] = (uint8_t) (a3 ^ all ^ xtime8(a3 ^ a0));
+            }
+        }
+        for (int i = 0; i < 16; i++) st[i] = t[i] ^ (uint8_t) (rk[4 * r + i / 4] >> (8 * (i % 4)));
+    }
+}
+
+/* One 256-thread workgroup per slot. */
+__global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab,
+                                                             const tlsrec_key_material *keys,
+                                                             uint32_t first, uint32_t count)
+{
+    __shared__ G128 pw[KEY_TABLES];
+    __shared__ uint4 base[KEY_TABLES][128];
+    const uint32_t slot = first + blockIdx.x;
+    if (blockIdx.x >= count) return;
+    SlotState *st = &slots[slot];
+    const tlsrec_key_material km = keys[blockIdx.x];
+    const int tid = threadIdx.x;
+    const bool gcm = km.cipher == TLSREC_CIPHER_AES_128_GCM || km.cipher == TLSREC_CIPHER_AES_256_GCM;
+    if (tid == 0) {
+        st->km = km;
+        st->nr = 0;
+        if (gcm) {
+            const int nk = km.cipher == TLSREC_CIPHER_AES_128_GCM ? 4 : 8;
+            aes_key_expand(km.key, nk, st->rk);
+            st->nr = (uint32_t) (nk + 6);
+            uint8_t h[16] = { 0 };
+            aes_encrypt_bytes(st->rk, nk + 6, h);
+            G128 H;
+            H.hi = 0; H.lo = 0;
+            for (int i = 0; i < 8; i++) { H.hi = (H.hi << 8) | h[i]; H.lo = (H.lo << 8) | h[8 + i]; }
+            for (int i = 0; i < 16; i++) st->h[i] = h[i];
+            pw[0] = H;
+            for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);
+        }
+    }
+    __syncthreads();
+    if (!gcm) return;
+    /* base[p][j] = H^(2^p) * x^j */
+    if (tid < KEY_TABLES) {
+        G128 v = pw[tid];
+        for (int j = 0; j < 128; j++) {
+            base[tid][j] = g_to_words(v);
+            v = g_shr1(v);
+        }
+    }
+    __syncthreads();
+    uint4 *out = ghtab + (size_t) slot * KEY_TABLE_WORDS;
+    for (int e = tid; e < KEY_TABLES * 32 * 16; e += 256) {
+        const int p = e >> 9, k = (e >> 4) & 31, nib = e & 15;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 4; i++)
+            if ((nib >> (3 - i)) & 1) acc = xor4(acc, base[p][4 * k + i]);
+        out[e] = acc;
+    }
+}
+
+/* ======================================================================
+ * Shared record helpers
+ * ==================================================================== */
+__device__ __forceinline__ uint32_t ld_u32le(const uint8_t *p)
+{
+    return (uint32_t) p[0] | ((uint32_t) p[1] << 8) | ((uint32_t) p[2] << 16) | ((uint32_t) p[3] << 24);
+}
+
+/* Load up to 16 bytes of an inner plaintext / ciphertext block.  `pos` is the
+ * offset of the block within the AEAD region [0, aead_len); bytes at
+ * [content_len, aead_len) are the TLS 1.3 inner type byte and zero padding
+ * (ssl_msg.c:466-491), bytes >= aead_len are zero. */
+__device__ __forceinline__ uint4 load_block(const uint8_t *src, uint32_t pos, uint32_t content_len,
+                                            uint32_t aead_len, uint8_t inner_type, bool aligned)
+{
+    if (aligned && pos + 16 <= content_len) return *reinterpret_cast<const uint4 *>(src + pos);
+    uint32_t w[4] = { 0, 0, 0, 0 };
+    for (int i = 0; i < 16; i++) {
+        uint32_t b = pos + i, v = 0;
+        if (b < content_len) v = src[b];
+        else if (b == content_len && b < aead_len) v = inner_type;
+        w[i >> 2] |= v << (8 * (i & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_block(uint8_t *dst, uint32_t pos, uint32_t len, uint4 v, bool aligned)
+{
+    if (aligned && pos + 16 <= len) {
+        *reinterpret_cast<uint4 *>(dst + pos) = v;
+        return;
+    }
+    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+    for (int i = 0; i < 16; i++)
+        if (pos + i < len) dst[pos + i] = (uint8_t) (w[i >> 2] >> (8 * (i & 3)));
+}
+
+/* zero the bytes of a block at or beyond `len` */
+__device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t pos, uint32_t len)
+{
+    if (pos + 16 <= len) return v;
+    uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int32_t valid = (int32_t) len - (int32_t) (pos + 4 * i);
+        uint32_t m = valid >= 4 ? 0xffffffffu : (valid <= 0 ? 0u : (0xffffffffu >> (8 * (4 - valid))));
+        w[i] &= m;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+/* (index+1) << 8 | value of the last non-zero byte of a block, or 0 */
+__device__ __forceinline__ uint32_t last_nonzero_key(uint4 v, uint32_t pos)
+{
+    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+    uint32_t key = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        if (w[d] != 0) {
+            uint32_t e = (31 - __builtin_clz(w[d])) >> 3;
+            key = ((pos + 4 * d + e + 1) << 8) | ((w[d] >> (8 * e)) & 0xff);
+        }
+    }
+    return key;
+}
+
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src)
+{
+    return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t) __shfl_xor(v, o));
+    return v;
+}
+
+template <int L>
+__device__ __forceinline__ uint32_t group_max(uint32_t v)
+{
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) v = max(v, (uint32_t) __shfl_xor(v, o));
+    return v;
+}
+
+__device__ __forceinline__ void zero_range(uint8_t *dst, uint32_t from, uint32_t to, int q, int L)
+{
+    for (uint32_t i = from + (uint32_t) q; i < to; i += (uint32_t) L) dst[i] = 0;
+}
+
+__device__ __forceinline__ tlsrec_plan_key plan_key(const tlsrec_key_material &km)
+{
+    tlsrec_plan_key k;
+    k.tls13 = km.tls_minor == 4;
+    k.fixed_ivlen = km.fixed_ivlen;
+    k.taglen = km.taglen;
+    k.iv = km.iv;
+    return k;
+}
+
+template <bool DEC>
+__device__ __forceinline__ void make_plan(tlsrec_plan &p, const tlsrec_batch_rec &d, const tlsrec_key_material &km)
+{
+    tlsrec_plan_key k = plan_key(km);
+    if (DEC)
+        tlsrec_plan_decrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len);
+    else
+        tlsrec_plan_encrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len,
+                            km.granularity ? km.granularity : TLSREC_PADDING_GRANULARITY);
+}
+
+/* Record whose plan stopped before the AEAD: status + pre-AEAD side effects. */
+__device__ inline void finish_early(const tlsrec_plan &p, const tlsrec_batch_rec &d, uint8_t *out,
+                                    tlsrec_batch_res *res)
+{
+    if (p.side_type) {
+        uint8_t *b = out + d.buf_off + p.side_pos;
+        b[0] = d.type;
+        for (uint32_t i = 0; i < p.side_zeros; i++) b[1 + i] = 0;
+    }
+    tlsrec_batch_res r;
+    r.status = p.status;
+    r.data_offset = p.data_offset;
+    r.data_len = p.data_len;
+    r.type = p.type;
+    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+    *res = r;
+}
+
+template <bool DEC>
+__device__ __forceinline__ void nonce_words(const tlsrec_plan &p, const tlsrec_batch_rec &d, const uint8_t *in,
+                                            uint32_t nw[3])
+{
+    uint8_t nonce[12];
+    for (int i = 0; i < 12; i++) nonce[i] = p.nonce[i];
+    if (DEC && p.explicit_iv) {   /* encrypt uses rec->ctr (ssl_msg.c:1012-1019) */
+        const uint8_t *e = in + d.buf_off + d.data_offset;   /* ssl_msg.c:1360 dynamic_iv = data */
+        for (int i = 0; i < 8; i++) nonce[4 + i] = e[i];
+    }
+    nw[0] = ld_u32le(nonce);
+    nw[1] = ld_u32le(nonce + 4);
+    nw[2] = ld_u32le(nonce + 8);
+}
+
+__device__ __forceinline__ uint4 aad_words(const tlsrec_plan &p)
+{
+    uint32_t w[4];
+    for (int i = 0; i < 4; i++) w[i] = ld_u32le(p.aad + 4 * i);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+/* ======================================================================
+ * AES-GCM
+ * ==================================================================== */
+template <int L> struct Log2;
+template <> struct Log2<1> { static constexpr int v = 0; };
+template <> struct Log2<2> { static constexpr int v = 1; };
+template <> struct Log2<4> { static constexpr int v = 2; };
+template <> struct Log2<8> { static constexpr int v = 3; };
+template <> struct Log2<16> { static constexpr int v = 4; };
+template <> struct Log2<32> { static constexpr int v = 5; };
+template <> struct Log2<64> { static constexpr int v = 6; };
+
+template <int L>
+struct GcmLds {
+    static constexpr int NT = Log2<L>::v + 1;           /* GHASH tables H^1 .. H^L */
+    static constexpr int GH = 0;
+    static constexpr int AES = NT * 8192;               /* T0/T1 x 32 copies */
+    static constexpr int EJ0 = AES + 65536;             /* 16 waves x 64 x 16 B */
+    static constexpr int RK = EJ0 + GCM_WAVES * 64 * 16;/* 60 round-key words */
+    static constexpr int CTL = RK + 256;
+    static constexpr int BYTES = CTL + 16;
+};
+
+template <int PI>
+__device__ __forceinline__ uint4 gmul_rt(const uint8_t *lds, uint4 y, int pi)
+{
+    /* runtime table selector for the tree: unrolled on PI */
+    if (pi == PI) return gmul<PI>(lds, y);
+    if constexpr (PI > 0) return gmul_rt<PI - 1>(lds, y, pi);
+    return y;
+}
+
+template <int L, int NR, bool DEC>
+__global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
+{
+    using LY = GcmLds<L>;
+    constexpr int LOGL = Log2<L>::v;
+    constexpr int R = 64 / L;
+    /* the kernel's only LDS object, so it starts at LDS address 0 and every
+     * table offset folds into the ds_read immediate */
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LY::BYTES];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g = lane / L, q = lane % L;
+    const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + LY::CTL);
+
+    aes_fill_tables(lds + LY::AES, tid, GCM_THREADS);
+
+    const uint64_t chunk = ((uint64_t) blockIdx.x * GCM_WAVES + wave) * a.rpw;
+    /* pass membership: lane l tracks record chunk + l of the pre-pass */
+    uint32_t my_slot = 0xffffffffu;
+    {
+        uint64_t r = chunk + (uint64_t) lane;
+        if (lane < (int) a.rpw && r < a.n) {
+            uint32_t s = a.recs[r].slot;
+            if (s < a.capacity && a.slots[s].km.cipher == a.cipher) my_slot = s;
+        }
+    }
+    if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
+    __syncthreads();
+
+    for (int iter = 0;; iter++) {
+        uint32_t *cur = &ctl[iter & 1];
+        if (my_slot != 0xffffffffu) atomicMin(cur, my_slot);
+        __syncthreads();
+        const uint32_t s = __builtin_amdgcn_readfirstlane(*cur);
+        if (s == 0xffffffffu) break;
+        if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
+        /* stage the slot's GHASH tables and round keys */
+        {
+            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
+            uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
+            for (int i = tid; i < LY::NT * 512; i += GCM_THREADS) dst[i] = src[i];
+            uint32_t *rkd = reinterpret_cast<uint32_t *>(lds + LY::RK);
+            if (tid < 60) rkd[tid] = a.slots[s].rk[tid];
+        }
+        __syncthreads();
+        const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LY::RK);
+        const tlsrec_key_material km = a.slots[s].km;
+
+        /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
+        {
+            uint4 ej0 = make_uint4(0, 0, 0, 0);
+            bool mine = my_slot == s;
+            uint32_t nw[3] = { 0, 0, 0 };
+            if (mine) {
+                const tlsrec_batch_rec d = a.recs[chunk + lane];
+                tlsrec_plan p;
+                make_plan<DEC>(p, d, km);
+                nonce_words<DEC>(p, d, a.in, nw);
+            }
+            ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+            reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
+        }
+        /* lanes of this wave read other lanes' E(J0): the wave's own LDS
+         * writes complete before its later reads (in-order LDS queue). */
+
+        /* ---- record rounds: L lanes per record, R records per wave ---- */
+        for (uint32_t rr = 0; rr < a.rpw; rr += R) {
+            const uint32_t slot_in_chunk = rr + (uint32_t) g;
+            const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
+            const bool active = slot_in_chunk < a.rpw && owner_slot == s;
+            const uint64_t ridx = chunk + slot_in_chunk;
+            tlsrec_batch_rec d;
+            tlsrec_plan p;
+            bool run = false;
+            if (active) {
+                d = a.recs[ridx];
+                make_plan<DEC>(p, d, km);
+                if (p.status != 0) {
+                    if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
+                } else {
+                    run = true;
+                }
+            }
+            const uint32_t aead_len = run ? p.aead_len : 0;
+            const uint32_t m = (aead_len + 15) >> 4;                 /* GHASH C blocks */
+            const uint32_t mm = m ? m : 1;
+            const uint32_t z = (L - mm % L) % L;
+            const uint32_t J = run ? (mm + z) / L : 0;
+            const uint32_t Jmax = wave_max(J);
+            uint32_t nw[3] = { 0, 0, 0 };
+            uint4 aadw = make_uint4(0, 0, 0, 0);
+            const uint8_t *src = a.in;
+            uint8_t *dst = a.out;
+            bool aligned = false;
+            uint32_t content_len = 0;
+            if (run) {
+                nonce_words<DEC>(p, d, a.in, nw);
+                aadw = aad_words(p);
+                src = a.in + d.buf_off + p.aead_pos;
+                dst = a.out + d.buf_off + p.aead_pos;
+                aligned = ((((uintptr_t) src) | ((uintptr_t) dst)) & 15) == 0;
+                content_len = DEC ? aead_len : p.content_len;
+            }
+            uint4 Y = (run && m > 0 && (uint32_t) q == z) ? aadw : make_uint4(0, 0, 0, 0);
+            uint32_t nzkey = 0;
+            for (uint32_t j = 0; j < Jmax; j++) {
+                const int32_t c = (int32_t) (L * j + q) - (int32_t) z;
+                const bool live = run && j < J;
+                const bool valid = live && c >= 0 && (uint32_t) c < m;
+                const uint32_t ctr = (uint32_t) c + 2u;
+                uint4 ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(ctr)));
+                uint4 X = make_uint4(0, 0, 0, 0);
+                if (valid) {
+                    const uint32_t pos = (uint32_t) c * 16;
+                    uint4 blk = load_block(src, pos, content_len, aead_len, p.inner_type, aligned);
+                    uint4 o = mask_block(xor4(blk, ks), pos, aead_len);
+                    store_block(dst, pos, aead_len, o, aligned);
+                    X = DEC ? blk : o;
+                    if (DEC && p.tls13) {
+                        uint32_t k = last_nonzero_key(o, pos);
+                        if (k) nzkey = k;
+                    }
+                }
+                if (live && m == 0 && c == 0) X = aadw;
+                uint4 Yn = (j == 0) ? gmul<0>(lds, Y) : gmul<LOGL>(lds, Y);
+                Yn = xor4(Yn, X);
+                if (live) Y = Yn;
+            }
+            /* tree: sum_q Y_q H^(L-q) */
+#pragma unroll
+            for (int sh = L / 2; sh >= 1; sh >>= 1) {
+                uint4 o = shfl4(Y, (lane + sh) & 63);
+                Y = xor4(gmul_rt<LOGL>(lds, Y, Log2<1>::v + __builtin_ctz(sh)), o);
+            }
+            Y = gmul<0>(lds, Y);                                     /* T */
+            const uint32_t alen = run ? p.aad_len : 0;
+            uint4 lenw = make_uint4(0, bswap32(alen * 8), 0, bswap32(aead_len * 8));
+            Y = gmul<0>(lds, xor4(Y, lenw));                         /* GHASH */
+            if (!run) continue;
+            const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
+            const uint4 tag = xor4(Y, ej0);
+            if (!DEC) {
+                if (q == 0) {
+                    store_block(dst, aead_len, aead_len + 16, tag, false);
+                    if (p.explicit_iv && p.post_status == 0) {
+                        uint8_t *e = a.out + d.buf_off + p.data_offset;
+                        for (int i = 0; i < 8; i++) e[i] = d.ctr[i];
+                    }
+                    tlsrec_batch_res r;
+                    r.status = p.post_status;
+                    r.data_offset = p.data_offset;
+                    r.data_len = p.data_len;
+                    r.type = p.type;
+                    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+                    a.res[ridx] = r;
+                }
+            } else {
+                uint4 want = load_block(src, aead_len, aead_len + 16, aead_len + 16, 0, false);
+                uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
+                diff = __shfl(diff, lane - q);                        /* group leader's verdict */
+                uint32_t key = group_max<L>(nzkey);
+                tlsrec_batch_res r;
+                r.data_offset = p.data_offset;
+                r.data_len = p.data_len;
+                r.type = d.type;
+                r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+                if (diff != 0) {
+                    /* PSA wipes the whole output buffer on a bad tag */
+                    zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
+                    r.status = TLSREC_E_INVALID_MAC;
+                } else if (p.tls13) {                                /* ssl_msg.c:1809-1818 */
+                    if (key == 0) {
+                        r.status = TLSREC_E_INVALID_RECORD;
+                    } else {
+                        r.status = 0;
+                        r.data_len = (key >> 8) - 1;
+                        r.type = (uint8_t) (key & 0xff);
+                    }
+                } else {
+                    r.status = 0;
+                }
+                if (q == 0) a.res[ridx] = r;
+            }
+        }
+        my_slot = (my_slot == s) ? 0xffffffffu : my_slot;
+    }
+}
+
+/* ======================================================================
+ * ChaCha20-Poly1305
+ * ==================================================================== */
+__device__ __forceinline__ P5 p_from_words(uint4 w)
+{
+    P5 r;
+    r.v[0] = w.x & TLSREC_M26;
+    r.v[1] = ((w.x >> 26) | (w.y << 6)) & TLSREC_M26;
+    r.v[2] = ((w.y >> 20) | (w.z << 12)) & TLSREC_M26;
+    r.v[3] = ((w.z >> 14) | (w.w << 18)) & TLSREC_M26;
+    r.v[4] = (w.w >> 8) | (1u << 24);
+    return r;
+}
+
+template <int L>
+__device__ __forceinline__ P5 shfl_p5(P5 v, int src)
+{
+    P5 r;
+#pragma unroll
+    for (int i = 0; i < 5; i++) r.v[i] = __shfl(v.v[i], src);
+    return r;
+}
+
+template <int L, bool DEC>
+__global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
+{
+    constexpr int R = 64 / L;
+    __shared__ uint32_t polykey[CP_WAVES][64][8];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g = lane / L, q = lane % L;
+    const uint64_t chunk = ((uint64_t) blockIdx.x * CP_WAVES + wave) * a.rpw;
+
+    /* ---- pre-pass: one-time Poly1305 key (ChaCha20 block 0, RFC 8439 2.6) ---- */
+    bool mine = false;
+    {
+        uint64_t r = chunk + (uint64_t) lane;
+        uint32_t key[8] = { 0 }, nw[3] = { 0, 0, 0 };
+        if (lane < (int) a.rpw && r < a.n) {
+            const tlsrec_batch_rec d = a.recs[r];
+            if (d.slot < a.capacity && a.slots[d.slot].km.cipher == TLSREC_CIPHER_CHACHA20_POLY1305) {
+                mine = true;
+                const tlsrec_key_material km = a.slots[d.slot].km;
+                tlsrec_plan p;
+                make_plan<DEC>(p, d, km);
+                nonce_words<DEC>(p, d, a.in, nw);
+                for (int i = 0; i < 8; i++) key[i] = ld_u32le(km.key + 4 * i);
+            }
+        }
+        uint32_t blk[16];
+        chacha_block(key, 0, nw, blk);
+        for (int i = 0; i < 8; i++) polykey[wave][lane][i] = blk[i];
+    }
+
+    for (uint32_t rr = 0; rr < a.rpw; rr += R) {
+        const uint32_t slot_in_chunk = rr + (uint32_t) g;
+        const bool owner_mine = __shfl((int) mine, (int) slot_in_chunk & 63) != 0;
+        const bool active = slot_in_chunk < a.rpw && owner_mine;
+        const uint64_t ridx = chunk + slot_in_chunk;
+        tlsrec_batch_rec d;
+        tlsrec_plan p;
+        tlsrec_key_material km;
+        bool run = false;
+        if (active) {
+            d = a.recs[ridx];
+            km = a.slots[d.slot].km;
+            make_plan<DEC>(p, d, km);
+            if (p.status != 0) {
+                if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
+            } else {
+                run = true;
+            }
+        }
+        const uint32_t aead_len = run ? p.aead_len : 0;
+        const uint32_t B = (aead_len + 63) >> 6;              /* ChaCha20 chunks */
+        const uint32_t M = (aead_len + 15) >> 4;              /* Poly1305 C blocks */
+        const uint32_t v = B ? M - 4 * (B - 1) : 0;
+        const uint32_t z = (L - B % L) % L;
+        const uint32_t J = run ? (B + z) / L : 0;
+        const uint32_t Jmax = wave_max(J);
+        uint32_t key[8] = { 0 }, nw[3] = { 0, 0, 0 };
+        uint4 aadw = make_uint4(0, 0, 0, 0);
+        const uint8_t *src = a.in;
+        uint8_t *dst = a.out;
+        bool aligned = false;
+        uint32_t content_len = 0;
+        if (run) {
+            for (int i = 0; i < 8; i++) key[i] = ld_u32le(km.key + 4 * i);
+            nonce_words<DEC>(p, d, a.in, nw);
+            aadw = aad_words(p);
+            src = a.in + d.buf_off + p.aead_pos;
+            dst = a.out + d.buf_off + p.aead_pos;
+            aligned = ((((uintptr_t) src) | ((uintptr_t) dst)) & 15) == 0;
+            content_len = DEC ? aead_len : p.content_len;
+        }
+        const uint32_t *pk = polykey[wave][slot_in_chunk & 63];
+        const P5 r1 = p_from_r(pk[0], pk[1], pk[2], pk[3]);
+        const uint4 sw = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+        const P5 r2 = p_mul(r1, r1);
+        const P5 r3 = p_mul(r2, r1);
+        const P5 r4 = p_mul(r2, r2);
+        P5 rpow[Log2<L>::v + 1];                                /* r^(4*2^i), i = 0..log2 L */
+        rpow[0] = r4;
+#pragma unroll
+        for (int i = 1; i <= Log2<L>::v; i++) rpow[i] = p_mul(rpow[i - 1], rpow[i - 1]);
+        const P5 aadr = p_mul(p_from_words(aadw), r1);          /* AAD folded before C_0 */
+
+        P5 acc = p_zero(), vf = p_zero();
+        uint32_t nzkey = 0;
+        for (uint32_t j = 0; j < Jmax; j++) {
+            const int32_t b = (int32_t) (L * j + q) - (int32_t) z;
+            const bool live = run && j < J;
+            const bool valid = live && b >= 0 && (uint32_t) b < B;
+            uint32_t ks[16];
+            chacha_block(key, (uint32_t) b + 1u, nw, ks);
+            uint4 ct[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) ct[t] = make_uint4(0, 0, 0, 0);
+            if (valid) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const uint32_t pos = (uint32_t) b * 64 + 16 * t;
+                    if (pos < aead_len) {
+                        uint4 blk = load_block(src, pos, content_len, aead_len, p.inner_type, aligned);
+                        uint4 o = mask_block(xor4(blk, make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3])),
+                                             pos, aead_len);
+                        store_block(dst, pos, aead_len, o, aligned);
+                        ct[t] = DEC ? blk : o;
+                        if (DEC && p.tls13) {
+                            uint32_t k = last_nonzero_key(o, pos);
+                            if (k) nzkey = k;
+                        }
+                    }
+                }
+            }
+            /* Horner over this chunk's Poly1305 blocks */
+            const uint32_t vv = (valid && (uint32_t) b == B - 1) ? v : 4;
+            P5 x = p_from_words(ct[0]);
+            x = p_sel(b == 0, p_add(x, aadr), x);
+#pragma unroll
+            for (int t = 1; t < 4; t++) {
+                P5 y = p_add(p_mul(x, r1), p_from_words(ct[t]));
+                x = p_sel((uint32_t) t < vv, y, x);
+            }
+            const bool is_final = valid && (uint32_t) b == B - 1;
+            if (is_final) vf = x;
+            P5 an = (j == 0) ? p_zero() : p_mul(acc, rpow[Log2<L>::v]);
+            an = p_add(an, (valid && !is_final) ? x : p_zero());
+            if (live && !is_final) acc = an;
+        }
+        if (run && B == 0 && q == L - 1) vf = p_from_words(aadw);
+        /* rotated tree: logical ql = (q+1) % L, anchored at chunk B-2 */
+        const int ql = (q + 1) % L;
+#pragma unroll
+        for (int i = Log2<L>::v - 1; i >= 0; i--) {
+            const int sh = 1 << i;
+            const int src_lane = (lane - q) + ((ql + sh + L - 1) % L);
+            P5 o = shfl_p5<L>(acc, src_lane);
+            P5 t = p_add(p_mul(acc, rpow[i]), o);
+            acc = p_carry(t);
+        }
+        /* in lane L-1: poly = r * (r * (vf + r^(4-delta) * W) + LEN) */
+        const uint32_t delta = 4 - v;
+        P5 rd = delta == 0 ? r4 : (delta == 1 ? r3 : (delta == 2 ? r2 : r1));
+        P5 X = p_add(p_mul(acc, rd), vf);
+        X = p_mul(p_carry(X), r1);
+        const uint32_t alen = run ? p.aad_len : 0;
+        X = p_add(X, p_from_words(make_uint4(alen, 0, aead_len, 0)));
+        X = p_mul(p_carry(X), r1);
+        const uint4 tag = p_finish(X, sw);
+        if (!run) continue;
+        const int leader = lane - q + (L - 1);
+        if (!DEC) {
+            if (q == L - 1) {
+                store_block(dst, aead_len, aead_len + 16, tag, false);
+                tlsrec_batch_res r;
+                r.status = p.post_status;
+                r.data_offset = p.data_offset;
+                r.data_len = p.data_len;
+                r.type = p.type;
+                r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+                a.res[ridx] = r;
+            }
+        } else {
+            uint4 want = load_block(src, aead_len, aead_len + 16, aead_len + 16, 0, false);
+            uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
+            diff = __shfl(diff, leader);
+            uint32_t key2 = group_max<L>(nzkey);
+            tlsrec_batch_res r;
+            r.data_offset = p.data_offset;
+            r.data_len = p.data_len;
+            r.type = d.type;
+            r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+            if (diff != 0) {
+                zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
+                r.status = TLSREC_E_INVALID_MAC;
+            } else if (p.tls13) {
+                if (key2 == 0) {
+                    r.status = TLSREC_E_INVALID_RECORD;
+                } else {
+                    r.status = 0;
+                    r.data_len = (key2 >> 8) - 1;
+                    r.type = (uint8_t) (key2 & 0xff);
+                }
+            } else {
+                r.status = 0;
+            }
+            if (q == L - 1) a.res[ridx] = r;
+        }
+    }
+}
+
+/* ======================================================================
+ * Launchers
+ * ==================================================================== */
+template <int L, int NR, bool DEC>
+static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC>), dim3(grid), dim3(GCM_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int L, bool DEC>
+static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, uint32_t grid, hipStream_t st)
+{
+    return nr == 10 ? launch_gcm_t<L, 10, DEC>(a, grid, st) : launch_gcm_t<L, 14, DEC>(a, grid, st);
+}
+
+template <int L, bool DEC>
+static hipError_t launch_cp_t(const CpArgs &a, uint32_t grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((tlsrec_chachapoly_kernel<L, DEC>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+} /* namespace tlsrec */
+
+using namespace tlsrec;
+
+extern "C" hipError_t tlsrec__launch_keysetup(SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
+                                              uint32_t first, uint32_t count, hipStream_t st)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(tlsrec_keysetup_kernel, dim3(count), dim3(256), 0, st, slots, ghtab, keys, first, count);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t tlsrec__launch_gcm(const GcmArgs *a, int dec, int lanes, int nr, uint32_t grid, hipStream_t st)
+{
+    switch (lanes) {
+        case 4: return dec ? launch_gcm_nr<4, true>(*a, nr, grid, st) : launch_gcm_nr<4, false>(*a, nr, grid, st);
+        case 8: return dec ? launch_gcm_nr<8, true>(*a, nr, grid, st) : launch_gcm_nr<8, false>(*a, nr, grid, st);
+        case 16: return dec ? launch_gcm_nr<16, true>(*a, nr, grid, st) : launch_gcm_nr<16, false>(*a, nr, grid, st);
+        case 64: return dec ? launch_gcm_nr<64, true>(*a, nr, grid, st) : launch_gcm_nr<64, false>(*a, nr, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+extern "C" hipError_t tlsrec__launch_chachapoly(const CpArgs *a, int dec, int lanes, uint32_t grid, hipStream_t st)
+{
+    switch (lanes) {
+        case 1: return dec ? launch_cp_t<1, true>(*a, grid, st) : launch_cp_t<1, false>(*a, grid, st);
+        case 2: return dec ? launch_cp_t<2, true>(*a, grid, st) : launch_cp_t<2, false>(*a, grid, st);
+        case 4: return dec ? launch_cp_t<4, true>(*a, grid, st) : launch_cp_t<4, false>(*a, grid, st);
+        case 8: return dec ? launch_cp_t<8, true>(*a, grid, st) : launch_cp_t<8, false>(*a, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}

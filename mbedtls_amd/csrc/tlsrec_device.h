@@ -1,0 +1,344 @@
+/*
+ * tlsrec_device.h -- CDNA4 (gfx950) device primitives for the record engine.
+ *
+ *  - AES forward cipher with two 256-entry "T" tables in LDS, replicated 32x
+ *    so that lane l always reads bank (l & 31): data-dependent indices never
+ *    conflict.  One v_perm_b32 builds each LDS address from a state byte.
+ *  - GHASH multiply by a fixed power of H with 4-bit position tables in LDS
+ *    (32 windows x 16 entries x 16 B = 8 KiB per power); one ds_read_b128
+ *    per nibble, conflict-free because a window's 16 entries span exactly the
+ *    64 banks.
+ *  - ChaCha20 block per lane (RFC 8439 2.3), v_alignbit rotates.
+ *  - Poly1305 arithmetic mod 2^130-5 in five 26-bit limbs with 64-bit
+ *    multiply-adds (v_mad_u64_u32).
+ *
+ * The AES S-box is generated at compile time from its FIPS-197 definition.
+ */
+#ifndef TLSREC_DEVICE_H
+#define TLSREC_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tlsrec {
+
+/* ---------------- AES S-box (constexpr, FIPS-197 5.1.1) ---------------- */
+struct SboxGen {
+    uint8_t v[256];
+    constexpr SboxGen() : v() {
+        uint8_t ex[256] = {};
+        uint8_t lg[256] = {};
+        uint8_t x = 1;
+        for (int i = 0; i < 255; i++) {
+            ex[i] = x;
+            lg[x] = (uint8_t) i;
+            uint8_t x2 = (uint8_t) ((x << 1) ^ ((x & 0x80) ? 0x1b : 0));
+            x = (uint8_t) (x2 ^ x);               /* generator 3 */
+        }
+        for (int a = 0; a < 256; a++) {
+            uint8_t inv = a ? ex[(255 - lg[a]) % 255] : 0;
+            uint8_t s = inv, r = inv;
+            for (int k = 0; k < 4; k++) {
+                r = (uint8_t) ((r << 1) | (r >> 7));
+                s = (uint8_t) (s ^ r);
+            }
+            v[a] = (uint8_t) (s ^ 0x63);
+        }
+    }
+};
+
+__constant__ const SboxGen kSbox{};
+
+__device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff; }
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+/* ---------------- LDS T-tables ----------------------------------------- */
+/* Entry x of table j (j = 0: T0 = (2s,s,s,3s), j = 1: T1 = rotl8(T0)),
+ * copy c, lives at lds_aes + x*256 + j*128 + c*4.  T2 = rotl16(T0) and
+ * T3 = rotl16(T1) are formed with one v_alignbit per column. */
+__device__ __forceinline__ void aes_fill_tables(uint8_t *lds_aes, int tid, int nthreads)
+{
+    for (int t = tid; t < 256 * 4; t += nthreads) {
+        uint32_t x = t & 255, part = t >> 8;          /* part: copies 8*part .. 8*part+7 */
+        uint32_t s = kSbox.v[x];
+        uint32_t s2 = xtime8(s), s3 = s2 ^ s;
+        uint32_t t0 = s2 | (s << 8) | (s << 16) | (s3 << 24);
+        uint32_t t1 = rotl32(t0, 8);
+        uint4 v0 = make_uint4(t0, t0, t0, t0), v1 = make_uint4(t1, t1, t1, t1);
+        uint8_t *row = lds_aes + x * 256 + part * 32;
+        *reinterpret_cast<uint4 *>(row) = v0;
+        *reinterpret_cast<uint4 *>(row + 16) = v0;
+        *reinterpret_cast<uint4 *>(row + 128) = v1;
+        *reinterpret_cast<uint4 *>(row + 144) = v1;
+    }
+}
+
+/* v_perm selector: byte0 <- lanebase byte 0 (= (lane&31)*4), byte1 <- state
+ * byte k, bytes 2,3 <- 0.  The result is the LDS address x*256 + (lane&31)*4. */
+#define TLSREC_PSEL(k) (0x0C0C0000u | ((4u + (k)) << 8))
+
+template <int AES_OFF>
+__device__ __forceinline__ uint32_t tlook(const uint8_t *lds, uint32_t w, uint32_t lb, int k, int tab)
+{
+    uint32_t a = __builtin_amdgcn_perm(w, lb, TLSREC_PSEL(k));
+    return *reinterpret_cast<const uint32_t *>(lds + a + AES_OFF + tab * 128);
+}
+
+/* AES-128 (NR=10) / AES-256 (NR=14) forward cipher of one block per lane.
+ * Words are little-endian columns: byte r of word c is row r of column c. */
+template <int NR, int AES_OFF>
+__device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk,
+                                             uint4 in)
+{
+    uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        uint32_t t0 = tlook<AES_OFF>(lds, s0, lb, 0, 0) ^ tlook<AES_OFF>(lds, s1, lb, 1, 1) ^
+                      rotl16(tlook<AES_OFF>(lds, s2, lb, 2, 0) ^ tlook<AES_OFF>(lds, s3, lb, 3, 1)) ^ rk[4 * r + 0];
+        uint32_t t1 = tlook<AES_OFF>(lds, s1, lb, 0, 0) ^ tlook<AES_OFF>(lds, s2, lb, 1, 1) ^
+                      rotl16(tlook<AES_OFF>(lds, s3, lb, 2, 0) ^ tlook<AES_OFF>(lds, s0, lb, 3, 1)) ^ rk[4 * r + 1];
+        uint32_t t2 = tlook<AES_OFF>(lds, s2, lb, 0, 0) ^ tlook<AES_OFF>(lds, s3, lb, 1, 1) ^
+                      rotl16(tlook<AES_OFF>(lds, s0, lb, 2, 0) ^ tlook<AES_OFF>(lds, s1, lb, 3, 1)) ^ rk[4 * r + 2];
+        uint32_t t3 = tlook<AES_OFF>(lds, s3, lb, 0, 0) ^ tlook<AES_OFF>(lds, s0, lb, 1, 1) ^
+                      rotl16(tlook<AES_OFF>(lds, s1, lb, 2, 0) ^ tlook<AES_OFF>(lds, s2, lb, 3, 1)) ^ rk[4 * r + 3];
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    /* last round: S[x] is byte 1 (and byte 2) of T0[x] */
+    uint32_t o[4];
+    const uint32_t s[4] = { s0, s1, s2, s3 };
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        uint32_t a = tlook<AES_OFF>(lds, s[c], lb, 0, 0);
+        uint32_t b = tlook<AES_OFF>(lds, s[(c + 1) & 3], lb, 1, 0);
+        uint32_t d2 = tlook<AES_OFF>(lds, s[(c + 2) & 3], lb, 2, 0);
+        uint32_t d3 = tlook<AES_OFF>(lds, s[(c + 3) & 3], lb, 3, 0);
+        uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0501u);   /* [a.b1, b.b1, 0, 0] */
+        uint32_t hi = __builtin_amdgcn_perm(d3, d2, 0x06020C0Cu);  /* [0, 0, d2.b2, d3.b2] */
+        o[c] = (lo | hi) ^ rk[4 * NR + c];
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+/* ---------------- GHASH with LDS position tables ----------------------- */
+/* Table PI (a power of H) holds T_k[n] = sum_{i<4} bit(3-i of n) * P * x^(4k+i)
+ * at PI*8192 + k*256 + n*16, as the 16-byte GCM string.  Window k = 2b is the
+ * high nibble of byte b, k = 2b+1 its low nibble. */
+template <int PI>
+__device__ __forceinline__ uint4 gmul(const uint8_t *lds, uint4 y)
+{
+    const uint32_t w[4] = { y.x, y.y, y.z, y.w };
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int b = 4 * d + e;
+            uint32_t ahi = (e == 0) ? (w[d] & 0xf0u) : ((w[d] >> (8 * e)) & 0xf0u);
+            uint32_t alo = (e == 0) ? ((w[d] << 4) & 0xf0u) : ((w[d] >> (8 * e - 4)) & 0xf0u);
+            uint4 th = *reinterpret_cast<const uint4 *>(lds + ahi + PI * 8192 + (2 * b) * 256);
+            uint4 tl = *reinterpret_cast<const uint4 *>(lds + alo + PI * 8192 + (2 * b + 1) * 256);
+            acc.x ^= th.x ^ tl.x;
+            acc.y ^= th.y ^ tl.y;
+            acc.z ^= th.z ^ tl.z;
+            acc.w ^= th.w ^ tl.w;
+        }
+    }
+    return acc;
+}
+
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
+
+/* ---------------- GF(2^128) bitwise helpers (key setup only) ----------- */
+/* big-endian (hi = bytes 0..7) representation */
+struct G128 { uint64_t hi, lo; };
+
+__device__ __forceinline__ G128 g_shr1(G128 v)
+{
+    uint64_t lsb = v.lo & 1;
+    G128 r;
+    r.lo = (v.lo >> 1) | (v.hi << 63);
+    r.hi = (v.hi >> 1) ^ (lsb ? 0xE100000000000000ULL : 0);
+    return r;
+}
+
+__device__ inline G128 g_mul(G128 x, G128 y)
+{
+    G128 z = { 0, 0 }, v = y;
+    for (int i = 0; i < 128; i++) {
+        uint64_t bit = (i < 64) ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
+        if (bit) { z.hi ^= v.hi; z.lo ^= v.lo; }
+        v = g_shr1(v);
+    }
+    return z;
+}
+
+__device__ __forceinline__ uint4 g_to_words(G128 v)
+{
+    return make_uint4(bswap32((uint32_t) (v.hi >> 32)), bswap32((uint32_t) v.hi),
+                      bswap32((uint32_t) (v.lo >> 32)), bswap32((uint32_t) v.lo));
+}
+
+__device__ __forceinline__ G128 g_from_words(uint4 w)
+{
+    G128 v;
+    v.hi = ((uint64_t) bswap32(w.x) << 32) | bswap32(w.y);
+    v.lo = ((uint64_t) bswap32(w.z) << 32) | bswap32(w.w);
+    return v;
+}
+
+/* ---------------- ChaCha20 (RFC 8439 2.3) ------------------------------ */
+#define TLSREC_QR(a, b, c, d)                                  \
+    do {                                                       \
+        a += b; d ^= a; d = rotl32(d, 16);                     \
+        c += d; b ^= c; b = rotl32(b, 12);                     \
+        a += b; d ^= a; d = rotl32(d, 8);                      \
+        c += d; b ^= c; b = rotl32(b, 7);                      \
+    } while (0)
+
+__device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3],
+                                             uint32_t out[16])
+{
+    const uint32_t in[16] = { 0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                              key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                              counter, nonce[0], nonce[1], nonce[2] };
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = in[i];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        TLSREC_QR(x[0], x[4], x[8], x[12]);
+        TLSREC_QR(x[1], x[5], x[9], x[13]);
+        TLSREC_QR(x[2], x[6], x[10], x[14]);
+        TLSREC_QR(x[3], x[7], x[11], x[15]);
+        TLSREC_QR(x[0], x[5], x[10], x[15]);
+        TLSREC_QR(x[1], x[6], x[11], x[12]);
+        TLSREC_QR(x[2], x[7], x[8], x[13]);
+        TLSREC_QR(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
+}
+
+/* ---------------- Poly1305 in 26-bit limbs ----------------------------- */
+struct P5 { uint32_t v[5]; };
+
+#define TLSREC_M26 0x3ffffffu
+
+__device__ __forceinline__ P5 p_zero() { P5 r; for (int i = 0; i < 5; i++) r.v[i] = 0; return r; }
+
+/* 16-byte little-endian block plus 2^128 (every AEAD block is full, RFC 8439 2.8) */
+__device__ __forceinline__ P5 p_block(uint4 w)
+{
+    P5 r;
+    r.v[0] = w.x & TLSREC_M26;
+    r.v[1] = ((w.x >> 26) | (w.y << 6)) & TLSREC_M26;
+    r.v[2] = ((w.y >> 20) | (w.z << 12)) & TLSREC_M26;
+    r.v[3] = ((w.z >> 14) | (w.w << 18)) & TLSREC_M26;
+    r.v[4] = (w.w >> 8) | (1u << 24);
+    return r;
+}
+
+/* clamped r from the first 16 bytes of the one-time key */
+__device__ __forceinline__ P5 p_from_r(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
+{
+    k0 &= 0x0fffffffu; k1 &= 0x0ffffffcu; k2 &= 0x0ffffffcu; k3 &= 0x0ffffffcu;
+    P5 r;
+    r.v[0] = k0 & TLSREC_M26;
+    r.v[1] = ((k0 >> 26) | (k1 << 6)) & TLSREC_M26;
+    r.v[2] = ((k1 >> 20) | (k2 << 12)) & TLSREC_M26;
+    r.v[3] = ((k2 >> 14) | (k3 << 18)) & TLSREC_M26;
+    r.v[4] = k3 >> 8;
+    return r;
+}
+
+__device__ __forceinline__ P5 p_add(P5 a, P5 b)
+{
+    P5 r;
+#pragma unroll
+    for (int i = 0; i < 5; i++) r.v[i] = a.v[i] + b.v[i];
+    return r;
+}
+
+__device__ __forceinline__ P5 p_sel(bool c, P5 a, P5 b)
+{
+    P5 r;
+#pragma unroll
+    for (int i = 0; i < 5; i++) r.v[i] = c ? a.v[i] : b.v[i];
+    return r;
+}
+
+/* h * r mod 2^130-5 (partially reduced).  Input limbs < 2^27, output limbs
+ * < 2^26 except limb 1 < 2^26 + 2^6. */
+__device__ __forceinline__ P5 p_mul(P5 h, P5 r)
+{
+    const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
+    uint64_t d0 = (uint64_t) h.v[0] * r.v[0] + (uint64_t) h.v[1] * s4 + (uint64_t) h.v[2] * s3 +
+                  (uint64_t) h.v[3] * s2 + (uint64_t) h.v[4] * s1;
+    uint64_t d1 = (uint64_t) h.v[0] * r.v[1] + (uint64_t) h.v[1] * r.v[0] + (uint64_t) h.v[2] * s4 +
+                  (uint64_t) h.v[3] * s3 + (uint64_t) h.v[4] * s2;
+    uint64_t d2 = (uint64_t) h.v[0] * r.v[2] + (uint64_t) h.v[1] * r.v[1] + (uint64_t) h.v[2] * r.v[0] +
+                  (uint64_t) h.v[3] * s4 + (uint64_t) h.v[4] * s3;
+    uint64_t d3 = (uint64_t) h.v[0] * r.v[3] + (uint64_t) h.v[1] * r.v[2] + (uint64_t) h.v[2] * r.v[1] +
+                  (uint64_t) h.v[3] * r.v[0] + (uint64_t) h.v[4] * s4;
+    uint64_t d4 = (uint64_t) h.v[0] * r.v[4] + (uint64_t) h.v[1] * r.v[3] + (uint64_t) h.v[2] * r.v[2] +
+                  (uint64_t) h.v[3] * r.v[1] + (uint64_t) h.v[4] * r.v[0];
+    P5 o;
+    uint64_t c;
+    c = d0 >> 26; o.v[0] = (uint32_t) d0 & TLSREC_M26; d1 += c;
+    c = d1 >> 26; o.v[1] = (uint32_t) d1 & TLSREC_M26; d2 += c;
+    c = d2 >> 26; o.v[2] = (uint32_t) d2 & TLSREC_M26; d3 += c;
+    c = d3 >> 26; o.v[3] = (uint32_t) d3 & TLSREC_M26; d4 += c;
+    c = d4 >> 26; o.v[4] = (uint32_t) d4 & TLSREC_M26;
+    uint64_t t = (uint64_t) o.v[0] + c * 5;
+    o.v[0] = (uint32_t) t & TLSREC_M26;
+    o.v[1] += (uint32_t) (t >> 26);
+    return o;
+}
+
+/* full carry so that every limb < 2^26 (value < 2^130 + small) */
+__device__ __forceinline__ P5 p_carry(P5 h)
+{
+    uint32_t c;
+    c = h.v[0] >> 26; h.v[0] &= TLSREC_M26; h.v[1] += c;
+    c = h.v[1] >> 26; h.v[1] &= TLSREC_M26; h.v[2] += c;
+    c = h.v[2] >> 26; h.v[2] &= TLSREC_M26; h.v[3] += c;
+    c = h.v[3] >> 26; h.v[3] &= TLSREC_M26; h.v[4] += c;
+    c = h.v[4] >> 26; h.v[4] &= TLSREC_M26; h.v[0] += c * 5;
+    c = h.v[0] >> 26; h.v[0] &= TLSREC_M26; h.v[1] += c;
+    return h;
+}
+
+/* tag = (h mod p) + s mod 2^128, as 4 little-endian words */
+__device__ __forceinline__ uint4 p_finish(P5 h, uint4 s)
+{
+    h = p_carry(h);
+    h = p_carry(h);
+    /* g = h + 5 - 2^130 */
+    uint32_t g[5], c;
+    g[0] = h.v[0] + 5; c = g[0] >> 26; g[0] &= TLSREC_M26;
+    g[1] = h.v[1] + c; c = g[1] >> 26; g[1] &= TLSREC_M26;
+    g[2] = h.v[2] + c; c = g[2] >> 26; g[2] &= TLSREC_M26;
+    g[3] = h.v[3] + c; c = g[3] >> 26; g[3] &= TLSREC_M26;
+    g[4] = h.v[4] + c - (1u << 26);
+    uint32_t mask = (g[4] >> 31) - 1;   /* all ones if h >= p */
+#pragma unroll
+    for (int i = 0; i < 5; i++) h.v[i] = (h.v[i] & ~mask) | (g[i] & mask);
+    uint32_t w0 = h.v[0] | (h.v[1] << 26);
+    uint32_t w1 = (h.v[1] >> 6) | (h.v[2] << 20);
+    uint32_t w2 = (h.v[2] >> 12) | (h.v[3] << 14);
+    uint32_t w3 = (h.v[3] >> 18) | (h.v[4] << 8);
+    uint64_t f = (uint64_t) w0 + s.x;
+    uint32_t o0 = (uint32_t) f;
+    f = (uint64_t) w1 + s.y + (f >> 32);
+    uint32_t o1 = (uint32_t) f;
+    f = (uint64_t) w2 + s.z + (f >> 32);
+    uint32_t o2 = (uint32_t) f;
+    f = (uint64_t) w3 + s.w + (f >> 32);
+    return make_uint4(o0, o1, o2, (uint32_t) f);
+}
+
+} /* namespace tlsrec */
+
+#endif /* TLSREC_DEVICE_H */

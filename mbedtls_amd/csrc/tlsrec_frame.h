@@ -1,0 +1,226 @@
+/*
+ * tlsrec_frame.h -- per-record framing plan for the AEAD record path.
+ *
+ * Restates, as straight-line integer code shared by the host C library and
+ * the HIP kernels, every decision mbedtls_ssl_encrypt_buf /
+ * mbedtls_ssl_decrypt_buf take before and after their psa_aead_* call:
+ *
+ *   structure checks            ssl_msg.c:814-823 (enc), :1301-1307 (dec)
+ *   content length limit        ssl_msg.c:831-839
+ *   TLS 1.3 inner plaintext     ssl_msg.c:853-868 with :431-435, :466-491
+ *   tag room                    ssl_msg.c:995-998
+ *   nonce                       ssl_msg.c:768-781, :1012-1019, :1383-1388
+ *   additional data             ssl_msg.c:568-735 (non-CID)
+ *   explicit IV (TLS 1.2 GCM)   ssl_msg.c:1066-1075 (enc), :1352-1365 (dec)
+ *   short-record checks         ssl_msg.c:1356-1377
+ *
+ * The plan says what the device must do (AEAD over which bytes, with which
+ * nonce and AAD) and what the record fields / status are if it stops early.
+ * The AEAD itself and the TLS 1.3 unpadding (ssl_msg.c:1809-1818) run in the
+ * kernels.
+ */
+#ifndef TLSREC_FRAME_H
+#define TLSREC_FRAME_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define TLSREC_HD __host__ __device__ static inline
+#else
+#define TLSREC_HD static inline
+#endif
+
+#define TLSREC_E_BAD_INPUT_DATA   (-135)
+#define TLSREC_E_BUFFER_TOO_SMALL (-138)
+#define TLSREC_E_INVALID_MAC      (-0x7180)
+#define TLSREC_E_INVALID_RECORD   (-0x7200)
+#define TLSREC_E_INTERNAL_ERROR   (-0x6C00)
+
+typedef struct tlsrec_plan {
+    int32_t  status;          /* error found before the AEAD (no AEAD runs) */
+    int32_t  post_status;     /* error the reference returns after its AEAD */
+    uint32_t data_offset;     /* rec->data_offset when the call returns */
+    uint32_t data_len;        /* rec->data_len when the call returns (enc) /
+                                 after tag removal (dec, before unpadding) */
+    uint8_t  type;            /* rec->type when the call returns (enc) */
+    uint8_t  tls13;
+    uint8_t  explicit_iv;     /* TLS 1.2 GCM: 8-byte nonce travels in the record */
+    uint8_t  aad_len;         /* 5 (TLS 1.3) or 13 (TLS 1.2) */
+    uint32_t aead_pos;        /* buffer offset of the AEAD input/output */
+    uint32_t aead_len;        /* AEAD plaintext length (ciphertext w/o tag) */
+    uint32_t content_len;     /* encrypt: bytes taken from the buffer; the
+                                 remaining aead_len - content_len bytes are
+                                 the inner type byte and zero padding */
+    uint8_t  inner_type;      /* encrypt TLS 1.3: real content type */
+    uint8_t  side_type;       /* early error still wrote the type byte ... */
+    uint16_t side_zeros;      /* ... and this many zero pad bytes after it */
+    uint32_t side_pos;        /* at this buffer offset */
+    uint8_t  aad[16];
+    uint8_t  nonce[12];       /* decrypt + explicit_iv: bytes 4..11 come from
+                                 the record (buffer offset data_offset) */
+} tlsrec_plan;
+
+/* Key-slot parameters the plan needs (from the transform / key material). */
+typedef struct tlsrec_plan_key {
+    int tls13;
+    uint32_t fixed_ivlen;     /* 12 or 4 */
+    uint32_t taglen;          /* 16 */
+    const uint8_t *iv;        /* fixed IV (iv_enc for encrypt, iv_dec for decrypt) */
+} tlsrec_plan_key;
+
+TLSREC_HD void tlsrec__nonce(uint8_t nonce[12], const uint8_t *fixed, uint32_t fixed_len,
+                             const uint8_t dyn[8])
+{
+    /* ssl_build_record_nonce (ssl_msg.c:768-781) */
+    for (int i = 0; i < 12; i++) nonce[i] = (uint32_t) i < fixed_len ? fixed[i] : 0;
+    for (int i = 0; i < 8; i++) nonce[4 + i] ^= dyn[i];
+}
+
+TLSREC_HD uint8_t tlsrec__aad(uint8_t aad[16], int tls13, const uint8_t ctr[8], uint8_t type,
+                              const uint8_t ver[2], uint32_t len_field)
+{
+    /* ssl_extract_add_data_from_record (ssl_msg.c:568-735), non-CID:
+     * TLS 1.3: type || ver || len(TLSCiphertext)        (:671-677, :727-731)
+     * TLS 1.2: seq  || type || ver || len(plaintext)    (:700-703, :727-731) */
+    uint8_t n = 0;
+    for (int i = 0; i < 16; i++) aad[i] = 0;
+    if (!tls13) {
+        for (int i = 0; i < 8; i++) aad[n++] = ctr[i];
+    }
+    aad[n++] = type;
+    aad[n++] = ver[0];
+    aad[n++] = ver[1];
+    aad[n++] = (uint8_t) (len_field >> 8);
+    aad[n++] = (uint8_t) len_field;
+    return n;
+}
+
+/* mbedtls_ssl_encrypt_buf, AEAD mode.  buf_len/data_offset/data_len are the
+ * mbedtls_record fields; granularity is MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY. */
+TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
+                                   const uint8_t ctr[8], uint8_t type, const uint8_t ver[2],
+                                   uint64_t buf_len, uint64_t data_offset, uint64_t data_len,
+                                   uint32_t granularity)
+{
+    p->status = 0;
+    p->post_status = 0;
+    p->data_offset = (uint32_t) data_offset;
+    p->data_len = (uint32_t) data_len;
+    p->type = type;
+    p->tls13 = (uint8_t) k->tls13;
+    p->explicit_iv = (uint8_t) (k->fixed_ivlen != 12);
+    p->aad_len = 0;
+    p->aead_pos = (uint32_t) data_offset;
+    p->aead_len = 0;
+    p->content_len = (uint32_t) data_len;
+    p->inner_type = type;
+    p->side_type = 0;
+    p->side_zeros = 0;
+    p->side_pos = 0;
+
+    if (buf_len < data_offset || buf_len - data_offset < data_len) {    /* :814-823 */
+        p->status = TLSREC_E_INTERNAL_ERROR;
+        return;
+    }
+    if (data_len > 16384) {                                            /* :831-839 */
+        p->status = TLSREC_E_BAD_INPUT_DATA;
+        return;
+    }
+    uint64_t post_avail = buf_len - (data_len + data_offset);
+    uint64_t len = data_len;
+    if (k->tls13) {                                                    /* :853-868 */
+        uint32_t g = granularity ? granularity : 16;
+        uint64_t pad = (g - (data_len + 1) % g) % g;                   /* :431-435 */
+        if (post_avail == 0) {                                         /* :473-475 */
+            p->status = TLSREC_E_BUFFER_TOO_SMALL;
+            return;
+        }
+        if (post_avail - 1 < pad) {                                    /* :480-482 */
+            /* the real type byte has already been written (:476) */
+            p->side_type = 1;
+            p->side_pos = (uint32_t) (data_offset + data_len);
+            p->status = TLSREC_E_BUFFER_TOO_SMALL;
+            return;
+        }
+        len = data_len + 1 + pad;
+        p->data_len = (uint32_t) len;
+        p->type = 23;                                                  /* :867 */
+        post_avail = buf_len - (len + data_offset);
+        if (post_avail < k->taglen) {                                  /* :995-998 */
+            /* inner plaintext was built in the buffer before this check */
+            p->side_type = 1;
+            p->side_zeros = (uint16_t) pad;
+            p->side_pos = (uint32_t) (data_offset + data_len);
+            p->status = TLSREC_E_BUFFER_TOO_SMALL;
+            return;
+        }
+    } else if (post_avail < k->taglen) {                               /* :995-998 */
+        p->status = TLSREC_E_BUFFER_TOO_SMALL;
+        return;
+    }
+    tlsrec__nonce(p->nonce, k->iv, k->fixed_ivlen, ctr);               /* :1012-1019 */
+    p->aad_len = tlsrec__aad(p->aad, k->tls13, ctr, p->type, ver,
+                             (uint32_t) (k->tls13 ? len + k->taglen : len));
+    p->aead_len = (uint32_t) len;
+    p->data_len = (uint32_t) (len + 16);                               /* psa_aead_encrypt output */
+    if (p->explicit_iv) {                                              /* :1066-1075 */
+        if (data_offset < 8) {
+            p->post_status = TLSREC_E_BUFFER_TOO_SMALL;
+        } else {
+            p->data_offset = (uint32_t) (data_offset - 8);
+            p->data_len += 8;
+        }
+    }
+}
+
+/* mbedtls_ssl_decrypt_buf, AEAD mode (up to, not including, the AEAD call). */
+TLSREC_HD void tlsrec_plan_decrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
+                                   const uint8_t ctr[8], uint8_t type, const uint8_t ver[2],
+                                   uint64_t buf_len, uint64_t data_offset, uint64_t data_len)
+{
+    p->status = 0;
+    p->post_status = 0;
+    p->data_offset = (uint32_t) data_offset;
+    p->data_len = (uint32_t) data_len;
+    p->type = type;
+    p->tls13 = (uint8_t) k->tls13;
+    p->explicit_iv = (uint8_t) (k->fixed_ivlen != 12);
+    p->aad_len = 0;
+    p->aead_pos = (uint32_t) data_offset;
+    p->aead_len = 0;
+    p->content_len = 0;
+    p->inner_type = 0;
+    p->side_type = 0;
+    p->side_zeros = 0;
+    p->side_pos = 0;
+
+    if (buf_len < data_offset || buf_len - data_offset < data_len) {    /* :1301-1307 */
+        p->status = TLSREC_E_INTERNAL_ERROR;
+        return;
+    }
+    uint64_t off = data_offset, len = data_len;
+    if (p->explicit_iv) {                                              /* :1352-1365 */
+        if (len < 8) {
+            p->status = TLSREC_E_INVALID_MAC;
+            return;
+        }
+        off += 8;
+        len -= 8;
+        p->data_offset = (uint32_t) off;
+        p->data_len = (uint32_t) len;
+    }
+    if (len < k->taglen) {                                             /* :1371-1377 */
+        p->status = TLSREC_E_INVALID_MAC;
+        return;
+    }
+    len -= k->taglen;
+    p->data_len = (uint32_t) len;
+    p->aead_pos = (uint32_t) off;
+    p->aead_len = (uint32_t) len;
+    /* the dynamic part is rec->ctr, or the explicit IV read from the record */
+    tlsrec__nonce(p->nonce, k->iv, k->fixed_ivlen, ctr);
+    p->aad_len = tlsrec__aad(p->aad, k->tls13, ctr, type, ver,
+                             (uint32_t) (k->tls13 ? len + k->taglen : len));
+}
+
+#endif /* TLSREC_FRAME_H */

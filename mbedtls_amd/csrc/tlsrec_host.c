@@ -1,0 +1,213 @@
+/*
+ * tlsrec_host.c -- single-record entry points (host C).
+ *
+ * tlsrec_encrypt_buf / tlsrec_decrypt_buf keep the contract of
+ * mbedtls_ssl_encrypt_buf / mbedtls_ssl_decrypt_buf (library/ssl_msg.c:784,
+ * :1270): the record's buffer is protected in place, data_offset / data_len /
+ * type are updated, 0 or MBEDTLS_ERR_SSL_* is returned.  Checks that need no
+ * record bytes are decided here with the same framing plan the kernels use
+ * (tlsrec_frame.h); everything else -- the AEAD, the tag check, the TLS 1.3
+ * unpadding -- runs on the GPU through the batch kernels with a batch of one.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "tlsrec.h"
+#include "tlsrec_frame.h"
+
+/* engine.hip */
+int tlsrec__engine_slot_alloc(const tlsrec_key_material *km);
+void tlsrec__engine_slot_free(int slot);
+int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
+                       tlsrec_batch_res *out);
+
+static void zeroize(void *p, size_t n)
+{
+    volatile unsigned char *v = (volatile unsigned char *) p;
+    while (n--) *v++ = 0;
+}
+
+int tlsrec_transform_setup(tlsrec_transform *t, int tls_version, int cipher,
+                           const unsigned char *key_enc, const unsigned char *key_dec,
+                           const unsigned char *iv_enc, const unsigned char *iv_dec)
+{
+    return tlsrec_transform_setup_ex(t, tls_version, cipher, key_enc, key_dec, iv_enc, iv_dec,
+                                     TLSREC_PADDING_GRANULARITY);
+}
+
+int tlsrec_transform_setup_ex(tlsrec_transform *t, int tls_version, int cipher,
+                              const unsigned char *key_enc, const unsigned char *key_dec,
+                              const unsigned char *iv_enc, const unsigned char *iv_dec,
+                              unsigned granularity)
+{
+    if (t == NULL || key_enc == NULL || key_dec == NULL || iv_enc == NULL || iv_dec == NULL)
+        return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (granularity == 0 || granularity > 255) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    memset(t, 0, sizeof(*t));
+    t->slot_enc = t->slot_dec = -1;
+    t->granularity = granularity;
+    switch (cipher) {                      /* mbedtls_ssl_cipher_to_psa, ssl_tls.c:2168-2363 */
+        case TLSREC_CIPHER_AES_128_GCM: t->keylen = 16; break;
+        case TLSREC_CIPHER_AES_256_GCM:
+        case TLSREC_CIPHER_CHACHA20_POLY1305: t->keylen = 32; break;
+        default: return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
+    }
+    t->cipher = cipher;
+    t->tls_version = tls_version;
+    t->ivlen = 12;
+    t->taglen = 16;
+    t->maclen = 0;
+    if (tls_version == TLSREC_VERSION_TLS1_3) {           /* ssl_tls13_keys.c:985-998 */
+        t->fixed_ivlen = t->ivlen;
+        t->minlen = t->taglen + granularity;
+    } else if (tls_version == TLSREC_VERSION_TLS1_2) {    /* ssl_tls.c:7768-7797 */
+        t->fixed_ivlen = cipher == TLSREC_CIPHER_CHACHA20_POLY1305 ? 12 : 4;
+        t->minlen = (t->ivlen - t->fixed_ivlen) + t->taglen;
+    } else {
+        return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    }
+    memcpy(t->key_enc, key_enc, t->keylen);
+    memcpy(t->key_dec, key_dec, t->keylen);
+    memcpy(t->iv_enc, iv_enc, t->fixed_ivlen);
+    memcpy(t->iv_dec, iv_dec, t->fixed_ivlen);
+
+    tlsrec_key_material km;
+    memset(&km, 0, sizeof(km));
+    km.cipher = (uint8_t) cipher;
+    km.tls_minor = tls_version == TLSREC_VERSION_TLS1_3 ? 4 : 3;
+    km.fixed_ivlen = (uint8_t) t->fixed_ivlen;
+    km.taglen = (uint8_t) t->taglen;
+    km.granularity = (uint8_t) granularity;
+    memcpy(km.iv, iv_enc, t->fixed_ivlen);
+    memcpy(km.key, key_enc, t->keylen);
+    int r = tlsrec__engine_slot_alloc(&km);
+    if (r < 0) {
+        zeroize(&km, sizeof(km));
+        zeroize(t, sizeof(*t));
+        return r;
+    }
+    t->slot_enc = r;
+    memcpy(km.iv, iv_dec, t->fixed_ivlen);
+    memcpy(km.key, key_dec, t->keylen);
+    r = tlsrec__engine_slot_alloc(&km);
+    zeroize(&km, sizeof(km));
+    if (r < 0) {
+        tlsrec__engine_slot_free(t->slot_enc);
+        zeroize(t, sizeof(*t));
+        return r;
+    }
+    t->slot_dec = r;
+    return 0;
+}
+
+void tlsrec_transform_free(tlsrec_transform *t)
+{
+    if (t == NULL) return;
+    if (t->slot_enc >= 0) tlsrec__engine_slot_free(t->slot_enc);
+    if (t->slot_dec >= 0) tlsrec__engine_slot_free(t->slot_dec);
+    zeroize(t, sizeof(*t));
+    t->slot_enc = t->slot_dec = -1;
+}
+
+static tlsrec_plan_key pkey(const tlsrec_transform *t, int dec)
+{
+    tlsrec_plan_key k;
+    k.tls13 = t->tls_version == TLSREC_VERSION_TLS1_3;
+    k.fixed_ivlen = (uint32_t) t->fixed_ivlen;
+    k.taglen = (uint32_t) t->taglen;
+    k.iv = dec ? t->iv_dec : t->iv_enc;
+    return k;
+}
+
+static int run(int dec, tlsrec_transform *t, tlsrec_record *rec)
+{
+    tlsrec_batch_rec d;
+    tlsrec_batch_res res;
+    memset(&d, 0, sizeof(d));
+    d.buf_off = 0;
+    d.buf_len = (uint32_t) rec->buf_len;
+    d.data_offset = (uint32_t) rec->data_offset;
+    d.data_len = (uint32_t) rec->data_len;
+    d.slot = (uint32_t) (dec ? t->slot_dec : t->slot_enc);
+    memcpy(d.ctr, rec->ctr, 8);
+    d.type = rec->type;
+    d.ver[0] = rec->ver[0];
+    d.ver[1] = rec->ver[1];
+    int r = tlsrec__engine_run(dec, &d, rec->buf, rec->buf_len, &res);
+    if (r != 0) return r;
+    rec->data_offset = res.data_offset;
+    rec->data_len = res.data_len;
+    rec->type = res.type;
+    return res.status;
+}
+
+/* mbedtls_ssl_encrypt_buf (ssl_msg.c:784-1268), AEAD transforms */
+int tlsrec_encrypt_buf(void *ssl, tlsrec_transform *t, tlsrec_record *rec)
+{
+    (void) ssl;   /* debug-only in the reference (ssl_msg.c:802-806) */
+    if (t == NULL) return TLSREC_ERR_SSL_INTERNAL_ERROR;                       /* :810-813 */
+    if (rec == NULL || rec->buf == NULL) return TLSREC_ERR_SSL_INTERNAL_ERROR; /* :814-823 */
+    if (rec->buf_len > 0xffffffffu) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    tlsrec_plan_key k = pkey(t, 0);
+    tlsrec_plan p;
+    tlsrec_plan_encrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset,
+                        rec->data_len, t->granularity);
+    if (p.status != 0) {
+        if (p.side_type) {
+            rec->buf[p.side_pos] = rec->type;
+            memset(rec->buf + p.side_pos + 1, 0, p.side_zeros);
+        }
+        rec->data_offset = p.data_offset;
+        rec->data_len = p.data_len;
+        rec->type = p.type;
+        return p.status;
+    }
+    if (t->slot_enc < 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    return run(0, t, rec);
+}
+
+/* mbedtls_ssl_decrypt_buf (ssl_msg.c:1270-1834), AEAD transforms */
+int tlsrec_decrypt_buf(const void *ssl, tlsrec_transform *t, tlsrec_record *rec)
+{
+    (void) ssl;
+    if (rec == NULL || rec->buf == NULL) return TLSREC_ERR_SSL_INTERNAL_ERROR; /* :1301-1307 */
+    if (t == NULL) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    if (rec->buf_len > 0xffffffffu) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    tlsrec_plan_key k = pkey(t, 1);
+    tlsrec_plan p;
+    tlsrec_plan_decrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset, rec->data_len);
+    if (p.status != 0) {
+        rec->data_offset = p.data_offset;
+        rec->data_len = p.data_len;
+        return p.status;
+    }
+    if (t->slot_dec < 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    return run(1, t, rec);
+}
+
+int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_batch_rec *rec,
+                       tlsrec_batch_res *early, uint32_t *aead_pos, uint32_t *aead_len)
+{
+    tlsrec_plan_key k;
+    tlsrec_plan p;
+    k.tls13 = km->tls_minor == 4;
+    k.fixed_ivlen = km->fixed_ivlen;
+    k.taglen = km->taglen;
+    k.iv = km->iv;
+    if (decrypt)
+        tlsrec_plan_decrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset,
+                            rec->data_len);
+    else
+        tlsrec_plan_encrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset,
+                            rec->data_len, km->granularity ? km->granularity : TLSREC_PADDING_GRANULARITY);
+    if (early) {
+        early->status = p.status;
+        early->data_offset = p.data_offset;
+        early->data_len = p.data_len;
+        early->type = p.type;
+        early->reserved[0] = early->reserved[1] = early->reserved[2] = 0;
+    }
+    if (aead_pos) *aead_pos = p.aead_pos;
+    if (aead_len) *aead_len = p.aead_len;
+    return p.status == 0;
+}

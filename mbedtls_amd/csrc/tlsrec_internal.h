@@ -1,0 +1,70 @@
+/*
+ * tlsrec_internal.h -- layouts shared by the kernels and the engine (C++).
+ */
+#ifndef TLSREC_INTERNAL_H
+#define TLSREC_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tlsrec.h"
+
+namespace tlsrec {
+
+constexpr int KEY_TABLES = 7;                       /* H^1, H^2, ..., H^64 */
+constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512;   /* uint4 entries per slot (56 KiB) */
+
+constexpr int GCM_THREADS = 1024;                   /* 16 waves, one workgroup per CU */
+constexpr int GCM_WAVES = GCM_THREADS / 64;
+constexpr int CP_THREADS = 256;
+constexpr int CP_WAVES = CP_THREADS / 64;
+
+/* Expanded per-slot state, 512 bytes. */
+struct SlotState {
+    tlsrec_key_material km;   /* raw material as loaded */
+    uint32_t rk[60];          /* AES round keys, little-endian column words */
+    uint32_t nr;              /* 10 / 14, 0 for ChaCha20-Poly1305 */
+    uint8_t h[16];            /* H = E_K(0^128) */
+    uint8_t pad[512 - 64 - 240 - 4 - 16];
+};
+static_assert(sizeof(SlotState) == 512, "SlotState layout");
+static_assert(sizeof(tlsrec_key_material) == 64, "key material layout");
+static_assert(sizeof(tlsrec_batch_rec) == 40, "batch record layout");
+static_assert(sizeof(tlsrec_batch_res) == 16, "batch result layout");
+
+struct GcmArgs {
+    const SlotState *slots;
+    const uint4 *ghtab;
+    const tlsrec_batch_rec *recs;
+    tlsrec_batch_res *res;
+    uint64_t n;
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t rpw;             /* records per wavefront chunk (<= 64) */
+    uint32_t capacity;
+    uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM */
+};
+
+struct CpArgs {
+    const SlotState *slots;
+    const tlsrec_batch_rec *recs;
+    tlsrec_batch_res *res;
+    uint64_t n;
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t rpw;
+    uint32_t capacity;
+};
+
+} /* namespace tlsrec */
+
+extern "C" {
+hipError_t tlsrec__launch_keysetup(tlsrec::SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
+                                   uint32_t first, uint32_t count, hipStream_t st);
+hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int nr, uint32_t grid,
+                              hipStream_t st);
+hipError_t tlsrec__launch_chachapoly(const tlsrec::CpArgs *a, int dec, int lanes, uint32_t grid,
+                                     hipStream_t st);
+}
+
+#endif

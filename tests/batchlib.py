@@ -1,0 +1,155 @@
+"""Helpers that lay out record batches in a device arena, run them through
+libtlsrec (GPU) and through the oracle (CPU), and compare.  Test-side only."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+import mbedtls_amd as M
+import oracle as O
+from tests.prng import prng_bytes
+
+CIPHERS = {"AES-128-GCM": M.CIPHER_AES_128_GCM, "AES-256-GCM": M.CIPHER_AES_256_GCM,
+           "CHACHA20-POLY1305": M.CIPHER_CHACHA20_POLY1305}
+VERSIONS = {"TLS1.2": M.VERSION_TLS1_2, "TLS1.3": M.VERSION_TLS1_3}
+
+
+def keylen(cipher):
+    return 16 if cipher == M.CIPHER_AES_128_GCM else 32
+
+
+def explicit(cipher, ver):
+    return ver == M.VERSION_TLS1_2 and cipher != M.CIPHER_CHACHA20_POLY1305
+
+
+@dataclass
+class Rec:
+    slot: int
+    buf: bytearray          # the whole record buffer (rec->buf .. rec->buf + buf_len)
+    data_offset: int
+    data_len: int
+    ctr: bytes
+    type: int
+    ver: bytes = b"\x03\x03"
+
+
+class Batch:
+    def __init__(self, slots, recs, align=16):
+        """slots: list of (cipher, version, key, iv, granularity)"""
+        self.slots = slots
+        self.recs = recs
+        offs, pos = [], 0
+        for r in recs:
+            offs.append(pos)
+            pos += (len(r.buf) + align - 1) // align * align + align
+        self.offs = offs
+        self.arena = np.zeros(max(pos, 16), dtype=np.uint8)
+        for r, o in zip(recs, offs):
+            self.arena[o:o + len(r.buf)] = np.frombuffer(bytes(r.buf), dtype=np.uint8)
+        d = M.records(len(recs))
+        for i, (r, o) in enumerate(zip(recs, offs)):
+            d[i]["buf_off"] = o
+            d[i]["buf_len"] = len(r.buf)
+            d[i]["data_offset"] = r.data_offset
+            d[i]["data_len"] = r.data_len
+            d[i]["slot"] = r.slot
+            d[i]["ctr"] = np.frombuffer(r.ctr, dtype=np.uint8)
+            d[i]["type"] = r.type
+            d[i]["ver"] = np.frombuffer(r.ver, dtype=np.uint8)
+        self.desc = d
+
+    def key_materials(self):
+        km = np.concatenate([M.key_material(c, v, k, iv, g) for (c, v, k, iv, g) in self.slots])
+        return km
+
+    def run_gpu(self, decrypt: bool, lanes=0, inplace=True):
+        import torch
+        dev = torch.device("cuda")
+        kt = M.KeyTable(max(1, len(self.slots)))
+        kt.load(self.key_materials())
+        arena = torch.from_numpy(self.arena.copy()).to(dev)
+        out = arena if inplace else torch.zeros_like(arena)
+        recs = torch.from_numpy(self.desc.view(np.uint8).copy()).to(dev)
+        res = torch.zeros(len(self.recs) * 16, dtype=torch.uint8, device=dev)
+        fn = M.batch_decrypt if decrypt else M.batch_encrypt
+        fn(kt, recs, res, len(self.recs), arena, out, lanes=lanes)
+        torch.cuda.synchronize()
+        out_np = out.cpu().numpy()
+        res_np = res.cpu().numpy().view(M.BATCH_RES)
+        kt.close()
+        return out_np, res_np
+
+    def run_oracle(self, decrypt: bool):
+        outs, stats = [], []
+        ts = {}
+        for r in self.recs:
+            c, v, k, iv, g = self.slots[r.slot]
+            if r.slot not in ts:
+                ts[r.slot] = O.Transform(v, c, k, k, iv, iv, granularity=g or 16)
+            t = ts[r.slot]
+            rec = O.Record(ctr=r.ctr, type=r.type, ver=r.ver, buf=bytearray(r.buf),
+                           data_offset=r.data_offset, data_len=r.data_len)
+            st = t.decrypt_buf(rec) if decrypt else t.encrypt_buf(rec)
+            outs.append(rec)
+            stats.append(st)
+        return outs, stats
+
+    def compare(self, decrypt: bool, gpu_out, gpu_res, inplace=True):
+        """Return list of mismatch descriptions (empty = bit-exact)."""
+        o_recs, o_stats = self.run_oracle(decrypt)
+        bad = []
+        for i, (r, orec, ost) in enumerate(zip(self.recs, o_recs, o_stats)):
+            g = gpu_res[i]
+            fields = (int(g["status"]), int(g["data_offset"]), int(g["data_len"]), int(g["type"]))
+            want = (ost, orec.data_offset, orec.data_len, orec.type)
+            if fields != want:
+                bad.append(f"rec {i}: fields {fields} != oracle {want}")
+                continue
+            o = self.offs[i]
+            gbuf = bytes(gpu_out[o:o + len(r.buf)])
+            if inplace:
+                if gbuf != bytes(orec.buf):
+                    diff = next(j for j in range(len(gbuf)) if gbuf[j] != orec.buf[j])
+                    bad.append(f"rec {i}: buffer differs from byte {diff} (len {len(gbuf)})")
+            elif ost == 0:
+                lo, hi = orec.data_offset, orec.data_offset + orec.data_len
+                if gbuf[lo:hi] != bytes(orec.buf[lo:hi]):
+                    bad.append(f"rec {i}: output region differs")
+        return bad
+
+
+def random_slots(rng_seed, ciphers, versions, count):
+    slots = []
+    for i in range(count):
+        c = ciphers[i % len(ciphers)]
+        v = versions[(i // len(ciphers)) % len(versions)]
+        b = prng_bytes(rng_seed * 1000 + i, 48)
+        slots.append((c, v, b[:keylen(c)], b[32:48], 0))
+    return slots
+
+
+def plaintext_records(slots, lengths, seed, head=8, tail=40):
+    recs = []
+    for i, L in enumerate(lengths):
+        s = i % len(slots)
+        payload = prng_bytes(seed + i, L)
+        buf = bytearray(head + L + tail)
+        buf[head:head + L] = payload
+        ctr = int(prng_bytes(seed ^ (i + 77), 8).hex(), 16).to_bytes(8, "big")
+        recs.append(Rec(slot=s, buf=buf, data_offset=head, data_len=L, ctr=ctr,
+                        type=23 if i % 5 else 22))
+    return recs
+
+
+def sealed_records(slots, lengths, seed, head=8, tail=40):
+    """Records encrypted by the oracle, ready for a decrypt batch."""
+    pre = plaintext_records(slots, lengths, seed, head, tail)
+    b = Batch(slots, pre)
+    outs, stats = b.run_oracle(False)
+    recs = []
+    for r, o, st in zip(pre, outs, stats):
+        assert st == 0
+        recs.append(Rec(slot=r.slot, buf=bytearray(o.buf), data_offset=o.data_offset,
+                        data_len=o.data_len, ctr=r.ctr, type=o.type, ver=r.ver))
+    return recs, pre

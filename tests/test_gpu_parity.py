@@ -1,0 +1,210 @@
+"""GPU parity: the HIP path (through the C ABI of libtlsrec.so) against the
+oracle restatement and the committed golden fixtures.  Bit-exact: every
+output byte of every record buffer and every record field / status.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import mbedtls_amd as M  # noqa: E402
+import oracle as O  # noqa: E402
+from tests import batchlib as B  # noqa: E402
+from tests.prng import prng_bytes  # noqa: E402
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+h = bytes.fromhex
+ALL_C = list(B.CIPHERS.values())
+ALL_V = list(B.VERSIONS.values())
+
+
+def _load(name):
+    with open(os.path.join(G, name)) as f:
+        return json.load(f)
+
+
+def test_device_and_library():
+    assert M.device_ok(), "libtlsrec did not find a gfx950 device"
+    assert "gfx950" in M.version()
+
+
+@pytest.mark.parametrize("kat", _load("reference_kats.json"), ids=lambda k: k["name"])
+def test_reference_kats_gpu(kat):
+    """test_suite_ssl.data:2776-2834 through tlsrec_encrypt_buf/decrypt_buf at
+    padding granularity 1 (the KATs' configuration)."""
+    sk, si, ck, ci = (h(kat[x]) for x in ("server_key", "server_iv", "client_key", "client_iv"))
+    if kat["endpoint"] == "client":
+        send = M.Transform(M.VERSION_TLS1_3, M.CIPHER_AES_128_GCM, ck, sk, ci, si, granularity=1)
+        recv = M.Transform(M.VERSION_TLS1_3, M.CIPHER_AES_128_GCM, sk, ck, si, ci, granularity=1)
+    else:
+        send = M.Transform(M.VERSION_TLS1_3, M.CIPHER_AES_128_GCM, sk, ck, si, ci, granularity=1)
+        recv = M.Transform(M.VERSION_TLS1_3, M.CIPHER_AES_128_GCM, ck, sk, ci, si, granularity=1)
+    pt, ct = h(kat["plaintext"]), h(kat["ciphertext"])
+    buf = bytearray(len(ct) + 16)
+    buf[:len(pt)] = pt
+    rec = M.Record(ctr=bytes(7) + bytes([kat["ctr"]]), type=23, ver=b"\x03\x03", buf=buf,
+                   data_offset=0, data_len=len(pt))
+    assert send.encrypt_buf(rec) == 0
+    assert rec.data() == ct and rec.type == 23
+    assert recv.decrypt_buf(rec) == 0
+    assert rec.data() == pt and rec.type == 23
+
+
+def test_record_fixtures_gpu():
+    fx = _load("records.json")
+    for c in fx["cases"]:
+        cipher, ver = B.CIPHERS[c["cipher"]], B.VERSIONS[c["version"]]
+        t = M.Transform(ver, cipher, h(c["key_enc"]), h(c["key_dec"]), h(c["iv_enc"]), h(c["iv_dec"]))
+        peer = M.Transform(ver, cipher, h(c["key_dec"]), h(c["key_enc"]), h(c["iv_dec"]), h(c["iv_enc"]))
+        L = c["len"]
+        payload = prng_bytes(c["seed"] ^ 0xA5A5, L)
+        head = 8 if B.explicit(cipher, ver) else 0
+        buf = bytearray(head + L + 64)
+        buf[head:head + L] = payload
+        rec = M.Record(ctr=h(c["ctr"]), type=c["type"], ver=b"\x03\x03", buf=buf, data_offset=head, data_len=L)
+        assert t.encrypt_buf(rec) == 0, c
+        assert (rec.data_offset, rec.data_len, rec.type) == (c["out_offset"], c["out_len"], c["out_type"])
+        assert hashlib.sha256(rec.data()).hexdigest() == c["wire_sha256"], (c["cipher"], c["version"], L)
+        assert peer.decrypt_buf(rec) == 0
+        assert rec.data() == payload and rec.type == c["type"]
+        t.close()
+        peer.close()
+
+
+EDGE_LENGTHS = [0, 1, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 255, 256, 1000, 1400, 4095, 4096, 16383]
+
+
+@pytest.mark.parametrize("cipher", ALL_C, ids=list(B.CIPHERS))
+@pytest.mark.parametrize("ver", ALL_V, ids=list(B.VERSIONS))
+@pytest.mark.parametrize("decrypt", [False, True], ids=["enc", "dec"])
+def test_batch_vs_oracle(cipher, ver, decrypt):
+    slots = B.random_slots(cipher * 10 + ver, [cipher], [ver], 3)
+    lengths = EDGE_LENGTHS + [int(x) for x in np.frombuffer(prng_bytes(cipher + ver, 80), np.uint16) % 2000]
+    if decrypt:
+        recs, _ = B.sealed_records(slots, lengths, seed=cipher * 7 + ver)
+    else:
+        recs = B.plaintext_records(slots, lengths, seed=cipher * 7 + ver)
+    b = B.Batch(slots, recs)
+    lane_opts = [0, 4, 16, 64] if cipher != M.CIPHER_CHACHA20_POLY1305 else [0, 1, 4, 8]
+    for lanes in lane_opts:
+        out, res = b.run_gpu(decrypt, lanes=lanes)
+        bad = b.compare(decrypt, out, res)
+        assert not bad, f"lanes={lanes}: " + "; ".join(bad[:5])
+    out, res = b.run_gpu(decrypt, inplace=False)
+    assert not b.compare(decrypt, out, res, inplace=False)
+
+
+@pytest.mark.parametrize("cipher", ALL_C, ids=list(B.CIPHERS))
+@pytest.mark.parametrize("ver", ALL_V, ids=list(B.VERSIONS))
+def test_batch_tamper(cipher, ver):
+    """1 bit flipped in every 7th record -> INVALID_MAC there (buffer wiped as
+    PSA does), every other record decrypts."""
+    slots = B.random_slots(99 + cipher, [cipher], [ver], 2)
+    lengths = [17 + 61 * i for i in range(60)]
+    recs, pre = B.sealed_records(slots, lengths, seed=1234)
+    bad_idx = set(range(0, len(recs), 7))
+    for i in bad_idx:
+        r = recs[i]
+        pos = r.data_offset + (i * 13) % r.data_len
+        r.buf[pos] ^= 1 << (i % 8)
+    b = B.Batch(slots, recs)
+    out, res = b.run_gpu(True)
+    assert not b.compare(True, out, res)
+    st = res["status"]
+    assert set(np.nonzero(st)[0].tolist()) == bad_idx
+    assert all(int(st[i]) == M.ERR_SSL_INVALID_MAC for i in bad_idx)
+
+
+def test_mixed_keys_interleaved():
+    """Config-4 shape at test scale: many keys, AES-256-GCM and
+    ChaCha20-Poly1305 interleaved by key, records round-robin over keys."""
+    nkeys, per = 96, 6
+    slots = B.random_slots(4242, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305],
+                           [M.VERSION_TLS1_3], nkeys)
+    lengths = [1400 if (i // nkeys) % 2 else 3000 for i in range(nkeys * per)]
+    for decrypt in (False, True):
+        if decrypt:
+            recs, _ = B.sealed_records(slots, lengths, seed=77)
+        else:
+            recs = B.plaintext_records(slots, lengths, seed=77)
+        b = B.Batch(slots, recs)
+        out, res = b.run_gpu(decrypt)
+        bad = b.compare(decrypt, out, res)
+        assert not bad, "; ".join(bad[:5])
+
+
+@pytest.mark.parametrize("cipher", ALL_C, ids=list(B.CIPHERS))
+@pytest.mark.parametrize("ver", ALL_V, ids=list(B.VERSIONS))
+def test_crypt_record_small_gpu(cipher, ver):
+    """ssl_crypt_record_small (test_suite_ssl.function:1697-1856) through the
+    single-record API, checked byte for byte against the oracle."""
+    kl = B.keylen(cipher)
+    k0, k1, ive, ivd = bytes([1]) * kl, bytes([2]) * kl, bytes([3]) * 16, bytes([4]) * 16
+    t_enc = M.Transform(ver, cipher, k1, k0, ivd, ive)
+    t_dec = M.Transform(ver, cipher, k0, k1, ive, ivd)
+    o_enc = O.Transform(ver, cipher, k1, k0, ivd, ive)
+    buflen = 256
+    for mode in (1, 2, 3):
+        seen = False
+        for off in range(0, 97, 3):
+            if mode == 1:
+                do, dl = off, buflen - off - 128
+            elif mode == 2:
+                do, dl = 64, buflen - 64 - off
+            else:
+                do, dl = off, buflen - 2 * off
+            buf = bytearray(buflen)
+            buf[do:do + dl] = bytes([42]) * dl
+            rec = M.Record(ctr=bytes([off]) * 8, type=42, ver=bytes([off, off]), buf=buf, data_offset=do, data_len=dl)
+            orec = O.Record(ctr=bytes([off]) * 8, type=42, ver=bytes([off, off]), buf=bytearray(buf),
+                            data_offset=do, data_len=dl)
+            r = t_enc.encrypt_buf(rec)
+            assert r == o_enc.encrypt_buf(orec)
+            assert bytes(rec.buf) == bytes(orec.buf)
+            assert (rec.data_offset, rec.data_len, rec.type) == (orec.data_offset, orec.data_len, orec.type)
+            if r == M.ERR_SSL_BUFFER_TOO_SMALL:
+                continue
+            assert r == 0
+            seen = True
+            assert t_dec.decrypt_buf(rec) == 0
+            assert (rec.type, rec.data_offset, rec.data_len) == (42, do, dl)
+            assert rec.data() == bytes([42]) * dl
+        assert seen
+
+
+def test_large_roundtrip_16k():
+    """Size-independent property at full record size: 16 KiB TLS 1.3 records,
+    encrypt then decrypt restores every payload; a sample is bit-exact vs the
+    oracle."""
+    n = 512
+    for cipher in (M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305):
+        slots = B.random_slots(5 + cipher, [cipher], [M.VERSION_TLS1_3], 1)
+        recs = B.plaintext_records(slots, [16383] * n, seed=9, head=0, tail=17)
+        b = B.Batch(slots, recs)
+        out, res = b.run_gpu(False)
+        assert (res["status"] == 0).all() and (res["data_len"] == 16400).all()
+        sample = B.Batch(slots, recs[:8])
+        o_recs, _ = sample.run_oracle(False)
+        for i in range(8):
+            o = b.offs[i]
+            assert bytes(out[o:o + 16400]) == o_recs[i].data()
+        # decrypt the GPU ciphertext
+        b.arena[:] = out
+        d = b.desc.copy()
+        d["data_offset"] = 0
+        d["data_len"] = 16400
+        d["type"] = 23
+        b.desc = d
+        out2, res2 = b.run_gpu(True)
+        assert (res2["status"] == 0).all() and (res2["data_len"] == 16383).all()
+        for i, r in enumerate(recs):
+            o = b.offs[i]
+            assert bytes(out2[o:o + 16383]) == bytes(r.buf[:16383])
