@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tlsrec.h"
 #include "tlsrec_device.h"
 #include "tlsrec_frame.h"
@@ -301,13 +303,17 @@ struct GcmLds {
     static constexpr int BYTES = CTL + 16;
 };
 
-template <int PI>
-__device__ __forceinline__ uint4 gmul_rt(const uint8_t *lds, uint4 y, int pi)
+/* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0 */
+template <int SH>
+__device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
 {
-    /* runtime table selector for the tree: unrolled on PI */
-    if (pi == PI) return gmul<PI>(lds, y);
-    if constexpr (PI > 0) return gmul_rt<PI - 1>(lds, y, pi);
-    return y;
+    if constexpr (SH >= 1) {
+        uint4 o = shfl4(Y, (lane + SH) & 63);
+        Y = xor4(gmul<Log2<SH>::v>(lds, Y), o);
+        return gtree<SH / 2>(lds, Y, lane);
+    } else {
+        return Y;
+    }
 }
 
 template <int L, int NR, bool DEC>
@@ -351,11 +357,9 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
             const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
             uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
             for (int i = tid; i < LY::NT * 512; i += GCM_THREADS) dst[i] = src[i];
-            uint32_t *rkd = reinterpret_cast<uint32_t *>(lds + LY::RK);
-            if (tid < 60) rkd[tid] = a.slots[s].rk[tid];
         }
         __syncthreads();
-        const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LY::RK);
+        const uint32_t *rk = a.slots[s].rk;    /* uniform: s_load into SGPRs */
         const tlsrec_key_material km = a.slots[s].km;
 
         /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
@@ -415,7 +419,12 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
             }
             uint4 Y = (run && m > 0 && (uint32_t) q == z) ? aadw : make_uint4(0, 0, 0, 0);
             uint32_t nzkey = 0;
-            for (uint32_t j = 0; j < Jmax; j++) {
+            /* one step: AES-CTR block c = L*j + q - z, GHASH Horner Y = Y*P ^ X.
+             * P = H for j = 0 (only the C_0 lane holds the AAD there), H^L after;
+             * the table index must stay a compile-time constant so every table
+             * read is one ds_read_b128 with an immediate offset. */
+            auto step = [&](uint32_t j, auto pic) {
+                constexpr int PI = decltype(pic)::value;
                 const int32_t c = (int32_t) (L * j + q) - (int32_t) z;
                 const bool live = run && j < J;
                 const bool valid = live && c >= 0 && (uint32_t) c < m;
@@ -434,16 +443,13 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
                     }
                 }
                 if (live && m == 0 && c == 0) X = aadw;
-                uint4 Yn = (j == 0) ? gmul<0>(lds, Y) : gmul<LOGL>(lds, Y);
-                Yn = xor4(Yn, X);
+                uint4 Yn = xor4(gmul<PI>(lds, Y), X);
                 if (live) Y = Yn;
-            }
+            };
+            if (Jmax > 0) step(0u, std::integral_constant<int, 0>{});
+            for (uint32_t j = 1; j < Jmax; j++) step(j, std::integral_constant<int, LOGL>{});
             /* tree: sum_q Y_q H^(L-q) */
-#pragma unroll
-            for (int sh = L / 2; sh >= 1; sh >>= 1) {
-                uint4 o = shfl4(Y, (lane + sh) & 63);
-                Y = xor4(gmul_rt<LOGL>(lds, Y, Log2<1>::v + __builtin_ctz(sh)), o);
-            }
+            Y = gtree<L / 2>(lds, Y, lane);
             Y = gmul<0>(lds, Y);                                     /* T */
             const uint32_t alen = run ? p.aad_len : 0;
             uint4 lenw = make_uint4(0, bswap32(alen * 8), 0, bswap32(aead_len * 8));
