@@ -140,6 +140,17 @@ extern "C" int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t co
     return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, src, first, count, st));
 }
 
+/* waves per GCM workgroup: 16 (default) or 8; TLSREC_GCM_WAVES overrides */
+static int gcm_waves(void)
+{
+    static int w = 0;
+    if (w == 0) {
+        const char *e = getenv("TLSREC_GCM_WAVES");
+        w = (e && atoi(e) == 8) ? 8 : GCM_WAVES;
+    }
+    return w;
+}
+
 static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t target_wgs)
 {
     uint64_t want = (n + (uint64_t) waves_per_wg * target_wgs - 1) / ((uint64_t) waves_per_wg * target_wgs);
@@ -172,13 +183,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.n = n;
         a.in = in;
         a.out = out;
-        a.rpw = pick_rpw(n, GCM_WAVES, 64 / L, (uint32_t) cu);
+        const int waves = gcm_waves();
+        a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = kt->capacity;
         a.cipher = (uint32_t) cipher;
-        uint64_t per_wg = (uint64_t) GCM_WAVES * a.rpw;
+        uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         int nr = cipher == TLSREC_CIPHER_AES_128_GCM ? 10 : 14;
-        if (tlsrec__launch_gcm(&a, dec, L, nr, grid, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (tlsrec__launch_gcm(&a, dec, L, nr, waves, grid, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305)) {
         int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;

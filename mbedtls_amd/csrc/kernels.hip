@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
 #include <type_traits>
 
 #include "tlsrec.h"
@@ -97,6 +98,10 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
             const int nk = km.cipher == TLSREC_CIPHER_AES_128_GCM ? 4 : 8;
             aes_key_expand(km.key, nk, st->rk);
             st->nr = (uint32_t) (nk + 6);
+            for (int i = 0; i < 4 * (nk + 7); i++) {
+                const bool middle = i >= 4 && i < 4 * (nk + 6);
+                st->rkr[i] = middle ? __builtin_amdgcn_alignbit(st->rk[i], st->rk[i], 16) : st->rk[i];
+            }
             uint8_t h[16] = { 0 };
             aes_encrypt_bytes(st->rk, nk + 6, h);
             G128 H;
@@ -136,35 +141,6 @@ __device__ __forceinline__ uint32_t ld_u32le(const uint8_t *p)
     return (uint32_t) p[0] | ((uint32_t) p[1] << 8) | ((uint32_t) p[2] << 16) | ((uint32_t) p[3] << 24);
 }
 
-/* Load up to 16 bytes of an inner plaintext / ciphertext block.  `pos` is the
- * offset of the block within the AEAD region [0, aead_len); bytes at
- * [content_len, aead_len) are the TLS 1.3 inner type byte and zero padding
- * (ssl_msg.c:466-491), bytes >= aead_len are zero. */
-__device__ __forceinline__ uint4 load_block(const uint8_t *src, uint32_t pos, uint32_t content_len,
-                                            uint32_t aead_len, uint8_t inner_type, bool aligned)
-{
-    if (aligned && pos + 16 <= content_len) return *reinterpret_cast<const uint4 *>(src + pos);
-    uint32_t w[4] = { 0, 0, 0, 0 };
-    for (int i = 0; i < 16; i++) {
-        uint32_t b = pos + i, v = 0;
-        if (b < content_len) v = src[b];
-        else if (b == content_len && b < aead_len) v = inner_type;
-        w[i >> 2] |= v << (8 * (i & 3));
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-__device__ __forceinline__ void store_block(uint8_t *dst, uint32_t pos, uint32_t len, uint4 v, bool aligned)
-{
-    if (aligned && pos + 16 <= len) {
-        *reinterpret_cast<uint4 *>(dst + pos) = v;
-        return;
-    }
-    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
-    for (int i = 0; i < 16; i++)
-        if (pos + i < len) dst[pos + i] = (uint8_t) (w[i >> 2] >> (8 * (i & 3)));
-}
-
 /* zero the bytes of a block at or beyond `len` */
 __device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t pos, uint32_t len)
 {
@@ -177,6 +153,55 @@ __device__ __forceinline__ uint4 mask_block(uint4 v, uint32_t pos, uint32_t len)
         w[i] &= m;
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+/* Load one 16-byte block of the AEAD input.  `pos` is the block offset within
+ * the AEAD region [0, aead_len); bytes at [content_len, aead_len) are the
+ * TLS 1.3 inner type byte followed by zero padding (ssl_msg.c:466-491), bytes
+ * >= aead_len are zero.  With a 16-B aligned region the full 16-byte read is
+ * always inside the record buffer: the tag (decrypt) or the tag room checked
+ * at ssl_msg.c:995-998 (encrypt) follows the AEAD data. */
+__device__ __forceinline__ uint4 load_block(const uint8_t *src, uint32_t pos, uint32_t content_len,
+                                            uint32_t aead_len, uint8_t inner_type, bool aligned)
+{
+    uint4 v;
+    if (aligned) {
+        v = *reinterpret_cast<const uint4 *>(src + pos);
+        if (pos + 16 <= content_len) return v;
+        v = mask_block(v, pos, content_len);
+    } else {
+        uint32_t w[4] = { 0, 0, 0, 0 };
+#pragma unroll 1
+        for (uint32_t i = 0; i < 16; i++) {
+            if (pos + i < content_len) w[i >> 2] |= (uint32_t) src[pos + i] << (8 * (i & 3));
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (content_len >= pos && content_len < pos + 16 && content_len < aead_len) {
+        const uint32_t e = content_len - pos, sh = 8 * (e & 3), t = (uint32_t) inner_type << sh;
+        if ((e >> 2) == 0) v.x |= t;
+        else if ((e >> 2) == 1) v.y |= t;
+        else if ((e >> 2) == 2) v.z |= t;
+        else v.w |= t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void store_block(uint8_t *dst, uint32_t pos, uint32_t len, uint4 v, bool aligned)
+{
+    if (aligned && pos + 16 <= len) {
+        *reinterpret_cast<uint4 *>(dst + pos) = v;
+        return;
+    }
+    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll 1
+    for (uint32_t i = 0; i < 16; i++) {
+        if (pos + i < len) {
+            const uint32_t d = i >> 2;
+            const uint32_t wd = d == 0 ? w[0] : (d == 1 ? w[1] : (d == 2 ? w[2] : w[3]));
+            dst[pos + i] = (uint8_t) (wd >> (8 * (i & 3)));
+        }
+    }
 }
 
 /* (index+1) << 8 | value of the last non-zero byte of a block, or 0 */
@@ -292,15 +317,45 @@ template <> struct Log2<16> { static constexpr int v = 4; };
 template <> struct Log2<32> { static constexpr int v = 5; };
 template <> struct Log2<64> { static constexpr int v = 6; };
 
-template <int L>
+template <int L, int W>
 struct GcmLds {
     static constexpr int NT = Log2<L>::v + 1;           /* GHASH tables H^1 .. H^L */
     static constexpr int GH = 0;
     static constexpr int AES = NT * 8192;               /* T0/T1 x 32 copies */
-    static constexpr int EJ0 = AES + 65536;             /* 16 waves x 64 x 16 B */
-    static constexpr int RK = EJ0 + GCM_WAVES * 64 * 16;/* 60 round-key words */
-    static constexpr int CTL = RK + 256;
+    static constexpr int EJ0 = AES + 65536;             /* W waves x 64 x 16 B */
+    static constexpr int CTL = EJ0 + W * 64 * 16;
     static constexpr int BYTES = CTL + 16;
+};
+
+/* Per-record state that the AEAD loop reads (kept small: it lives in
+ * VGPRs across the loop). */
+struct GcmJob {
+    bool run, aligned, tls13;
+    uint8_t inner_type;
+    uint32_t aead_len, content_len, aad_len;
+    uint32_t nw0, nw1, nw2;
+    uint4 aadw;
+    const uint8_t *src;
+    uint8_t *dst;
+
+    template <bool DEC>
+    __device__ __forceinline__ void setup(const tlsrec_plan &p, const tlsrec_batch_rec &d, const uint8_t *in,
+                                          uint8_t *out)
+    {
+        uint32_t nw[3];
+        nonce_words<DEC>(p, d, in, nw);
+        nw0 = nw[0]; nw1 = nw[1]; nw2 = nw[2];
+        aadw = aad_words(p);
+        aad_len = p.aad_len;
+        aead_len = p.aead_len;
+        content_len = DEC ? p.aead_len : p.content_len;
+        inner_type = p.inner_type;
+        tls13 = p.tls13;
+        src = in + d.buf_off + p.aead_pos;
+        dst = out + d.buf_off + p.aead_pos;
+        aligned = ((((uintptr_t) src) | ((uintptr_t) dst)) & 15) == 0;
+        run = true;
+    }
 };
 
 /* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0 */
@@ -316,10 +371,11 @@ __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
     }
 }
 
-template <int L, int NR, bool DEC>
-__global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
+template <int L, int NR, bool DEC, int W, int B>
+__global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 {
-    using LY = GcmLds<L>;
+    using LY = GcmLds<L, W>;
+    constexpr int NTHR = W * 64;
     constexpr int LOGL = Log2<L>::v;
     constexpr int R = 64 / L;
     /* the kernel's only LDS object, so it starts at LDS address 0 and every
@@ -330,9 +386,9 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
     const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
     uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + LY::CTL);
 
-    aes_fill_tables(lds + LY::AES, tid, GCM_THREADS);
+    aes_fill_tables(lds + LY::AES, tid, NTHR);
 
-    const uint64_t chunk = ((uint64_t) blockIdx.x * GCM_WAVES + wave) * a.rpw;
+    const uint64_t chunk = ((uint64_t) blockIdx.x * W + wave) * a.rpw;
     /* pass membership: lane l tracks record chunk + l of the pre-pass */
     uint32_t my_slot = 0xffffffffu;
     {
@@ -356,10 +412,10 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
         {
             const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
             uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
-            for (int i = tid; i < LY::NT * 512; i += GCM_THREADS) dst[i] = src[i];
+            for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
         }
         __syncthreads();
-        const uint32_t *rk = a.slots[s].rk;    /* uniform: s_load into SGPRs */
+        const uint32_t *rk = a.slots[s].rkr;   /* uniform: s_load into SGPRs */
         const tlsrec_key_material km = a.slots[s].km;
 
         /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
@@ -385,81 +441,85 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
             const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
             const bool active = slot_in_chunk < a.rpw && owner_slot == s;
             const uint64_t ridx = chunk + slot_in_chunk;
-            tlsrec_batch_rec d;
-            tlsrec_plan p;
-            bool run = false;
+            /* Only what the AEAD loop needs stays live across it; the plan is
+             * re-derived from the (cached) descriptor afterwards. */
+            GcmJob jb;
+            jb.run = false;
             if (active) {
-                d = a.recs[ridx];
+                const tlsrec_batch_rec d = a.recs[ridx];
+                tlsrec_plan p;
                 make_plan<DEC>(p, d, km);
                 if (p.status != 0) {
                     if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
                 } else {
-                    run = true;
+                    jb.setup<DEC>(p, d, a.in, a.out);
                 }
             }
-            const uint32_t aead_len = run ? p.aead_len : 0;
-            const uint32_t m = (aead_len + 15) >> 4;                 /* GHASH C blocks */
+            const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
             const uint32_t mm = m ? m : 1;
-            const uint32_t z = (L - mm % L) % L;
-            const uint32_t J = run ? (mm + z) / L : 0;
+            constexpr uint32_t BL = (uint32_t) (B * L);
+            const uint32_t z = (BL - mm % BL) % BL;                    /* front padding */
+            const uint32_t J = jb.run ? (mm + z) / BL : 0;
             const uint32_t Jmax = wave_max(J);
-            uint32_t nw[3] = { 0, 0, 0 };
-            uint4 aadw = make_uint4(0, 0, 0, 0);
-            const uint8_t *src = a.in;
-            uint8_t *dst = a.out;
-            bool aligned = false;
-            uint32_t content_len = 0;
-            if (run) {
-                nonce_words<DEC>(p, d, a.in, nw);
-                aadw = aad_words(p);
-                src = a.in + d.buf_off + p.aead_pos;
-                dst = a.out + d.buf_off + p.aead_pos;
-                aligned = ((((uintptr_t) src) | ((uintptr_t) dst)) & 15) == 0;
-                content_len = DEC ? aead_len : p.content_len;
-            }
-            uint4 Y = (run && m > 0 && (uint32_t) q == z) ? aadw : make_uint4(0, 0, 0, 0);
+            /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H, so
+             * every step below is the same Horner step Y = Y*H^L ^ X. */
+            const uint4 aadh = gmul<0>(lds, jb.aadw);
+            uint4 Y = make_uint4(0, 0, 0, 0);
             uint32_t nzkey = 0;
-            /* one step: AES-CTR block c = L*j + q - z, GHASH Horner Y = Y*P ^ X.
-             * P = H for j = 0 (only the C_0 lane holds the AAD there), H^L after;
-             * the table index must stay a compile-time constant so every table
-             * read is one ds_read_b128 with an immediate offset. */
-            auto step = [&](uint32_t j, auto pic) {
-                constexpr int PI = decltype(pic)::value;
-                const int32_t c = (int32_t) (L * j + q) - (int32_t) z;
-                const bool live = run && j < J;
-                const bool valid = live && c >= 0 && (uint32_t) c < m;
-                const uint32_t ctr = (uint32_t) c + 2u;
-                uint4 ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(ctr)));
-                uint4 X = make_uint4(0, 0, 0, 0);
-                if (valid) {
-                    const uint32_t pos = (uint32_t) c * 16;
-                    uint4 blk = load_block(src, pos, content_len, aead_len, p.inner_type, aligned);
-                    uint4 o = mask_block(xor4(blk, ks), pos, aead_len);
-                    store_block(dst, pos, aead_len, o, aligned);
-                    X = DEC ? blk : o;
-                    if (DEC && p.tls13) {
-                        uint32_t k = last_nonzero_key(o, pos);
-                        if (k) nzkey = k;
-                    }
+            for (uint32_t j = 0; j < Jmax; j++) {
+                const bool live = jb.run && j < J;
+                uint4 X[B];
+                int32_t cc[B];
+                bool valid[B];
+                uint4 blk[B];
+#pragma unroll
+                for (int b = 0; b < B; b++) {
+                    cc[b] = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                    valid[b] = live && cc[b] >= 0 && (uint32_t) cc[b] < m;
+                    blk[b] = valid[b] ? load_block(jb.src, (uint32_t) cc[b] * 16, jb.content_len, jb.aead_len,
+                                                   jb.inner_type, jb.aligned)
+                                      : make_uint4(0, 0, 0, 0);
                 }
-                if (live && m == 0 && c == 0) X = aadw;
-                uint4 Yn = xor4(gmul<PI>(lds, Y), X);
+                uint4 ks[B];
+#pragma unroll
+                for (int b = 0; b < B; b++)
+                    ks[b] = aes_encrypt<NR, LY::AES>(lds, lanebase, rk,
+                                                     make_uint4(jb.nw0, jb.nw1, jb.nw2, bswap32((uint32_t) cc[b] + 2u)));
+#pragma unroll
+                for (int b = 0; b < B; b++) {
+                    X[b] = make_uint4(0, 0, 0, 0);
+                    if (valid[b]) {
+                        const uint32_t pos = (uint32_t) cc[b] * 16;
+                        uint4 o = mask_block(xor4(blk[b], ks[b]), pos, jb.aead_len);
+                        store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
+                        X[b] = DEC ? blk[b] : o;
+                        if (DEC && jb.tls13) {
+                            uint32_t k = last_nonzero_key(o, pos);
+                            if (k) nzkey = k;
+                        }
+                        if (cc[b] == 0) X[b] = xor4(X[b], aadh);
+                    }
+                    if (live && m == 0 && cc[b] == 0) X[b] = jb.aadw;
+                }
+                uint4 Yn = Y;
+#pragma unroll
+                for (int b = 0; b < B; b++) Yn = xor4(gmul<LOGL>(lds, Yn), X[b]);
                 if (live) Y = Yn;
-            };
-            if (Jmax > 0) step(0u, std::integral_constant<int, 0>{});
-            for (uint32_t j = 1; j < Jmax; j++) step(j, std::integral_constant<int, LOGL>{});
+            }
             /* tree: sum_q Y_q H^(L-q) */
             Y = gtree<L / 2>(lds, Y, lane);
             Y = gmul<0>(lds, Y);                                     /* T */
-            const uint32_t alen = run ? p.aad_len : 0;
-            uint4 lenw = make_uint4(0, bswap32(alen * 8), 0, bswap32(aead_len * 8));
+            uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
             Y = gmul<0>(lds, xor4(Y, lenw));                         /* GHASH */
-            if (!run) continue;
+            if (!jb.run) continue;
             const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
             const uint4 tag = xor4(Y, ej0);
+            const tlsrec_batch_rec d = a.recs[ridx];
+            tlsrec_plan p;
+            make_plan<DEC>(p, d, km);
             if (!DEC) {
                 if (q == 0) {
-                    store_block(dst, aead_len, aead_len + 16, tag, false);
+                    store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
                     if (p.explicit_iv && p.post_status == 0) {
                         uint8_t *e = a.out + d.buf_off + p.data_offset;
                         for (int i = 0; i < 8; i++) e[i] = d.ctr[i];
@@ -473,7 +533,7 @@ __global__ __launch_bounds__(GCM_THREADS) void tlsrec_gcm_kernel(GcmArgs a)
                     a.res[ridx] = r;
                 }
             } else {
-                uint4 want = load_block(src, aead_len, aead_len + 16, aead_len + 16, 0, false);
+                uint4 want = load_block(jb.src, jb.aead_len, jb.aead_len + 16, jb.aead_len + 16, 0, false);
                 uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
                 diff = __shfl(diff, lane - q);                        /* group leader's verdict */
                 uint32_t key = group_max<L>(nzkey);
@@ -718,17 +778,23 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
 /* ======================================================================
  * Launchers
  * ==================================================================== */
-template <int L, int NR, bool DEC>
+template <int L, int NR, bool DEC, int W>
 static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
 {
-    hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC>), dim3(grid), dim3(GCM_THREADS), 0, st, a);
+    /* 16 waves x 1 block per lane, or 8 waves x 2 independent blocks per lane */
+    if constexpr (W == 8)
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 8, 2>), dim3(grid), dim3(8 * 64), 0, st, a);
+    else
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 16, 1>), dim3(grid), dim3(16 * 64), 0, st, a);
     return hipGetLastError();
 }
 
 template <int L, bool DEC>
-static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, uint32_t grid, hipStream_t st)
+static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t grid, hipStream_t st)
 {
-    return nr == 10 ? launch_gcm_t<L, 10, DEC>(a, grid, st) : launch_gcm_t<L, 14, DEC>(a, grid, st);
+    if (waves == 8)
+        return nr == 10 ? launch_gcm_t<L, 10, DEC, 8>(a, grid, st) : launch_gcm_t<L, 14, DEC, 8>(a, grid, st);
+    return nr == 10 ? launch_gcm_t<L, 10, DEC, 16>(a, grid, st) : launch_gcm_t<L, 14, DEC, 16>(a, grid, st);
 }
 
 template <int L, bool DEC>
@@ -750,13 +816,14 @@ extern "C" hipError_t tlsrec__launch_keysetup(SlotState *slots, uint4 *ghtab, co
     return hipGetLastError();
 }
 
-extern "C" hipError_t tlsrec__launch_gcm(const GcmArgs *a, int dec, int lanes, int nr, uint32_t grid, hipStream_t st)
+extern "C" hipError_t tlsrec__launch_gcm(const GcmArgs *a, int dec, int lanes, int nr, int waves, uint32_t grid,
+                                         hipStream_t st)
 {
     switch (lanes) {
-        case 4: return dec ? launch_gcm_nr<4, true>(*a, nr, grid, st) : launch_gcm_nr<4, false>(*a, nr, grid, st);
-        case 8: return dec ? launch_gcm_nr<8, true>(*a, nr, grid, st) : launch_gcm_nr<8, false>(*a, nr, grid, st);
-        case 16: return dec ? launch_gcm_nr<16, true>(*a, nr, grid, st) : launch_gcm_nr<16, false>(*a, nr, grid, st);
-        case 64: return dec ? launch_gcm_nr<64, true>(*a, nr, grid, st) : launch_gcm_nr<64, false>(*a, nr, grid, st);
+        case 4: return dec ? launch_gcm_nr<4, true>(*a, nr, waves, grid, st) : launch_gcm_nr<4, false>(*a, nr, waves, grid, st);
+        case 8: return dec ? launch_gcm_nr<8, true>(*a, nr, waves, grid, st) : launch_gcm_nr<8, false>(*a, nr, waves, grid, st);
+        case 16: return dec ? launch_gcm_nr<16, true>(*a, nr, waves, grid, st) : launch_gcm_nr<16, false>(*a, nr, waves, grid, st);
+        case 64: return dec ? launch_gcm_nr<64, true>(*a, nr, waves, grid, st) : launch_gcm_nr<64, false>(*a, nr, waves, grid, st);
         default: return hipErrorInvalidValue;
     }
 }

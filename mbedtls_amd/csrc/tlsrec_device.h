@@ -53,6 +53,11 @@ __device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+/* gfx950 v_bitop3_b32: one VALU op for a ^ b ^ c */
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 /* ---------------- LDS T-tables ----------------------------------------- */
 /* Entry x of table j (j = 0: T0 = (2s,s,s,3s), j = 1: T1 = rotl8(T0)),
@@ -87,7 +92,11 @@ __device__ __forceinline__ uint32_t tlook(const uint8_t *lds, uint32_t w, uint32
 }
 
 /* AES-128 (NR=10) / AES-256 (NR=14) forward cipher of one block per lane.
- * Words are little-endian columns: byte r of word c is row r of column c. */
+ * Words are little-endian columns: byte r of word c is row r of column c.
+ * `rk` holds the key schedule in the engine's "rotated" form: words of the
+ * middle rounds 1..NR-1 are stored rotr16(rk) so that each output column is
+ *     xor3(T0[a], T1[b], rotl16(xor3(T0[c], T1[d], rotr16(rk))))
+ * = 4 lookups + 3 VALU ops (rotl16(x ^ rotr16(k)) = rotl16(x) ^ k). */
 template <int NR, int AES_OFF>
 __device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk,
                                              uint4 in)
@@ -95,14 +104,14 @@ __device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, co
     uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
 #pragma unroll
     for (int r = 1; r < NR; r++) {
-        uint32_t t0 = tlook<AES_OFF>(lds, s0, lb, 0, 0) ^ tlook<AES_OFF>(lds, s1, lb, 1, 1) ^
-                      rotl16(tlook<AES_OFF>(lds, s2, lb, 2, 0) ^ tlook<AES_OFF>(lds, s3, lb, 3, 1)) ^ rk[4 * r + 0];
-        uint32_t t1 = tlook<AES_OFF>(lds, s1, lb, 0, 0) ^ tlook<AES_OFF>(lds, s2, lb, 1, 1) ^
-                      rotl16(tlook<AES_OFF>(lds, s3, lb, 2, 0) ^ tlook<AES_OFF>(lds, s0, lb, 3, 1)) ^ rk[4 * r + 1];
-        uint32_t t2 = tlook<AES_OFF>(lds, s2, lb, 0, 0) ^ tlook<AES_OFF>(lds, s3, lb, 1, 1) ^
-                      rotl16(tlook<AES_OFF>(lds, s0, lb, 2, 0) ^ tlook<AES_OFF>(lds, s1, lb, 3, 1)) ^ rk[4 * r + 2];
-        uint32_t t3 = tlook<AES_OFF>(lds, s3, lb, 0, 0) ^ tlook<AES_OFF>(lds, s0, lb, 1, 1) ^
-                      rotl16(tlook<AES_OFF>(lds, s1, lb, 2, 0) ^ tlook<AES_OFF>(lds, s2, lb, 3, 1)) ^ rk[4 * r + 3];
+        uint32_t t0 = xor3(tlook<AES_OFF>(lds, s0, lb, 0, 0), tlook<AES_OFF>(lds, s1, lb, 1, 1),
+                           rotl16(xor3(tlook<AES_OFF>(lds, s2, lb, 2, 0), tlook<AES_OFF>(lds, s3, lb, 3, 1), rk[4 * r + 0])));
+        uint32_t t1 = xor3(tlook<AES_OFF>(lds, s1, lb, 0, 0), tlook<AES_OFF>(lds, s2, lb, 1, 1),
+                           rotl16(xor3(tlook<AES_OFF>(lds, s3, lb, 2, 0), tlook<AES_OFF>(lds, s0, lb, 3, 1), rk[4 * r + 1])));
+        uint32_t t2 = xor3(tlook<AES_OFF>(lds, s2, lb, 0, 0), tlook<AES_OFF>(lds, s3, lb, 1, 1),
+                           rotl16(xor3(tlook<AES_OFF>(lds, s0, lb, 2, 0), tlook<AES_OFF>(lds, s1, lb, 3, 1), rk[4 * r + 2])));
+        uint32_t t3 = xor3(tlook<AES_OFF>(lds, s3, lb, 0, 0), tlook<AES_OFF>(lds, s0, lb, 1, 1),
+                           rotl16(xor3(tlook<AES_OFF>(lds, s1, lb, 2, 0), tlook<AES_OFF>(lds, s2, lb, 3, 1), rk[4 * r + 3])));
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     /* last round: S[x] is byte 1 (and byte 2) of T0[x] */
@@ -116,7 +125,7 @@ __device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, co
         uint32_t d3 = tlook<AES_OFF>(lds, s[(c + 3) & 3], lb, 3, 0);
         uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0501u);   /* [a.b1, b.b1, 0, 0] */
         uint32_t hi = __builtin_amdgcn_perm(d3, d2, 0x06020C0Cu);  /* [0, 0, d2.b2, d3.b2] */
-        o[c] = (lo | hi) ^ rk[4 * NR + c];
+        o[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);   /* (lo | hi) ^ k */
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
@@ -139,11 +148,15 @@ __device__ __forceinline__ uint4 gmul(const uint8_t *lds, uint4 y)
             uint32_t alo = (e == 0) ? ((w[d] << 4) & 0xf0u) : ((w[d] >> (8 * e - 4)) & 0xf0u);
             uint4 th = *reinterpret_cast<const uint4 *>(lds + ahi + PI * 8192 + (2 * b) * 256);
             uint4 tl = *reinterpret_cast<const uint4 *>(lds + alo + PI * 8192 + (2 * b + 1) * 256);
-            acc.x ^= th.x ^ tl.x;
-            acc.y ^= th.y ^ tl.y;
-            acc.z ^= th.z ^ tl.z;
-            acc.w ^= th.w ^ tl.w;
+            acc.x = xor3(acc.x, th.x, tl.x);
+            acc.y = xor3(acc.y, th.y, tl.y);
+            acc.z = xor3(acc.z, th.z, tl.z);
+            acc.w = xor3(acc.w, th.w, tl.w);
         }
+        /* at most 8 table reads (32 VGPRs) in flight: the opaque acc + memory
+         * clobber keeps the next group's ds_read_b128 below this group's XORs
+         * (otherwise all 32 reads are hoisted and the multiply needs 128 VGPRs) */
+        asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w) : : "memory");
     }
     return acc;
 }

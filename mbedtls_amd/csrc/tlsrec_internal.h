@@ -14,20 +14,20 @@ namespace tlsrec {
 constexpr int KEY_TABLES = 7;                       /* H^1, H^2, ..., H^64 */
 constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512;   /* uint4 entries per slot (56 KiB) */
 
-constexpr int GCM_THREADS = 1024;                   /* 16 waves, one workgroup per CU */
-constexpr int GCM_WAVES = GCM_THREADS / 64;
+constexpr int GCM_WAVES = 16;                       /* default waves per workgroup (one WG per CU) */
 constexpr int CP_THREADS = 256;
 constexpr int CP_WAVES = CP_THREADS / 64;
 
-/* Expanded per-slot state, 512 bytes. */
+/* Expanded per-slot state, 1024 bytes. */
 struct SlotState {
     tlsrec_key_material km;   /* raw material as loaded */
     uint32_t rk[60];          /* AES round keys, little-endian column words */
+    uint32_t rkr[60];         /* same, middle rounds 1..NR-1 stored rotr16 (aes_encrypt) */
     uint32_t nr;              /* 10 / 14, 0 for ChaCha20-Poly1305 */
     uint8_t h[16];            /* H = E_K(0^128) */
-    uint8_t pad[512 - 64 - 240 - 4 - 16];
+    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16];
 };
-static_assert(sizeof(SlotState) == 512, "SlotState layout");
+static_assert(sizeof(SlotState) == 1024, "SlotState layout");
 static_assert(sizeof(tlsrec_key_material) == 64, "key material layout");
 static_assert(sizeof(tlsrec_batch_rec) == 40, "batch record layout");
 static_assert(sizeof(tlsrec_batch_res) == 16, "batch result layout");
@@ -61,7 +61,7 @@ struct CpArgs {
 extern "C" {
 hipError_t tlsrec__launch_keysetup(tlsrec::SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
                                    uint32_t first, uint32_t count, hipStream_t st);
-hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int nr, uint32_t grid,
+hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int nr, int waves, uint32_t grid,
                               hipStream_t st);
 hipError_t tlsrec__launch_chachapoly(const tlsrec::CpArgs *a, int dec, int lanes, uint32_t grid,
                                      hipStream_t st);
