@@ -415,7 +415,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
         }
         __syncthreads();
-        const uint32_t *rk = a.slots[s].rkr;   /* uniform: s_load into SGPRs */
+        /* Round keys through the constant address space: scalar loads.  (Read
+         * through a.slots they compile to vector loads + vmcnt(0) waits in
+         * every round, since the kernel's own stores might alias the table.) */
+        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) a.slots[s].rkr;
         const tlsrec_key_material km = a.slots[s].km;
 
         /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
@@ -464,47 +467,66 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H, so
              * every step below is the same Horner step Y = Y*H^L ^ X. */
             const uint4 aadh = gmul<0>(lds, jb.aadw);
-            uint4 Y = make_uint4(0, 0, 0, 0);
-            uint32_t nzkey = 0;
-            for (uint32_t j = 0; j < Jmax; j++) {
-                const bool live = jb.run && j < J;
-                uint4 X[B];
-                int32_t cc[B];
-                bool valid[B];
-                uint4 blk[B];
+            /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
+             * does not depend on step j's keystream, so its table reads share
+             * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
+            uint4 Z = make_uint4(0, 0, 0, 0), Xp = make_uint4(0, 0, 0, 0);
+            /* TLS 1.3 inner type: position + 1 of the last non-zero output block */
+            uint32_t nzpos = 0;
+            /* a readable 16-byte address for lanes with nothing to load */
+            const uint8_t *safe = jb.run ? jb.src : reinterpret_cast<const uint8_t *>(a.recs);
+            auto steps = [&](auto cached) {
+                constexpr bool CACHED = decltype(cached)::value;
+                CtrCache ccache;
+                if constexpr (CACHED) ccache = ctr_cache<LY::AES>(lds, lanebase, rk, jb.nw0, jb.nw1, jb.nw2);
+                for (uint32_t j = 0; j < Jmax; j++) {
+                    const bool live = jb.run && j < J;
 #pragma unroll
-                for (int b = 0; b < B; b++) {
-                    cc[b] = (int32_t) (BL * j + L * b + q) - (int32_t) z;
-                    valid[b] = live && cc[b] >= 0 && (uint32_t) cc[b] < m;
-                    blk[b] = valid[b] ? load_block(jb.src, (uint32_t) cc[b] * 16, jb.content_len, jb.aead_len,
-                                                   jb.inner_type, jb.aligned)
-                                      : make_uint4(0, 0, 0, 0);
-                }
-                uint4 ks[B];
-#pragma unroll
-                for (int b = 0; b < B; b++)
-                    ks[b] = aes_encrypt<NR, LY::AES>(lds, lanebase, rk,
-                                                     make_uint4(jb.nw0, jb.nw1, jb.nw2, bswap32((uint32_t) cc[b] + 2u)));
-#pragma unroll
-                for (int b = 0; b < B; b++) {
-                    X[b] = make_uint4(0, 0, 0, 0);
-                    if (valid[b]) {
-                        const uint32_t pos = (uint32_t) cc[b] * 16;
-                        uint4 o = mask_block(xor4(blk[b], ks[b]), pos, jb.aead_len);
-                        store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
-                        X[b] = DEC ? blk[b] : o;
-                        if (DEC && jb.tls13) {
-                            uint32_t k = last_nonzero_key(o, pos);
-                            if (k) nzkey = k;
+                    for (int b = 0; b < B; b++) {
+                        const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                        const bool valid = live && cc >= 0 && (uint32_t) cc < m;
+                        const uint32_t pos = (uint32_t) cc * 16;
+                        /* full, aligned interior block: plain 16-byte load/store */
+                        const bool fast = valid && jb.aligned && pos + 16 <= jb.content_len;
+                        uint4 blk = *reinterpret_cast<const uint4 *>(fast ? jb.src + pos : safe);
+                        uint4 ks, Zn;
+                        const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
+                        if constexpr (CACHED) {
+                            aes_ghash<NR, LY::AES, LOGL>(lds, lanebase, rk, ccache, ctrw, xor4(Z, Xp), ks, Zn);
+                        } else {
+                            ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                            Zn = gmul<LOGL>(lds, xor4(Z, Xp));
                         }
-                        if (cc[b] == 0) X[b] = xor4(X[b], aadh);
+                        uint4 X = make_uint4(0, 0, 0, 0);
+                        if (fast) {
+                            const uint4 o = xor4(blk, ks);
+                            *reinterpret_cast<uint4 *>(jb.dst + pos) = o;
+                            X = DEC ? blk : o;
+                            if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                        } else if (valid) {
+                            blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type, jb.aligned);
+                            const uint4 o = mask_block(xor4(blk, ks), pos, jb.aead_len);
+                            store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
+                            X = DEC ? blk : o;
+                            if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                        }
+                        if (valid && cc == 0) X = xor4(X, aadh);
+                        if (live && m == 0 && cc == 0) X = jb.aadw;
+                        if (live) { Z = Zn; Xp = X; }
                     }
-                    if (live && m == 0 && cc[b] == 0) X[b] = jb.aadw;
                 }
-                uint4 Yn = Y;
-#pragma unroll
-                for (int b = 0; b < B; b++) Yn = xor4(gmul<LOGL>(lds, Yn), X[b]);
-                if (live) Y = Yn;
+            };
+            /* counters stay below 2^16 (any TLS record): cached rounds 1-2 */
+            if (wave_max(m) + 2 < 65536u)
+                steps(std::integral_constant<bool, true>());
+            else
+                steps(std::integral_constant<bool, false>());
+            uint4 Y = xor4(Z, Xp);
+            uint32_t nzkey = 0;
+            if (DEC && jb.tls13 && nzpos) {
+                /* the lane's last non-zero plaintext block, as written above */
+                const uint32_t pos = nzpos - 1;
+                nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
             }
             /* tree: sum_q Y_q H^(L-q) */
             Y = gtree<L / 2>(lds, Y, lane);

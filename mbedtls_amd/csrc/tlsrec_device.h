@@ -52,6 +52,7 @@ __constant__ const SboxGen kSbox{};
 __device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff; }
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t rotr16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 /* gfx950 v_bitop3_b32: one VALU op for a ^ b ^ c */
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
@@ -82,6 +83,9 @@ __device__ __forceinline__ void aes_fill_tables(uint8_t *lds_aes, int tid, int n
 
 /* v_perm selector: byte0 <- lanebase byte 0 (= (lane&31)*4), byte1 <- state
  * byte k, bytes 2,3 <- 0.  The result is the LDS address x*256 + (lane&31)*4. */
+/* constant address space: read-only for the kernel's lifetime, scalar loads */
+typedef const __attribute__((address_space(4))) uint32_t kconst_u32;
+
 #define TLSREC_PSEL(k) (0x0C0C0000u | ((4u + (k)) << 8))
 
 template <int AES_OFF>
@@ -97,8 +101,8 @@ __device__ __forceinline__ uint32_t tlook(const uint8_t *lds, uint32_t w, uint32
  * middle rounds 1..NR-1 are stored rotr16(rk) so that each output column is
  *     xor3(T0[a], T1[b], rotl16(xor3(T0[c], T1[d], rotr16(rk))))
  * = 4 lookups + 3 VALU ops (rotl16(x ^ rotr16(k)) = rotl16(x) ^ k). */
-template <int NR, int AES_OFF>
-__device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, const uint32_t *__restrict__ rk,
+template <int NR, int AES_OFF, typename RK>
+__device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, RK rk,
                                              uint4 in)
 {
     uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
@@ -134,7 +138,10 @@ __device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, co
 /* Table PI (a power of H) holds T_k[n] = sum_{i<4} bit(3-i of n) * P * x^(4k+i)
  * at PI*8192 + k*256 + n*16, as the 16-byte GCM string.  Window k = 2b is the
  * high nibble of byte b, k = 2b+1 its low nibble. */
-template <int PI>
+/* G = table-read groups per multiply (8 reads each when G = 4); MEM = whether
+ * a group boundary also orders memory (stops later LDS reads -- including
+ * unrelated AES lookups -- from moving above it). */
+template <int PI, int G = 4, bool MEM = true>
 __device__ __forceinline__ uint4 gmul(const uint8_t *lds, uint4 y)
 {
     const uint32_t w[4] = { y.x, y.y, y.z, y.w };
@@ -153,12 +160,147 @@ __device__ __forceinline__ uint4 gmul(const uint8_t *lds, uint4 y)
             acc.z = xor3(acc.z, th.z, tl.z);
             acc.w = xor3(acc.w, th.w, tl.w);
         }
-        /* at most 8 table reads (32 VGPRs) in flight: the opaque acc + memory
-         * clobber keeps the next group's ds_read_b128 below this group's XORs
-         * (otherwise all 32 reads are hoisted and the multiply needs 128 VGPRs) */
-        asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w) : : "memory");
+        /* bound the table reads in flight: the opaque acc (+ memory clobber)
+         * keeps the next group's ds_read_b128 below this group's XORs;
+         * otherwise all 32 reads are hoisted and the multiply needs 128 VGPRs */
+        if ((d + 1) % (4 / G) == 0) {
+            if constexpr (MEM)
+                asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w) : : "memory");
+            else
+                asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w));
+        }
     }
     return acc;
+}
+
+/* Part of gmul: the table reads of bytes e0 .. e0+NE-1 of 32-bit word d of y. */
+template <int PI, int NE = 4>
+__device__ __forceinline__ void gmul_word(const uint8_t *lds, uint32_t wd, int d, uint4 &acc, int e0 = 0)
+{
+#pragma unroll
+    for (int i = 0; i < NE; i++) {
+        const int e = e0 + i;
+        const int b = 4 * d + e;
+        uint32_t ahi = (e == 0) ? (wd & 0xf0u) : ((wd >> (8 * e)) & 0xf0u);
+        uint32_t alo = (e == 0) ? ((wd << 4) & 0xf0u) : ((wd >> (8 * e - 4)) & 0xf0u);
+        uint4 th = *reinterpret_cast<const uint4 *>(lds + ahi + PI * 8192 + (2 * b) * 256);
+        uint4 tl = *reinterpret_cast<const uint4 *>(lds + alo + PI * 8192 + (2 * b + 1) * 256);
+        acc.x = xor3(acc.x, th.x, tl.x);
+        acc.y = xor3(acc.y, th.y, tl.y);
+        acc.z = xor3(acc.z, th.z, tl.z);
+        acc.w = xor3(acc.w, th.w, tl.w);
+    }
+}
+
+/* AES middle round r on (s0..s3), rotated round keys (see aes_encrypt). */
+template <int AES_OFF, typename RK>
+__device__ __forceinline__ void aes_round(const uint8_t *lds, uint32_t lb, RK rk, int r,
+                                          uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3)
+{
+    uint32_t t0 = xor3(tlook<AES_OFF>(lds, s0, lb, 0, 0), tlook<AES_OFF>(lds, s1, lb, 1, 1),
+                       rotl16(xor3(tlook<AES_OFF>(lds, s2, lb, 2, 0), tlook<AES_OFF>(lds, s3, lb, 3, 1), rk[4 * r + 0])));
+    uint32_t t1 = xor3(tlook<AES_OFF>(lds, s1, lb, 0, 0), tlook<AES_OFF>(lds, s2, lb, 1, 1),
+                       rotl16(xor3(tlook<AES_OFF>(lds, s3, lb, 2, 0), tlook<AES_OFF>(lds, s0, lb, 3, 1), rk[4 * r + 1])));
+    uint32_t t2 = xor3(tlook<AES_OFF>(lds, s2, lb, 0, 0), tlook<AES_OFF>(lds, s3, lb, 1, 1),
+                       rotl16(xor3(tlook<AES_OFF>(lds, s0, lb, 2, 0), tlook<AES_OFF>(lds, s1, lb, 3, 1), rk[4 * r + 2])));
+    uint32_t t3 = xor3(tlook<AES_OFF>(lds, s3, lb, 0, 0), tlook<AES_OFF>(lds, s0, lb, 1, 1),
+                       rotl16(xor3(tlook<AES_OFF>(lds, s1, lb, 2, 0), tlook<AES_OFF>(lds, s2, lb, 3, 1), rk[4 * r + 3])));
+    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+}
+
+/* ---------------- counter-mode round caching -------------------------- *
+ * Within one record the GCM counter block is (N0, N1, N2, BE32(ctr)) with
+ * ctr < 2^16, so after whitening only rows 2 and 3 of column 3 vary: round 1
+ * has one varying lookup in columns 0 and 1 and none in columns 2 and 3, and
+ * round 2 has two varying lookups per column.  ctr_cache() folds everything
+ * else into six per-record words (rotated round-key form, see aes_encrypt):
+ *   t0 = rotl16(k0r ^ T1[s3.b3])          t1 = rotl16(k1r ^ T0[s3.b2])
+ *   u0 = T0[t0.b0] ^ T1[t1.b1] ^ d0       u1 = T0[t1.b0] ^ d1 ^ rotl16(T1[t0.b3])
+ *   u2 = rotl16(T0[t0.b2] ^ T1[t1.b3] ^ d2r)
+ *   u3 = T1[t0.b1] ^ d3 ^ rotl16(T0[t1.b2])
+ * (10 lookups instead of 32 for rounds 1-2). */
+struct CtrCache { uint32_t k0r, k1r, d0, d1, d2r, d3; };
+
+template <int AES_OFF, typename RK>
+__device__ __forceinline__ CtrCache ctr_cache(const uint8_t *lds, uint32_t lb, RK rk, uint32_t n0, uint32_t n1,
+                                              uint32_t n2)
+{
+#define TA(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 0)
+#define TB(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 1)
+    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2], s3 = rk[3];   /* ctr rows 0,1 = 0 */
+    CtrCache c;
+    c.k0r = rotr16(xor3(TA(s0, 0), TB(s1, 1), rotl16(TA(s2, 2) ^ rk[4])));
+    c.k1r = rotr16(xor3(TA(s1, 0), TB(s2, 1), rotl16(TB(s0, 3) ^ rk[5])));
+    const uint32_t t2 = xor3(TA(s2, 0), TB(s3, 1), rotl16(xor3(TA(s0, 2), TB(s1, 3), rk[6])));
+    const uint32_t t3 = xor3(TA(s3, 0), TB(s0, 1), rotl16(xor3(TA(s1, 2), TB(s2, 3), rk[7])));
+    c.d0 = rotl16(xor3(TA(t2, 2), TB(t3, 3), rk[8]));
+    c.d1 = TB(t2, 1) ^ rotl16(TA(t3, 2) ^ rk[9]);
+    c.d2r = rotr16(TA(t2, 0) ^ TB(t3, 1)) ^ rk[10];
+    c.d3 = TA(t3, 0) ^ rotl16(TB(t2, 3) ^ rk[11]);
+    return c;
+#undef TA
+#undef TB
+}
+
+/* Fused counter-block encryption and one GHASH multiply, for a step whose
+ * GHASH input does not depend on this step's keystream:
+ *     ks = E_K(N0, N1, N2, ctrw),  prod = y * P_PI
+ * (ctrw = BE32(ctr) as a little-endian word, ctr < 2^16, rounds 1-2 from `cc`).
+ * The 32 GHASH table reads are issued in 8 groups of 4 (a half word of y),
+ * group g after AES round R0 + g*RS, each sharing its phase with that
+ * round's T-table reads so the LDS sees both streams at once.  The empty
+ * asm statements are the phase boundaries: they re-define the AES state, the
+ * accumulator and the source words still to be read, so no read moves into an
+ * earlier phase (bounded reads in flight and VGPRs, no memory clobber). */
+template <int NR, int AES_OFF, int PI, int R0 = 2, int RS = 1, typename RK>
+__device__ __forceinline__ void aes_ghash(const uint8_t *lds, uint32_t lb, RK rk, const CtrCache &cc, uint32_t ctrw,
+                                          uint4 y, uint4 &ks, uint4 &prod)
+{
+    static_assert(R0 >= 2 && R0 + 7 * RS <= NR - 1, "GHASH groups must fall on middle rounds 2..NR-1");
+#define TA(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 0)
+#define TB(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 1)
+    uint32_t s0, s1, s2, s3;
+    {
+        const uint32_t w3 = ctrw ^ rk[3];
+        const uint32_t t0 = rotl16(cc.k0r ^ TB(w3, 3));
+        const uint32_t t1 = rotl16(cc.k1r ^ TA(w3, 2));
+        s0 = xor3(TA(t0, 0), TB(t1, 1), cc.d0);
+        s1 = xor3(TA(t1, 0), cc.d1, rotl16(TB(t0, 3)));
+        s2 = rotl16(xor3(TA(t0, 2), TB(t1, 3), cc.d2r));
+        s3 = xor3(TB(t0, 1), cc.d3, rotl16(TA(t1, 2)));
+    }
+#undef TA
+#undef TB
+    uint32_t w[4] = { y.x, y.y, y.z, y.w };
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int r = 2; r < NR; r++) {
+        if (r > 2) aes_round<AES_OFF>(lds, lb, rk, r, s0, s1, s2, s3);
+        const int g = (r - R0) / RS;
+        if (r >= R0 && (r - R0) % RS == 0 && g < 8) {
+            gmul_word<PI, 2>(lds, w[g >> 1], g >> 1, acc, 2 * (g & 1));
+            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(acc.x), "+v"(acc.y), "+v"(acc.z),
+                         "+v"(acc.w));
+            /* the words still to be read enter the next phase through the barrier */
+            if (g < 2) asm volatile("" : "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+            else if (g < 4) asm volatile("" : "+v"(w[2]), "+v"(w[3]));
+            else if (g < 6) asm volatile("" : "+v"(w[3]));
+        }
+    }
+    uint32_t o[4];
+    const uint32_t s[4] = { s0, s1, s2, s3 };
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        uint32_t a = tlook<AES_OFF>(lds, s[c], lb, 0, 0);
+        uint32_t b = tlook<AES_OFF>(lds, s[(c + 1) & 3], lb, 1, 0);
+        uint32_t d2 = tlook<AES_OFF>(lds, s[(c + 2) & 3], lb, 2, 0);
+        uint32_t d3 = tlook<AES_OFF>(lds, s[(c + 3) & 3], lb, 3, 0);
+        uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0501u);
+        uint32_t hi = __builtin_amdgcn_perm(d3, d2, 0x06020C0Cu);
+        o[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);
+    }
+    ks = make_uint4(o[0], o[1], o[2], o[3]);
+    prod = acc;
 }
 
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }

@@ -153,3 +153,35 @@ def sealed_records(slots, lengths, seed, head=8, tail=40):
         recs.append(Rec(slot=r.slot, buf=bytearray(o.buf), data_offset=o.data_offset,
                         data_len=o.data_len, ctr=r.ctr, type=o.type, ver=r.ver))
     return recs, pre
+
+
+def gcm_sealed_records(slots, lengths, seed, head=8, tail=40):
+    """GCM records sealed with the oracle's raw AEAD (no OUT_CONTENT_LEN cap,
+    unlike the record-layer encrypt), framed as ssl_msg.c frames them:
+    TLS 1.2 explicit nonce = ctr, AAD = ctr|type|ver|len16(plaintext);
+    TLS 1.3 nonce = iv ^ (0^4|ctr), AAD = 23|ver|len16(ct+tag), inner type byte.
+    Used for records the encrypt side may not produce (counters past 2^16)."""
+    recs = []
+    for i, L in enumerate(lengths):
+        s = i % len(slots)
+        c, v, k, iv, _ = slots[s]
+        payload = prng_bytes(seed + i, L)
+        ctr = int(prng_bytes(seed ^ (i + 77), 8).hex(), 16).to_bytes(8, "big")
+        rtype = 23 if i % 5 else 22
+        if v == M.VERSION_TLS1_3:
+            inner = payload + bytes([rtype])
+            nonce = bytes(a ^ b for a, b in zip(iv[:12], bytes(4) + ctr))
+            aad = bytes([23]) + b"\x03\x03" + ((len(inner) + 16) & 0xffff).to_bytes(2, "big")
+            ct, tag = O.gcm_encrypt(k, nonce, aad, inner)
+            body = ct + tag
+            wire_type = 23
+        else:
+            nonce = iv[:4] + ctr
+            aad = ctr + bytes([rtype]) + b"\x03\x03" + (L & 0xffff).to_bytes(2, "big")
+            ct, tag = O.gcm_encrypt(k, nonce, aad, payload)
+            body = ctr + ct + tag
+            wire_type = rtype
+        buf = bytearray(head + len(body) + tail)
+        buf[head:head + len(body)] = body
+        recs.append(Rec(slot=s, buf=buf, data_offset=head, data_len=len(body), ctr=ctr, type=wire_type))
+    return recs

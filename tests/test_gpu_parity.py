@@ -208,3 +208,26 @@ def test_large_roundtrip_16k():
         for i, r in enumerate(recs):
             o = b.offs[i]
             assert bytes(out2[o:o + 16383]) == bytes(r.buf[:16383])
+
+
+@pytest.mark.parametrize("cipher", [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM], ids=["AES-128-GCM", "AES-256-GCM"])
+def test_gcm_counter_boundary(cipher):
+    """Decrypt of records whose GCM counter passes 2^16 (> 1 MiB of
+    ciphertext) takes the kernel's uncached-round path; lengths straddle the
+    last cached counter.  ssl_decrypt_buf has no size cap of its own (the
+    encrypt side stops at OUT_CONTENT_LEN, ssl_msg.c:831, also checked)."""
+    slots = B.random_slots(77 + cipher, [cipher], [M.VERSION_TLS1_2, M.VERSION_TLS1_3], 2)
+    lengths = [65533 * 16 - 20, 65533 * 16 - 1, 65534 * 16 + 3, 70000 * 16 + 5, 100, 0]
+    recs = B.gcm_sealed_records(slots, lengths, seed=31)
+    b = B.Batch(slots, recs)
+    _, o_stats = b.run_oracle(True)
+    assert o_stats == [0] * len(recs)
+    for lanes in (0, 64):
+        out, res = b.run_gpu(True, lanes=lanes)
+        bad = b.compare(True, out, res)
+        assert not bad, f"lanes={lanes}: " + "; ".join(bad[:5])
+    # encrypt of the same plaintext sizes: BAD_INPUT_DATA above 16384, like the reference
+    pb = B.Batch(slots, B.plaintext_records(slots, lengths, seed=31))
+    out, res = pb.run_gpu(False)
+    assert not pb.compare(False, out, res)
+    assert res["status"].tolist()[:4] == [M.ERR_SSL_BAD_INPUT_DATA] * 4
