@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--align", type=int, default=128, help="record slot alignment in the arena (bytes; 128 = HBM/L2 line)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of the CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", type=int, default=64, help="records spot-checked against the oracle")
@@ -86,7 +87,7 @@ def main():
     ver = M.VERSION_TLS1_3 if tls == "TLS1.3" else M.VERSION_TLS1_2
     inner = inner_len(content, tls)
     wire = inner + 16
-    stride = (wire + 15) // 16 * 16
+    stride = (wire + args.align - 1) // args.align * args.align
     ciphers = {"AES-256-GCM": [M.CIPHER_AES_256_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
                "MIX": [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]}[cname]
     nkeys = min(nkeys, n)
@@ -102,14 +103,16 @@ def main():
         km["taglen"] = 16
         km["key"] = raw[:, :32]
         km["iv"][:, :12] = raw[:, 32:44]
-    keys_dev = torch.from_numpy(km.view(np.uint8).copy()).to(dev)
-    if world > 1:
-        dist.broadcast(keys_dev, src=0)
+    keys_dev = M.broadcast_keys(km, dev)          # RCCL broadcast when world > 1
     kt = M.KeyTable(nkeys)
     kt.load(keys_dev)
 
     # ---- synthetic records (this rank's shard) ---------------------------------
-    shard0 = rank * n
+    # weak scaling: a global stream of n x world records, one contiguous range
+    # per rank (mbedtls_amd.shard); record bytes never leave their GPU
+    sh = M.shard_bounds(n * world, rank, world)
+    assert sh.count == n
+    shard0 = sh.start
     arena = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev)
     recs = M.records(n)
     recs["buf_off"] = np.arange(n, dtype=np.uint64) * stride
@@ -214,13 +217,16 @@ def main():
         alg_per_rec = content + wire + 40 + 16
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
     achieved = alg_per_rec * n / kern_avg_s / 1e9
+    # HBM traffic per launch: PMC FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE
+    # per record, measured by profiles/run_profile.sh on this config and
+    # committed as profiles/traffic_<config>.json, scaled to this launch.
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("records") == n:
-            traffic = tj.get("hbm_bytes_per_launch")
+        if tj.get("direction") == direction and tj.get("record_inner_bytes") == inner:
+            traffic = round(tj["hbm_bytes_per_record"] * n)
 
     steps_s = wall / args.steps
     payload_total = float(n) * inner * world
@@ -245,7 +251,7 @@ def main():
         "data": "synthetic (splitmix64 keys/nonces, uniform random payload; decrypt inputs made by the verified encrypt kernel)",
         "config": {"workload": workload, "config": args.config, "records_per_gpu": n,
                    "record_inner_bytes": inner, "record_wire_bytes": wire, "keys": nkeys,
-                   "lanes_per_record": args.lanes or "auto", "parallelism": f"shard{world}"},
+                   "lanes_per_record": args.lanes or "auto", "slot_align": args.align, "parallelism": f"shard{world}"},
         "records_per_s": round(n * world / steps_s, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

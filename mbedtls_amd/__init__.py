@@ -13,6 +13,7 @@ from ._abi import (CIPHER_AES_128_GCM, CIPHER_AES_256_GCM, CIPHER_CHACHA20_POLY1
 from .batch import (KeyTable, batch_decrypt, batch_encrypt, frame_check, key_material,  # noqa: F401
                     records, results, seq_bytes)
 from .record import Record, Transform, decrypt_buf, encrypt_buf  # noqa: F401
+from .shard import Shard, broadcast_keys, reduce_status, shard_bounds, status_counts  # noqa: F401
 
 
 def device_ok() -> bool:

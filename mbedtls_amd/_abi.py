@@ -92,10 +92,12 @@ def load():
         import torch  # noqa: F401  (shares its HIP runtime with us)
     except Exception:
         pass
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} is missing: build it with `python -m mbedtls_amd.build` "
+    # TLSREC_LIBRARY: an alternative in-tree build of the same ABI (A/B runs)
+    path = os.environ.get("TLSREC_LIBRARY") or LIB_PATH
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: build it with `python -m mbedtls_amd.build` "
                           "(there is no CPU fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(L, name)
         f.restype = res

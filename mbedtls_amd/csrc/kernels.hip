@@ -166,7 +166,7 @@ __device__ __forceinline__ uint4 load_block(const uint8_t *src, uint32_t pos, ui
 {
     uint4 v;
     if (aligned) {
-        v = *reinterpret_cast<const uint4 *>(src + pos);
+        v = gload16(src + pos);
         if (pos + 16 <= content_len) return v;
         v = mask_block(v, pos, content_len);
     } else {
@@ -190,7 +190,7 @@ __device__ __forceinline__ uint4 load_block(const uint8_t *src, uint32_t pos, ui
 __device__ __forceinline__ void store_block(uint8_t *dst, uint32_t pos, uint32_t len, uint4 v, bool aligned)
 {
     if (aligned && pos + 16 <= len) {
-        *reinterpret_cast<uint4 *>(dst + pos) = v;
+        gstore16(dst + pos, v);
         return;
     }
     const uint32_t w[4] = { v.x, v.y, v.z, v.w };
@@ -228,6 +228,13 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t) __shfl_xor(v, o));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t) __shfl_xor(v, o));
     return v;
 }
 
@@ -323,7 +330,8 @@ struct GcmLds {
     static constexpr int GH = 0;
     static constexpr int AES = NT * 8192;               /* T0/T1 x 32 copies */
     static constexpr int EJ0 = AES + 65536;             /* W waves x 64 x 16 B */
-    static constexpr int CTL = EJ0 + W * 64 * 16;
+    static constexpr int FOLD = EJ0 + W * 64 * 16;      /* W waves x 64 x 16 B: AAD fold */
+    static constexpr int CTL = FOLD + W * 64 * 16;
     static constexpr int BYTES = CTL + 16;
 };
 
@@ -464,9 +472,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint32_t z = (BL - mm % BL) % BL;                    /* front padding */
             const uint32_t J = jb.run ? (mm + z) / BL : 0;
             const uint32_t Jmax = wave_max(J);
-            /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H, so
-             * every step below is the same Horner step Y = Y*H^L ^ X. */
-            const uint4 aadh = gmul<0>(lds, jb.aadw);
+            /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
+             * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
+             * only the step with cc == 0 reads it. */
+            uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + wave * 64 + lane;
+            {
+                const uint4 aadh = gmul<0>(lds, jb.aadw);
+                *fold = m ? aadh : jb.aadw;
+            }
             /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
              * does not depend on step j's keystream, so its table reads share
              * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
@@ -475,11 +488,32 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             uint32_t nzpos = 0;
             /* a readable 16-byte address for lanes with nothing to load */
             const uint8_t *safe = jb.run ? jb.src : reinterpret_cast<const uint8_t *>(a.recs);
+            /* Body steps [1, jh): every lane of the wave holds a full, aligned
+             * block inside its record's content (wave-uniform bound), so they run
+             * without masks or branches.  Step 0 (AAD fold, front padding) and
+             * the tail (partial blocks, ragged lengths) take the general step. */
+            uint32_t jh = 0;
+            {
+                const uint32_t mfast = (jb.run && jb.aligned) ? jb.content_len / 16 : 0;
+                uint32_t h = jb.run ? (mfast + z) / BL : 0;
+                h = wave_min(h);
+                jh = h > 1 ? h : 0;
+            }
+            const uint32_t jl = jh ? 1u : Jmax;
             auto steps = [&](auto cached) {
                 constexpr bool CACHED = decltype(cached)::value;
                 CtrCache ccache;
                 if constexpr (CACHED) ccache = ctr_cache<LY::AES>(lds, lanebase, rk, jb.nw0, jb.nw1, jb.nw2);
-                for (uint32_t j = 0; j < Jmax; j++) {
+                auto crypt = [&](int32_t cc, uint4 y, uint4 &ks, uint4 &Zn) {
+                    const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
+                    if constexpr (CACHED) {
+                        aes_ghash<NR, LY::AES, LOGL>(lds, lanebase, rk, ccache, ctrw, y, ks, Zn);
+                    } else {
+                        ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                        Zn = gmul<LOGL>(lds, y);
+                    }
+                };
+                auto general = [&](uint32_t j) {
                     const bool live = jb.run && j < J;
 #pragma unroll
                     for (int b = 0; b < B; b++) {
@@ -488,19 +522,13 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                         const uint32_t pos = (uint32_t) cc * 16;
                         /* full, aligned interior block: plain 16-byte load/store */
                         const bool fast = valid && jb.aligned && pos + 16 <= jb.content_len;
-                        uint4 blk = *reinterpret_cast<const uint4 *>(fast ? jb.src + pos : safe);
+                        uint4 blk = gload16(fast ? jb.src + pos : safe);
                         uint4 ks, Zn;
-                        const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
-                        if constexpr (CACHED) {
-                            aes_ghash<NR, LY::AES, LOGL>(lds, lanebase, rk, ccache, ctrw, xor4(Z, Xp), ks, Zn);
-                        } else {
-                            ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
-                            Zn = gmul<LOGL>(lds, xor4(Z, Xp));
-                        }
+                        crypt(cc, xor4(Z, Xp), ks, Zn);
                         uint4 X = make_uint4(0, 0, 0, 0);
                         if (fast) {
                             const uint4 o = xor4(blk, ks);
-                            *reinterpret_cast<uint4 *>(jb.dst + pos) = o;
+                            gstore16(jb.dst + pos, o);
                             X = DEC ? blk : o;
                             if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                         } else if (valid) {
@@ -510,11 +538,33 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                             X = DEC ? blk : o;
                             if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                         }
-                        if (valid && cc == 0) X = xor4(X, aadh);
-                        if (live && m == 0 && cc == 0) X = jb.aadw;
+                        if (live && cc == 0) X = xor4(X, *fold);
                         if (live) { Z = Zn; Xp = X; }
                     }
+                };
+                uint32_t j = 0;
+                for (; j < jl; j++) general(j);
+                {
+                    const uint8_t *sp = jb.src + (size_t) (BL * j + q - z) * 16;
+                    uint8_t *dp = jb.dst + (size_t) (BL * j + q - z) * 16;
+                    for (; j < jh; j++) {
+#pragma unroll
+                        for (int b = 0; b < B; b++) {
+                            const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                            const uint4 blk = gload16(sp + 16 * L * b);
+                            uint4 ks, Zn;
+                            crypt(cc, xor4(Z, Xp), ks, Zn);
+                            const uint4 o = xor4(blk, ks);
+                            gstore16(dp + 16 * L * b, o);
+                            if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
+                            Z = Zn;
+                            Xp = DEC ? blk : o;
+                        }
+                        sp += 16 * BL;
+                        dp += 16 * BL;
+                    }
                 }
+                for (; j < Jmax; j++) general(j);
             };
             /* counters stay below 2^16 (any TLS record): cached rounds 1-2 */
             if (wave_max(m) + 2 < 65536u)

@@ -86,6 +86,24 @@ __device__ __forceinline__ void aes_fill_tables(uint8_t *lds_aes, int tid, int n
 /* constant address space: read-only for the kernel's lifetime, scalar loads */
 typedef const __attribute__((address_space(4))) uint32_t kconst_u32;
 
+/* Record payload access through the global address space.  Through generic
+ * pointers (struct members) these compile to flat_load/flat_store, which
+ * count on lgkmcnt as well as vmcnt: the first LDS wait after the load then
+ * becomes vmcnt(0) lgkmcnt(0) and the wave stalls for the full HBM latency
+ * in every step. */
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 glob_u32x4;
+__device__ __forceinline__ uint4 gload16(const uint8_t *p)
+{
+    const u32x4 v = *(const glob_u32x4 *) (uintptr_t) p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore16(uint8_t *p, uint4 v)
+{
+    u32x4 w = { v.x, v.y, v.z, v.w };
+    *(glob_u32x4 *) (uintptr_t) p = w;
+}
+
 #define TLSREC_PSEL(k) (0x0C0C0000u | ((4u + (k)) << 8))
 
 template <int AES_OFF>
@@ -301,6 +319,72 @@ __device__ __forceinline__ void aes_ghash(const uint8_t *lds, uint32_t lb, RK rk
     }
     ks = make_uint4(o[0], o[1], o[2], o[3]);
     prod = acc;
+}
+
+/* NB independent counter blocks of one record and NB independent GHASH
+ * multiplies per call (NB Horner chains per lane), phase-interleaved as in
+ * aes_ghash: chain b's group g of 4 table reads follows AES round 2 + g. */
+template <int NR, int AES_OFF, int PI, int NB, typename RK>
+__device__ __forceinline__ void aes_ghash_n(const uint8_t *lds, uint32_t lb, RK rk, const CtrCache &cc,
+                                            const uint32_t (&ctrw)[NB], const uint4 (&y)[NB], uint4 (&ks)[NB],
+                                            uint4 (&prod)[NB])
+{
+    static_assert(NR >= 10, "rounds 2..9 carry the GHASH groups");
+#define TA(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 0)
+#define TB(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 1)
+    uint32_t s[NB][4];
+    uint32_t w[NB][4];
+    uint4 acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t w3 = ctrw[b] ^ rk[3];
+        const uint32_t t0 = rotl16(cc.k0r ^ TB(w3, 3));
+        const uint32_t t1 = rotl16(cc.k1r ^ TA(w3, 2));
+        s[b][0] = xor3(TA(t0, 0), TB(t1, 1), cc.d0);
+        s[b][1] = xor3(TA(t1, 0), cc.d1, rotl16(TB(t0, 3)));
+        s[b][2] = rotl16(xor3(TA(t0, 2), TB(t1, 3), cc.d2r));
+        s[b][3] = xor3(TB(t0, 1), cc.d3, rotl16(TA(t1, 2)));
+        w[b][0] = y[b].x; w[b][1] = y[b].y; w[b][2] = y[b].z; w[b][3] = y[b].w;
+        acc[b] = make_uint4(0, 0, 0, 0);
+    }
+#undef TA
+#undef TB
+#pragma unroll
+    for (int r = 2; r < NR; r++) {
+        if (r > 2) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) aes_round<AES_OFF>(lds, lb, rk, r, s[b][0], s[b][1], s[b][2], s[b][3]);
+        }
+        const int g = r - 2;
+        if (g < 8) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) gmul_word<PI, 2>(lds, w[b][g >> 1], g >> 1, acc[b], 2 * (g & 1));
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                asm volatile("" : "+v"(s[b][0]), "+v"(s[b][1]), "+v"(s[b][2]), "+v"(s[b][3]), "+v"(acc[b].x),
+                             "+v"(acc[b].y), "+v"(acc[b].z), "+v"(acc[b].w));
+                if (g < 2) asm volatile("" : "+v"(w[b][1]), "+v"(w[b][2]), "+v"(w[b][3]));
+                else if (g < 4) asm volatile("" : "+v"(w[b][2]), "+v"(w[b][3]));
+                else if (g < 6) asm volatile("" : "+v"(w[b][3]));
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        uint32_t o[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            uint32_t a = tlook<AES_OFF>(lds, s[b][c], lb, 0, 0);
+            uint32_t bb = tlook<AES_OFF>(lds, s[b][(c + 1) & 3], lb, 1, 0);
+            uint32_t d2 = tlook<AES_OFF>(lds, s[b][(c + 2) & 3], lb, 2, 0);
+            uint32_t d3 = tlook<AES_OFF>(lds, s[b][(c + 3) & 3], lb, 3, 0);
+            uint32_t lo = __builtin_amdgcn_perm(bb, a, 0x0C0C0501u);
+            uint32_t hi = __builtin_amdgcn_perm(d3, d2, 0x06020C0Cu);
+            o[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);
+        }
+        ks[b] = make_uint4(o[0], o[1], o[2], o[3]);
+        prod[b] = acc[b];
+    }
 }
 
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }

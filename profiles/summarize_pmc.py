@@ -12,7 +12,7 @@ from collections import defaultdict
 def summarize(root, pattern):
     vals = defaultdict(lambda: defaultdict(float))
     durs = {}
-    for path in glob.glob(f"{root}/*/run_counter_collection.csv"):
+    for path in glob.glob(f"{root}/run_counter_collection.csv") + glob.glob(f"{root}/*/run_counter_collection.csv"):
         for row in csv.DictReader(open(path)):
             if pattern not in row["Kernel_Name"]:
                 continue
