@@ -38,7 +38,7 @@ CONFIGS = {
     "c3": ("CHACHA20-POLY1305", "TLS1.3", "encrypt", 1400, 1 << 20, 1,
            "ChaCha20-Poly1305 encrypt, 1M x 1.4 KiB TLS 1.3 records, single key"),
     "c4": ("MIX", "TLS1.3", "decrypt", 16383, 1 << 22, 1 << 16,
-           "64K keys x 64 records, AES-256-GCM + ChaCha20-Poly1305 interleaved, 16 KiB"),
+           "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 16 KiB TLS 1.3 decrypt"),
 }
 
 
@@ -119,10 +119,9 @@ def main():
     recs["buf_len"] = stride
     recs["data_offset"] = 0
     recs["data_len"] = content
-    if nkeys == 1:
-        recs["slot"] = 0
-    else:   # round-robin over keys, then grouped by key so a workgroup shares its key
-        recs["slot"] = np.sort(np.arange(n, dtype=np.uint64) % nkeys).astype(np.uint32)
+    # records round-robin over keys: neighbours never share a
+    # key; the engine's bucket pass groups them by key on the device
+    recs["slot"] = (np.arange(n, dtype=np.uint64) % nkeys).astype(np.uint32)
     seq = np.arange(shard0, shard0 + n, dtype=np.uint64)
     recs["ctr"] = M.seq_bytes(seq)
     recs["type"] = 23

@@ -176,8 +176,16 @@ typedef struct tlsrec_batch_res {
 /* Protect / unprotect `n` records.  `recs` and `res` are device arrays; the
  * record buffers live in `in_arena`; results are written to the same offsets
  * of `out_arena` (== in_arena for the reference's in-place behaviour).
- * lanes_per_record: 0 = auto, else 8/16/32/64 lanes of a wavefront share one
- * record.  Asynchronous on `stream`; per-record status lands in `res`. */
+ * Per-record semantics are those of mbedtls_ssl_encrypt_buf / _decrypt_buf
+ * under the slot's key; a record naming a slot past the table or never
+ * loaded gets TLSREC_ERR_SSL_BAD_INPUT_DATA and is left untouched.
+ * Records may reference any mix of slots and ciphers in any order (the
+ * engine groups them by key on the device); 128-byte aligned record buffers
+ * avoid partial-line HBM writes.
+ * lanes_per_record: 0 = auto, else lanes of a wavefront sharing one record:
+ * 4/8/16/64 for AES-GCM, 1/2/4/8 for ChaCha20-Poly1305 (other values: auto).
+ * Asynchronous on `stream` (hipStream_t, NULL = default stream); per-record
+ * status lands in `res`. */
 int tlsrec_batch_encrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
                          tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
                          uint8_t *out_arena, uint32_t lanes_per_record, void *stream);

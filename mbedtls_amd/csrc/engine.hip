@@ -7,6 +7,7 @@
  * transformed by the kernels in kernels.hip.
  */
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -25,6 +26,7 @@ struct tlsrec_keytab {
     tlsrec_key_material *d_stage;
     uint8_t *h_cipher;        /* host mirror of each slot's cipher */
     uint32_t cipher_mask;     /* 1 << TLSREC_CIPHER_* of every loaded slot */
+    uint32_t nloaded;         /* slots holding a key */
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED; }
@@ -125,6 +127,7 @@ extern "C" int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t co
         }
     }
     for (uint32_t i = 0; i < count; i++) {
+        if (kt->h_cipher[first + i] == 0) kt->nloaded++;
         kt->h_cipher[first + i] = hk[i].cipher;
         kt->cipher_mask |= 1u << hk[i].cipher;
     }
@@ -160,6 +163,50 @@ static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t
     return (uint32_t) want;
 }
 
+/* Device scratch of one bucketed batch (stream-ordered allocation). */
+struct BucketScratch {
+    void *mem = nullptr;
+    uint32_t *counts, *offs, *cursor, *perm;
+    void *scan_tmp;
+    size_t scan_bytes;
+};
+
+static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
+                  hipStream_t st, BucketScratch &b)
+{
+    const size_t nk = 2 * (size_t) kt->capacity + 2;   /* AES-128 slots, AES-256 slots, ChaCha, end */
+    b.scan_bytes = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, b.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
+                                         (int) nk, st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    const size_t al = 256;
+    const size_t szk = (nk * 4 + al - 1) / al * al, szp = ((size_t) n * 4 + al - 1) / al * al;
+    const size_t total = 3 * szk + szp + b.scan_bytes + al;
+    if (hipMallocAsync(&b.mem, total, st) != hipSuccess) return TLSREC_ERR_SSL_ALLOC_FAILED;
+    uint8_t *m = (uint8_t *) b.mem;
+    b.counts = (uint32_t *) m;
+    b.offs = (uint32_t *) (m + szk);
+    b.cursor = (uint32_t *) (m + 2 * szk);
+    b.perm = (uint32_t *) (m + 3 * szk);
+    b.scan_tmp = m + 3 * szk + szp;
+    BucketArgs a;
+    a.slots = kt->d_slots;
+    a.recs = recs;
+    a.res = res;
+    a.n = n;
+    a.capacity = kt->capacity;
+    a.counts = b.counts;
+    a.cursor = b.cursor;
+    a.perm = b.perm;
+    if (hipMemsetAsync(b.counts, 0, nk * 4, st) != hipSuccess ||
+        tlsrec__launch_bucket_count(&a, st) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, b.scan_bytes, b.counts, b.offs, (int) nk, st) != hipSuccess ||
+        hipMemcpyAsync(b.cursor, b.offs, nk * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        tlsrec__launch_bucket_scatter(&a, st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    return 0;
+}
+
 static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
                  const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec)
 {
@@ -172,42 +219,66 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (hipGetDeviceProperties(&prop, kt->device) == hipSuccess && prop.multiProcessorCount > 0)
             cu = prop.multiProcessorCount;
     }
-    for (int cipher = TLSREC_CIPHER_AES_128_GCM; cipher <= TLSREC_CIPHER_AES_256_GCM; cipher++) {
+    /* A table holding a single key needs no grouping: the kernels walk the
+     * descriptors in order and flag records naming an unusable slot.
+     * Otherwise the bucket pass groups GCM records by key (then ChaCha). */
+    BucketScratch bs;
+    const bool identity = kt->nloaded == 1;
+    if (!identity) {
+        int r = bucket(kt, recs, res, n, st, bs);
+        if (r) {
+            if (bs.mem) hipFreeAsync(bs.mem, st);
+            return r;
+        }
+    }
+    const uint32_t cap = kt->capacity;
+    int rc = 0;
+    for (int cipher = TLSREC_CIPHER_AES_128_GCM; cipher <= TLSREC_CIPHER_AES_256_GCM && !rc; cipher++) {
         if (!(kt->cipher_mask & (1u << cipher))) continue;
-        int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes : 8;
+        /* lanes per record: 8; 16 when keys average fewer than 256 records of
+         * this batch (a key pass then still fills 16 waves x 4 records) */
+        int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
+                : (kt->nloaded > 1 && n / kt->nloaded < 256 ? 16 : 8);
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;
         a.recs = recs;
         a.res = res;
         a.n = n;
+        a.perm = identity ? nullptr : bs.perm;
+        a.lo = identity ? nullptr : bs.offs + (cipher == TLSREC_CIPHER_AES_128_GCM ? 0 : cap);
+        a.hi = identity ? nullptr : bs.offs + (cipher == TLSREC_CIPHER_AES_128_GCM ? cap : 2 * cap);
         a.in = in;
         a.out = out;
         const int waves = gcm_waves();
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
-        a.capacity = kt->capacity;
+        a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         int nr = cipher == TLSREC_CIPHER_AES_128_GCM ? 10 : 14;
-        if (tlsrec__launch_gcm(&a, dec, L, nr, waves, grid, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (tlsrec__launch_gcm(&a, dec, L, nr, waves, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    if (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305)) {
+    if (!rc && (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
         int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;
         CpArgs a;
         a.slots = kt->d_slots;
         a.recs = recs;
         a.res = res;
         a.n = n;
+        a.perm = identity ? nullptr : bs.perm;
+        a.lo = identity ? nullptr : bs.offs + 2 * cap;
+        a.hi = identity ? nullptr : bs.offs + 2 * cap + 1;
         a.in = in;
         a.out = out;
         a.rpw = pick_rpw(n, CP_WAVES, 64 / L, (uint32_t) cu * 4);
-        a.capacity = kt->capacity;
+        a.capacity = cap;
         uint64_t per_wg = (uint64_t) CP_WAVES * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
-        if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    return 0;
+    if (bs.mem && hipFreeAsync(bs.mem, st) != hipSuccess && !rc) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    return rc;
 }
 
 extern "C" int tlsrec_batch_encrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,

@@ -272,6 +272,18 @@ __device__ __forceinline__ void make_plan(tlsrec_plan &p, const tlsrec_batch_rec
                             km.granularity ? km.granularity : TLSREC_PADDING_GRANULARITY);
 }
 
+/* Record naming no usable key slot (out of range or never loaded). */
+__device__ inline void bad_slot_result(const tlsrec_batch_rec &d, tlsrec_batch_res *res)
+{
+    tlsrec_batch_res r;
+    r.status = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    r.data_offset = d.data_offset;
+    r.data_len = d.data_len;
+    r.type = d.type;
+    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+    *res = r;
+}
+
 /* Record whose plan stopped before the AEAD: status + pre-AEAD side effects. */
 __device__ inline void finish_early(const tlsrec_plan &p, const tlsrec_batch_rec &d, uint8_t *out,
                                     tlsrec_batch_res *res)
@@ -394,16 +406,29 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
     uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + LY::CTL);
 
+    /* This workgroup's positions: wave w owns positions base + k*W + w,
+     * k < rpw (interleaved, so a key's run of records in perm spreads over
+     * all waves of the workgroup within one key pass). */
+    const uint32_t lo = a.perm ? *a.lo : 0u;
+    const uint32_t count = a.perm ? *a.hi - lo : (uint32_t) a.n;
+    const uint64_t wg_base = (uint64_t) blockIdx.x * W * a.rpw;
+    if (wg_base >= count) return;                      /* uniform: before any barrier */
+
     aes_fill_tables(lds + LY::AES, tid, NTHR);
 
-    const uint64_t chunk = ((uint64_t) blockIdx.x * W + wave) * a.rpw;
-    /* pass membership: lane l tracks record chunk + l of the pre-pass */
-    uint32_t my_slot = 0xffffffffu;
+    /* pass membership: lane l tracks the record at chunk position k = l */
+    uint32_t my_slot = 0xffffffffu, my_rec = 0;
     {
-        uint64_t r = chunk + (uint64_t) lane;
-        if (lane < (int) a.rpw && r < a.n) {
-            uint32_t s = a.recs[r].slot;
-            if (s < a.capacity && a.slots[s].km.cipher == a.cipher) my_slot = s;
+        const uint64_t pos = wg_base + (uint64_t) lane * W + wave;
+        if (lane < (int) a.rpw && pos < count) {
+            my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
+            const uint32_t s = a.recs[my_rec].slot;
+            if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
+                my_slot = s;
+            } else if (!a.perm && !(s < a.capacity && a.slots[s].km.cipher != 0)) {
+                /* identity order: this kernel is the only one that sees the record */
+                bad_slot_result(a.recs[my_rec], &a.res[my_rec]);
+            }
         }
     }
     if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
@@ -435,7 +460,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             bool mine = my_slot == s;
             uint32_t nw[3] = { 0, 0, 0 };
             if (mine) {
-                const tlsrec_batch_rec d = a.recs[chunk + lane];
+                const tlsrec_batch_rec d = a.recs[my_rec];
                 tlsrec_plan p;
                 make_plan<DEC>(p, d, km);
                 nonce_words<DEC>(p, d, a.in, nw);
@@ -451,7 +476,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint32_t slot_in_chunk = rr + (uint32_t) g;
             const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
             const bool active = slot_in_chunk < a.rpw && owner_slot == s;
-            const uint64_t ridx = chunk + slot_in_chunk;
+            const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
             /* Only what the AEAD loop needs stays live across it; the plan is
              * re-derived from the (cached) descriptor afterwards. */
             GcmJob jb;
@@ -637,6 +662,66 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 }
 
 /* ======================================================================
+ * Bucket pass: group the batch's records by key for the GCM kernels (a key
+ * pass stages one key's GHASH tables for a whole workgroup), ChaCha records
+ * after them; records without a usable slot get BAD_INPUT_DATA here.
+ *   key index: class 0 (AES-128) -> slot, class 1 (AES-256) -> cap + slot,
+ *   ChaCha -> 2 cap, none -> no index.
+ * Atomics are wave-aggregated when the wave's records share one key (a
+ * batch already grouped by key costs one atomic per wave).
+ * ==================================================================== */
+__device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec_batch_rec &d)
+{
+    if (d.slot >= a.capacity) return 0xffffffffu;
+    switch (a.slots[d.slot].km.cipher) {
+        case TLSREC_CIPHER_AES_128_GCM: return d.slot;
+        case TLSREC_CIPHER_AES_256_GCM: return a.capacity + d.slot;
+        case TLSREC_CIPHER_CHACHA20_POLY1305: return 2 * a.capacity;
+        default: return 0xffffffffu;
+    }
+}
+
+/* position of this lane's record within its key's run: one atomic per wave
+ * when every pending lane has the same key, else one per lane */
+__device__ __forceinline__ uint32_t bucket_claim(uint32_t *ctr, uint32_t key)
+{
+    const bool pend = key != 0xffffffffu;
+    const uint64_t pmask = __ballot(pend);
+    if (pmask == 0) return 0;
+    const uint32_t first = __builtin_amdgcn_readlane(key, __builtin_ctzll(pmask));
+    const uint64_t same = __ballot(pend && key == first);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) same, 0));
+    if (same == pmask) {
+        uint32_t base = 0;
+        if (pend && rank == 0) base = atomicAdd(&ctr[first], (uint32_t) __popcll(same));
+        base = __builtin_amdgcn_readlane(base, __builtin_ctzll(pmask));
+        return base + rank;
+    }
+    return pend ? atomicAdd(&ctr[key], 1u) : 0u;
+}
+
+__global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    uint32_t key = 0xffffffffu;
+    if (i < a.n) {
+        const tlsrec_batch_rec d = a.recs[i];
+        key = bucket_key(a, d);
+        if (key == 0xffffffffu) bad_slot_result(d, &a.res[i]);
+    }
+    (void) bucket_claim(a.counts, key);
+}
+
+__global__ __launch_bounds__(256) void tlsrec_bucket_scatter_kernel(BucketArgs a)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    uint32_t key = 0xffffffffu;
+    if (i < a.n) key = bucket_key(a, a.recs[i]);
+    const uint32_t pos = bucket_claim(a.cursor, key);
+    if (key != 0xffffffffu) a.perm[pos] = i;
+}
+
+/* ======================================================================
  * ChaCha20-Poly1305
  * ==================================================================== */
 __device__ __forceinline__ P5 p_from_words(uint4 w)
@@ -666,15 +751,21 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
     __shared__ uint32_t polykey[CP_WAVES][64][8];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane / L, q = lane % L;
+    const uint32_t lo = a.perm ? *a.lo : 0u;
+    const uint32_t count = a.perm ? *a.hi - lo : (uint32_t) a.n;
     const uint64_t chunk = ((uint64_t) blockIdx.x * CP_WAVES + wave) * a.rpw;
 
     /* ---- pre-pass: one-time Poly1305 key (ChaCha20 block 0, RFC 8439 2.6) ---- */
     bool mine = false;
+    uint32_t my_rec = 0;
     {
-        uint64_t r = chunk + (uint64_t) lane;
+        const uint64_t pos = chunk + (uint64_t) lane;
         uint32_t key[8] = { 0 }, nw[3] = { 0, 0, 0 };
-        if (lane < (int) a.rpw && r < a.n) {
-            const tlsrec_batch_rec d = a.recs[r];
+        if (lane < (int) a.rpw && pos < count) {
+            my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
+            const tlsrec_batch_rec d = a.recs[my_rec];
+            if (!a.perm && !(d.slot < a.capacity && a.slots[d.slot].km.cipher != 0))
+                bad_slot_result(d, &a.res[my_rec]);
             if (d.slot < a.capacity && a.slots[d.slot].km.cipher == TLSREC_CIPHER_CHACHA20_POLY1305) {
                 mine = true;
                 const tlsrec_key_material km = a.slots[d.slot].km;
@@ -693,7 +784,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         const uint32_t slot_in_chunk = rr + (uint32_t) g;
         const bool owner_mine = __shfl((int) mine, (int) slot_in_chunk & 63) != 0;
         const bool active = slot_in_chunk < a.rpw && owner_mine;
-        const uint64_t ridx = chunk + slot_in_chunk;
+        const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
         tlsrec_batch_rec d;
         tlsrec_plan p;
         tlsrec_key_material km;
@@ -898,6 +989,20 @@ extern "C" hipError_t tlsrec__launch_gcm(const GcmArgs *a, int dec, int lanes, i
         case 64: return dec ? launch_gcm_nr<64, true>(*a, nr, waves, grid, st) : launch_gcm_nr<64, false>(*a, nr, waves, grid, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+extern "C" hipError_t tlsrec__launch_bucket_count(const BucketArgs *a, hipStream_t st)
+{
+    if (a->n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tlsrec_bucket_count_kernel, dim3((a->n + 255) / 256), dim3(256), 0, st, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t tlsrec__launch_bucket_scatter(const BucketArgs *a, hipStream_t st)
+{
+    if (a->n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tlsrec_bucket_scatter_kernel, dim3((a->n + 255) / 256), dim3(256), 0, st, *a);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t tlsrec__launch_chachapoly(const CpArgs *a, int dec, int lanes, uint32_t grid, hipStream_t st)

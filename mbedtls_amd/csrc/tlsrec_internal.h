@@ -32,12 +32,19 @@ static_assert(sizeof(tlsrec_key_material) == 64, "key material layout");
 static_assert(sizeof(tlsrec_batch_rec) == 40, "batch record layout");
 static_assert(sizeof(tlsrec_batch_res) == 16, "batch result layout");
 
+/* Records a kernel processes: positions [*lo, *hi) of `perm` (record
+ * indices grouped by key, built by the bucket pass), or, with perm == NULL,
+ * positions [0, n) of the descriptor array itself (identity order: a table
+ * holding a single key).  lo/hi live in device memory so the launches need
+ * no host synchronisation. */
 struct GcmArgs {
     const SlotState *slots;
     const uint4 *ghtab;
     const tlsrec_batch_rec *recs;
     tlsrec_batch_res *res;
     uint64_t n;
+    const uint32_t *perm;
+    const uint32_t *lo, *hi;
     const uint8_t *in;
     uint8_t *out;
     uint32_t rpw;             /* records per wavefront chunk (<= 64) */
@@ -50,10 +57,26 @@ struct CpArgs {
     const tlsrec_batch_rec *recs;
     tlsrec_batch_res *res;
     uint64_t n;
+    const uint32_t *perm;
+    const uint32_t *lo, *hi;
     const uint8_t *in;
     uint8_t *out;
     uint32_t rpw;
     uint32_t capacity;
+};
+
+/* Bucket pass: key class of a record = 0 (AES-128-GCM slot), 1 (AES-256-GCM
+ * slot), 2 (ChaCha20-Poly1305), 3 (no usable slot: BAD_INPUT_DATA). */
+struct BucketArgs {
+    const SlotState *slots;
+    const tlsrec_batch_rec *recs;
+    tlsrec_batch_res *res;
+    uint32_t n;
+    uint32_t capacity;
+    uint32_t *counts;         /* [2 * capacity + 1] records per (class, slot), then exclusive offsets */
+    uint32_t *cursor;         /* copy of the offsets, consumed by the scatter */
+    uint32_t *cp_cursor;      /* ChaCha records appended after the GCM ones */
+    uint32_t *perm;           /* [n] */
 };
 
 } /* namespace tlsrec */
@@ -65,6 +88,8 @@ hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int 
                               hipStream_t st);
 hipError_t tlsrec__launch_chachapoly(const tlsrec::CpArgs *a, int dec, int lanes, uint32_t grid,
                                      hipStream_t st);
+hipError_t tlsrec__launch_bucket_count(const tlsrec::BucketArgs *a, hipStream_t st);
+hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_t st);
 }
 
 #endif

@@ -231,3 +231,58 @@ def test_gcm_counter_boundary(cipher):
     out, res = pb.run_gpu(False)
     assert not pb.compare(False, out, res)
     assert res["status"].tolist()[:4] == [M.ERR_SSL_BAD_INPUT_DATA] * 4
+
+
+@pytest.mark.parametrize("lanes", [0, 8, 16])
+def test_many_keys_all_ciphers_round_robin(lanes):
+    """Bucket pass: 3 ciphers x 2 TLS versions over 150 keys, records
+    round-robin over keys (every neighbour has another key), ragged lengths;
+    bit-exact vs the oracle for both directions and several lane counts."""
+    nkeys = 150
+    slots = B.random_slots(9001, [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305],
+                           [M.VERSION_TLS1_2, M.VERSION_TLS1_3], nkeys)
+    lengths = [int(x) for x in np.frombuffer(prng_bytes(31337, 2 * nkeys * 5), np.uint16) % 3000]
+    for decrypt in (False, True):
+        recs = (B.sealed_records(slots, lengths, seed=5)[0] if decrypt
+                else B.plaintext_records(slots, lengths, seed=5))
+        b = B.Batch(slots, recs)
+        out, res = b.run_gpu(decrypt, lanes=lanes)
+        bad = b.compare(decrypt, out, res)
+        assert not bad, "; ".join(bad[:5])
+
+
+@pytest.mark.parametrize("nslots", [1, 4], ids=["identity", "bucket"])
+def test_unusable_slot_gets_bad_input(nslots):
+    """Records naming a slot past the table or never loaded are reported
+    BAD_INPUT_DATA with their buffer untouched; the other records are
+    processed normally -- with a single-key table (kernels walk the
+    descriptors in order) and a multi-key one (bucket pass)."""
+    import torch
+    slots = B.random_slots(123, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305], [M.VERSION_TLS1_3], nslots)
+    recs = B.plaintext_records(slots, [100, 2000, 17, 500, 64, 1400], seed=3)
+    b = B.Batch(slots, recs)
+    d = b.desc.copy()
+    cap = nslots + 2                        # slot nslots .. cap-1 never loaded
+    d["slot"][1] = cap + 5                  # past the table
+    d["slot"][4] = nslots + 1               # inside the table, never loaded
+    dev = torch.device("cuda")
+    kt = M.KeyTable(cap)
+    kt.load(b.key_materials())
+    arena = torch.from_numpy(b.arena.copy()).to(dev)
+    res = torch.zeros(len(recs) * 16, dtype=torch.uint8, device=dev)
+    recs_d = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+    M.batch_encrypt(kt, recs_d, res, len(recs), arena, arena)
+    torch.cuda.synchronize()
+    out = arena.cpu().numpy()
+    r = res.cpu().numpy().view(M.BATCH_RES)
+    kt.close()
+    for i in (1, 4):
+        assert int(r["status"][i]) == M.ERR_SSL_BAD_INPUT_DATA
+        o = b.offs[i]
+        assert bytes(out[o:o + len(recs[i].buf)]) == bytes(recs[i].buf)
+    good = B.Batch(slots, [recs[i] for i in (0, 2, 3, 5)])
+    o_recs, o_stats = good.run_oracle(False)
+    for k, i in enumerate((0, 2, 3, 5)):
+        assert int(r["status"][i]) == o_stats[k] == 0
+        o = b.offs[i]
+        assert bytes(out[o:o + len(recs[i].buf)]) == bytes(o_recs[k].buf)
