@@ -681,23 +681,34 @@ __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec
     }
 }
 
-/* position of this lane's record within its key's run: one atomic per wave
- * when every pending lane has the same key, else one per lane */
-__device__ __forceinline__ uint32_t bucket_claim(uint32_t *ctr, uint32_t key)
+/* One wave's claim on the counters ctr[key] for its pending lanes: lanes
+ * sharing the wave's first pending key take one atomic together (rank from
+ * mbcnt), the rest one atomic each.  Returns the lane's position. */
+__device__ __forceinline__ uint32_t claim_group(uint32_t *ctr, uint32_t key, bool pend)
 {
-    const bool pend = key != 0xffffffffu;
     const uint64_t pmask = __ballot(pend);
     if (pmask == 0) return 0;
-    const uint32_t first = __builtin_amdgcn_readlane(key, __builtin_ctzll(pmask));
-    const uint64_t same = __ballot(pend && key == first);
+    const int lead = __builtin_ctzll(pmask);
+    const uint32_t first = __builtin_amdgcn_readlane(key, lead);
+    const bool grp = pend && key == first;
+    const uint64_t same = __ballot(grp);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) same, 0));
-    if (same == pmask) {
-        uint32_t base = 0;
-        if (pend && rank == 0) base = atomicAdd(&ctr[first], (uint32_t) __popcll(same));
-        base = __builtin_amdgcn_readlane(base, __builtin_ctzll(pmask));
-        return base + rank;
-    }
+    uint32_t base = 0;
+    if (grp && rank == 0) base = atomicAdd(&ctr[first], (uint32_t) __popcll(same));
+    base = __builtin_amdgcn_readlane(base, lead);
+    if (grp) return base + rank;
     return pend ? atomicAdd(&ctr[key], 1u) : 0u;
+}
+
+/* ChaCha records share one counter: always one atomic per wave for them;
+ * GCM records: one per wave when the wave's GCM records share a key (a batch
+ * grouped by key), else one per record (distinct addresses, no contention). */
+__device__ __forceinline__ uint32_t bucket_claim(const BucketArgs &a, uint32_t *ctr, uint32_t key)
+{
+    const bool cp = key == 2 * a.capacity;
+    const uint32_t pc = claim_group(ctr, key, cp);
+    const uint32_t pg = claim_group(ctr, key, key != 0xffffffffu && !cp);
+    return cp ? pc : pg;
 }
 
 __global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
@@ -709,7 +720,7 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
         key = bucket_key(a, d);
         if (key == 0xffffffffu) bad_slot_result(d, &a.res[i]);
     }
-    (void) bucket_claim(a.counts, key);
+    (void) bucket_claim(a, a.counts, key);
 }
 
 __global__ __launch_bounds__(256) void tlsrec_bucket_scatter_kernel(BucketArgs a)
@@ -717,7 +728,7 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_scatter_kernel(BucketArgs a
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     uint32_t key = 0xffffffffu;
     if (i < a.n) key = bucket_key(a, a.recs[i]);
-    const uint32_t pos = bucket_claim(a.cursor, key);
+    const uint32_t pos = bucket_claim(a, a.cursor, key);
     if (key != 0xffffffffu) a.perm[pos] = i;
 }
 
