@@ -755,22 +755,90 @@ __device__ __forceinline__ P5 shfl_p5(P5 v, int src)
     return r;
 }
 
+/* Per-record constants of the ChaCha20-Poly1305 kernel, one per chunk
+ * position of a wave, written by the wave's pre-pass and read (L lanes per
+ * record) from LDS in the record loop instead of living in VGPRs. */
+struct CpRec {
+    uint32_t key[8];
+    uint32_t nonce[3];
+    uint32_t pad0;
+    uint32_t s[4];           /* Poly1305 s */
+    uint32_t r1[5], r2[5], r3[5], rl[5];   /* r, r^2, r^3, r^(4L) (26-bit limbs) */
+};
+static_assert(sizeof(CpRec) == 144, "CpRec layout");
+
+__device__ __forceinline__ P5 p_lds(const uint32_t *v)
+{
+    P5 r;
+#pragma unroll
+    for (int i = 0; i < 5; i++) r.v[i] = v[i];
+    return r;
+}
+
+/* 64-bit limb accumulator: sums of 26x28-bit limb products, reduced once */
+struct D5 { uint64_t v[5]; };
+
+__device__ __forceinline__ void p_mac(D5 &d, const P5 &h, const P5 &r)
+{
+    const uint32_t s1 = r.v[1] * 5, s2 = r.v[2] * 5, s3 = r.v[3] * 5, s4 = r.v[4] * 5;
+    d.v[0] += (uint64_t) h.v[0] * r.v[0] + (uint64_t) h.v[1] * s4 + (uint64_t) h.v[2] * s3 +
+              (uint64_t) h.v[3] * s2 + (uint64_t) h.v[4] * s1;
+    d.v[1] += (uint64_t) h.v[0] * r.v[1] + (uint64_t) h.v[1] * r.v[0] + (uint64_t) h.v[2] * s4 +
+              (uint64_t) h.v[3] * s3 + (uint64_t) h.v[4] * s2;
+    d.v[2] += (uint64_t) h.v[0] * r.v[2] + (uint64_t) h.v[1] * r.v[1] + (uint64_t) h.v[2] * r.v[0] +
+              (uint64_t) h.v[3] * s4 + (uint64_t) h.v[4] * s3;
+    d.v[3] += (uint64_t) h.v[0] * r.v[3] + (uint64_t) h.v[1] * r.v[2] + (uint64_t) h.v[2] * r.v[1] +
+              (uint64_t) h.v[3] * r.v[0] + (uint64_t) h.v[4] * s4;
+    d.v[4] += (uint64_t) h.v[0] * r.v[4] + (uint64_t) h.v[1] * r.v[3] + (uint64_t) h.v[2] * r.v[2] +
+              (uint64_t) h.v[3] * r.v[1] + (uint64_t) h.v[4] * r.v[0];
+}
+
+/* carry-propagate a D5 of up to four limb products plus a block (< 2^59 per
+ * limb) into limbs < 2^26, limb 1 < 2^26 + 2^10 -- the form p_mul returns */
+__device__ __forceinline__ P5 p_reduce(D5 d)
+{
+    P5 o;
+    uint64_t c;
+    c = d.v[0] >> 26; o.v[0] = (uint32_t) d.v[0] & TLSREC_M26; d.v[1] += c;
+    c = d.v[1] >> 26; o.v[1] = (uint32_t) d.v[1] & TLSREC_M26; d.v[2] += c;
+    c = d.v[2] >> 26; o.v[2] = (uint32_t) d.v[2] & TLSREC_M26; d.v[3] += c;
+    c = d.v[3] >> 26; o.v[3] = (uint32_t) d.v[3] & TLSREC_M26; d.v[4] += c;
+    c = d.v[4] >> 26; o.v[4] = (uint32_t) d.v[4] & TLSREC_M26;
+    const uint64_t t = (uint64_t) o.v[0] + c * 5;
+    o.v[0] = (uint32_t) t & TLSREC_M26;
+    o.v[1] += (uint32_t) (t >> 26);
+    return o;
+}
+
+__device__ __forceinline__ void chacha_block_kn(const uint32_t *kn, uint32_t counter, uint32_t out[16])
+{
+    uint32_t key[8], nw[3];
+#pragma unroll
+    for (int i = 0; i < 8; i++) key[i] = kn[i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) nw[i] = kn[8 + i];
+    chacha_block(key, counter, nw, out);
+}
+
 template <int L, bool DEC>
-__global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
+__global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void tlsrec_chachapoly_kernel(CpArgs a)
 {
     constexpr int R = 64 / L;
-    __shared__ uint32_t polykey[CP_WAVES][64][8];
+    constexpr int LOGL = Log2<L>::v;
+    __shared__ CpRec crec[CP_WAVES][64];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane / L, q = lane % L;
     const uint32_t lo = a.perm ? *a.lo : 0u;
     const uint32_t count = a.perm ? *a.hi - lo : (uint32_t) a.n;
     const uint64_t chunk = ((uint64_t) blockIdx.x * CP_WAVES + wave) * a.rpw;
 
-    /* ---- pre-pass: one-time Poly1305 key (ChaCha20 block 0, RFC 8439 2.6) ---- */
+    /* ---- pre-pass: per chunk position, the record's key/nonce, the one-time
+     * Poly1305 key (ChaCha20 block 0, RFC 8439 2.6) and powers of r ---- */
     bool mine = false;
     uint32_t my_rec = 0;
     {
         const uint64_t pos = chunk + (uint64_t) lane;
+        CpRec &cr = crec[wave][lane];
         uint32_t key[8] = { 0 }, nw[3] = { 0, 0, 0 };
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
@@ -788,21 +856,35 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         }
         uint32_t blk[16];
         chacha_block(key, 0, nw, blk);
-        for (int i = 0; i < 8; i++) polykey[wave][lane][i] = blk[i];
+        for (int i = 0; i < 8; i++) cr.key[i] = key[i];
+        for (int i = 0; i < 3; i++) cr.nonce[i] = nw[i];
+        for (int i = 0; i < 4; i++) cr.s[i] = blk[4 + i];
+        const P5 r1 = p_from_r(blk[0], blk[1], blk[2], blk[3]);
+        const P5 r2 = p_mul(r1, r1);
+        const P5 r3 = p_mul(r2, r1);
+        P5 rl = p_mul(r2, r2);                                  /* r^4 */
+        for (int i = 0; i < LOGL; i++) rl = p_mul(rl, rl);      /* r^(4L) */
+        for (int i = 0; i < 5; i++) {
+            cr.r1[i] = r1.v[i];
+            cr.r2[i] = r2.v[i];
+            cr.r3[i] = r3.v[i];
+            cr.rl[i] = rl.v[i];
+        }
     }
+    /* lanes read other lanes' CpRec: the wave's own LDS writes land first */
 
     for (uint32_t rr = 0; rr < a.rpw; rr += R) {
         const uint32_t slot_in_chunk = rr + (uint32_t) g;
         const bool owner_mine = __shfl((int) mine, (int) slot_in_chunk & 63) != 0;
         const bool active = slot_in_chunk < a.rpw && owner_mine;
         const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
+        const CpRec &cr = crec[wave][slot_in_chunk & 63];
         tlsrec_batch_rec d;
         tlsrec_plan p;
-        tlsrec_key_material km;
         bool run = false;
         if (active) {
             d = a.recs[ridx];
-            km = a.slots[d.slot].km;
+            const tlsrec_key_material km = a.slots[d.slot].km;
             make_plan<DEC>(p, d, km);
             if (p.status != 0) {
                 if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
@@ -817,41 +899,32 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         const uint32_t z = (L - B % L) % L;
         const uint32_t J = run ? (B + z) / L : 0;
         const uint32_t Jmax = wave_max(J);
-        uint32_t key[8] = { 0 }, nw[3] = { 0, 0, 0 };
         uint4 aadw = make_uint4(0, 0, 0, 0);
         const uint8_t *src = a.in;
         uint8_t *dst = a.out;
         bool aligned = false;
         uint32_t content_len = 0;
         if (run) {
-            for (int i = 0; i < 8; i++) key[i] = ld_u32le(km.key + 4 * i);
-            nonce_words<DEC>(p, d, a.in, nw);
             aadw = aad_words(p);
             src = a.in + d.buf_off + p.aead_pos;
             dst = a.out + d.buf_off + p.aead_pos;
             aligned = ((((uintptr_t) src) | ((uintptr_t) dst)) & 15) == 0;
             content_len = DEC ? aead_len : p.content_len;
         }
-        const uint32_t *pk = polykey[wave][slot_in_chunk & 63];
-        const P5 r1 = p_from_r(pk[0], pk[1], pk[2], pk[3]);
-        const uint4 sw = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-        const P5 r2 = p_mul(r1, r1);
-        const P5 r3 = p_mul(r2, r1);
-        const P5 r4 = p_mul(r2, r2);
-        P5 rpow[Log2<L>::v + 1];                                /* r^(4*2^i), i = 0..log2 L */
-        rpow[0] = r4;
-#pragma unroll
-        for (int i = 1; i <= Log2<L>::v; i++) rpow[i] = p_mul(rpow[i - 1], rpow[i - 1]);
-        const P5 aadr = p_mul(p_from_words(aadw), r1);          /* AAD folded before C_0 */
+        const uint8_t inner_type = run ? p.inner_type : 0;
+        const bool tls13 = run && p.tls13;
 
         P5 acc = p_zero(), vf = p_zero();
-        uint32_t nzkey = 0;
-        for (uint32_t j = 0; j < Jmax; j++) {
+        uint32_t nzpos = 0;                 /* TLS 1.3: 1 + position of the last non-zero 16-B block */
+
+        /* general step: any chunk (front padding, AAD fold at chunk 0, the
+         * final chunk with v <= 4 Poly1305 blocks, partial or unaligned data) */
+        auto general = [&](uint32_t j) {
             const int32_t b = (int32_t) (L * j + q) - (int32_t) z;
             const bool live = run && j < J;
             const bool valid = live && b >= 0 && (uint32_t) b < B;
             uint32_t ks[16];
-            chacha_block(key, (uint32_t) b + 1u, nw, ks);
+            chacha_block_kn(cr.key, (uint32_t) b + 1u, ks);
             uint4 ct[4];
 #pragma unroll
             for (int t = 0; t < 4; t++) ct[t] = make_uint4(0, 0, 0, 0);
@@ -860,22 +933,20 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
                 for (int t = 0; t < 4; t++) {
                     const uint32_t pos = (uint32_t) b * 64 + 16 * t;
                     if (pos < aead_len) {
-                        uint4 blk = load_block(src, pos, content_len, aead_len, p.inner_type, aligned);
+                        uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, aligned);
                         uint4 o = mask_block(xor4(blk, make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3])),
                                              pos, aead_len);
                         store_block(dst, pos, aead_len, o, aligned);
                         ct[t] = DEC ? blk : o;
-                        if (DEC && p.tls13) {
-                            uint32_t k = last_nonzero_key(o, pos);
-                            if (k) nzkey = k;
-                        }
+                        if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                     }
                 }
             }
-            /* Horner over this chunk's Poly1305 blocks */
+            /* Horner over this chunk's Poly1305 blocks (AAD folded before C_0) */
+            const P5 r1 = p_lds(cr.r1);
             const uint32_t vv = (valid && (uint32_t) b == B - 1) ? v : 4;
             P5 x = p_from_words(ct[0]);
-            x = p_sel(b == 0, p_add(x, aadr), x);
+            if (b == 0) x = p_add(x, p_mul(p_from_words(aadw), r1));
 #pragma unroll
             for (int t = 1; t < 4; t++) {
                 P5 y = p_add(p_mul(x, r1), p_from_words(ct[t]));
@@ -883,15 +954,68 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
             }
             const bool is_final = valid && (uint32_t) b == B - 1;
             if (is_final) vf = x;
-            P5 an = (j == 0) ? p_zero() : p_mul(acc, rpow[Log2<L>::v]);
+            P5 an = (j == 0) ? p_zero() : p_mul(acc, p_lds(cr.rl));
             an = p_add(an, (valid && !is_final) ? x : p_zero());
             if (live && !is_final) acc = an;
+        };
+
+        /* Body chunks [1, jh): every lane of the wave holds a full, aligned,
+         * non-final chunk inside its record's content (wave-uniform bound):
+         * no masks, and Poly1305 as acc*r^(4L) + c0 r^3 + c1 r^2 + c2 r + c3
+         * with one carry propagation per chunk. */
+        uint32_t jh = 0;
+        {
+            const uint32_t bmax = (run && aligned && B > 0) ? min(B - 1, content_len / 64) : 0;
+            const uint32_t h = wave_min(run ? (bmax + z) / L : 0);
+            jh = h > 1 ? h : 0;
         }
+        const uint32_t jl = jh ? 1u : Jmax;
+        uint32_t j = 0;
+        for (; j < jl; j++) general(j);
+        for (; j < jh; j++) {
+            const uint32_t b = L * j + q - z;
+            const uint8_t *sp = src + (size_t) b * 64;
+            uint4 c[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) c[t] = gload16(sp + 16 * t);
+            /* keep the loads here, a ChaCha20 block ahead of their use: left
+             * alone, the scheduler sinks each to just before its XOR and the
+             * step pays four serial memory latencies */
+            asm volatile("" ::: "memory");
+            uint32_t ks[16];
+            chacha_block_kn(cr.key, b + 1u, ks);
+            uint8_t *dp = dst + (size_t) b * 64;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint4 o = xor4(c[t], make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]));
+                gstore16(dp + 16 * t, o);
+                if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = b * 64 + 16 * t + 1;
+                if (!DEC) c[t] = o;
+            }
+            D5 dd;
+            const P5 c3 = p_from_words(c[3]);
+#pragma unroll
+            for (int i = 0; i < 5; i++) dd.v[i] = c3.v[i];
+            p_mac(dd, acc, p_lds(cr.rl));
+            p_mac(dd, p_from_words(c[0]), p_lds(cr.r3));
+            p_mac(dd, p_from_words(c[1]), p_lds(cr.r2));
+            p_mac(dd, p_from_words(c[2]), p_lds(cr.r1));
+            acc = p_reduce(dd);
+        }
+        for (; j < Jmax; j++) general(j);
+
         if (run && B == 0 && q == L - 1) vf = p_from_words(aadw);
-        /* rotated tree: logical ql = (q+1) % L, anchored at chunk B-2 */
+        /* rotated tree: logical ql = (q+1) % L, anchored at chunk B-2;
+         * level i combines with r^(4 * 2^i) */
+        const P5 r1 = p_lds(cr.r1), r2 = p_lds(cr.r2);
+        const P5 r4 = p_mul(r2, r2);
+        P5 rpow[LOGL + 1];
+        rpow[0] = r4;
+#pragma unroll
+        for (int i = 1; i <= LOGL; i++) rpow[i] = p_mul(rpow[i - 1], rpow[i - 1]);
         const int ql = (q + 1) % L;
 #pragma unroll
-        for (int i = Log2<L>::v - 1; i >= 0; i--) {
+        for (int i = LOGL - 1; i >= 0; i--) {
             const int sh = 1 << i;
             const int src_lane = (lane - q) + ((ql + sh + L - 1) % L);
             P5 o = shfl_p5<L>(acc, src_lane);
@@ -900,12 +1024,13 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         }
         /* in lane L-1: poly = r * (r * (vf + r^(4-delta) * W) + LEN) */
         const uint32_t delta = 4 - v;
-        P5 rd = delta == 0 ? r4 : (delta == 1 ? r3 : (delta == 2 ? r2 : r1));
+        P5 rd = delta == 0 ? r4 : (delta == 1 ? p_lds(cr.r3) : (delta == 2 ? r2 : r1));
         P5 X = p_add(p_mul(acc, rd), vf);
         X = p_mul(p_carry(X), r1);
         const uint32_t alen = run ? p.aad_len : 0;
         X = p_add(X, p_from_words(make_uint4(alen, 0, aead_len, 0)));
         X = p_mul(p_carry(X), r1);
+        const uint4 sw = make_uint4(cr.s[0], cr.s[1], cr.s[2], cr.s[3]);
         const uint4 tag = p_finish(X, sw);
         if (!run) continue;
         const int leader = lane - q + (L - 1);
@@ -924,7 +1049,12 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
             uint4 want = load_block(src, aead_len, aead_len + 16, aead_len + 16, 0, false);
             uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
             diff = __shfl(diff, leader);
-            uint32_t key2 = group_max<L>(nzkey);
+            uint32_t nzkey = 0;
+            if (tls13 && nzpos) {
+                const uint32_t pos = nzpos - 1;
+                nzkey = last_nonzero_key(load_block(dst, pos, aead_len, aead_len, 0, false), pos);
+            }
+            const uint32_t key2 = group_max<L>(nzkey);
             tlsrec_batch_res r;
             r.data_offset = p.data_offset;
             r.data_len = p.data_len;
