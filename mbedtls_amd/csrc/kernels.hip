@@ -913,6 +913,8 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
         const uint8_t inner_type = run ? p.inner_type : 0;
         const bool tls13 = run && p.tls13;
+        /* a readable 16-byte address for lanes with nothing to load */
+        const uint8_t *safe = run ? src : reinterpret_cast<const uint8_t *>(a.recs);
 
         P5 acc = p_zero(), vf = p_zero();
         uint32_t nzpos = 0;                 /* TLS 1.3: 1 + position of the last non-zero 16-B block */
@@ -923,23 +925,36 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             const int32_t b = (int32_t) (L * j + q) - (int32_t) z;
             const bool live = run && j < J;
             const bool valid = live && b >= 0 && (uint32_t) b < B;
+            /* all four loads first (full aligned blocks directly, the rest from
+             * a safe address and redone below), a ChaCha block ahead of use */
+            uint4 ct[4];
+            bool fast[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint32_t pos = (uint32_t) b * 64 + 16 * t;
+                fast[t] = valid && aligned && pos + 16 <= content_len;
+                ct[t] = gload16(fast[t] ? src + pos : safe);
+            }
+            asm volatile("" ::: "memory");
             uint32_t ks[16];
             chacha_block_kn(cr.key, (uint32_t) b + 1u, ks);
-            uint4 ct[4];
 #pragma unroll
-            for (int t = 0; t < 4; t++) ct[t] = make_uint4(0, 0, 0, 0);
-            if (valid) {
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const uint32_t pos = (uint32_t) b * 64 + 16 * t;
-                    if (pos < aead_len) {
-                        uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, aligned);
-                        uint4 o = mask_block(xor4(blk, make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3])),
-                                             pos, aead_len);
-                        store_block(dst, pos, aead_len, o, aligned);
-                        ct[t] = DEC ? blk : o;
-                        if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
-                    }
+            for (int t = 0; t < 4; t++) {
+                const uint32_t pos = (uint32_t) b * 64 + 16 * t;
+                const uint4 k = make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]);
+                if (fast[t]) {
+                    const uint4 o = xor4(ct[t], k);
+                    gstore16(dst + pos, o);
+                    if (!DEC) ct[t] = o;
+                    if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                } else if (valid && pos < aead_len) {
+                    const uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, aligned);
+                    const uint4 o = mask_block(xor4(blk, k), pos, aead_len);
+                    store_block(dst, pos, aead_len, o, aligned);
+                    ct[t] = DEC ? blk : o;
+                    if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                } else {
+                    ct[t] = make_uint4(0, 0, 0, 0);
                 }
             }
             /* Horner over this chunk's Poly1305 blocks (AAD folded before C_0) */
