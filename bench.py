@@ -33,12 +33,16 @@ SEED = 0x7115EC0DE
 
 CONFIGS = {
     # name: (cipher, tls, direction, content bytes, records, keys, workload text)
+    "c1": ("AES-128-GCM", "TLS1.2", "encrypt", 1400, 1024, 1,
+           "AES-128-GCM encrypt, 1024 x 1.4 KiB TLS 1.2 records, single key (plumbing check; the CPU leg is the reference-path restatement)"),
     "c2": ("AES-256-GCM", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
            "AES-256-GCM decrypt, 1M x 16 KiB TLS 1.3 application-data records, single key"),
     "c3": ("CHACHA20-POLY1305", "TLS1.3", "encrypt", 1400, 1 << 20, 1,
            "ChaCha20-Poly1305 encrypt, 1M x 1.4 KiB TLS 1.3 records, single key"),
     "c4": ("MIX", "TLS1.3", "decrypt", 16383, 1 << 22, 1 << 16,
            "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 16 KiB TLS 1.3 decrypt"),
+    "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
+            "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 1.4 KiB TLS 1.3 decrypt"),
 }
 
 
@@ -47,7 +51,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="c2 (default) = the metric's workload; c1/c3/c4/c4s = the other BASELINE configs")
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--align", type=int, default=128, help="record slot alignment in the arena (bytes; 128 = HBM/L2 line)")
@@ -86,9 +91,10 @@ def main():
     n = args.records or n_default
     ver = M.VERSION_TLS1_3 if tls == "TLS1.3" else M.VERSION_TLS1_2
     inner = inner_len(content, tls)
-    wire = inner + 16
+    head = 8 if tls == "TLS1.2" and cname != "CHACHA20-POLY1305" else 0   # TLS 1.2 GCM explicit nonce
+    wire = head + inner + 16
     stride = (wire + args.align - 1) // args.align * args.align
-    ciphers = {"AES-256-GCM": [M.CIPHER_AES_256_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
+    ciphers = {"AES-128-GCM": [M.CIPHER_AES_128_GCM], "AES-256-GCM": [M.CIPHER_AES_256_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
                "MIX": [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]}[cname]
     nkeys = min(nkeys, n)
 
@@ -99,7 +105,7 @@ def main():
         raw = prng_array(SEED, nkeys * 48).reshape(nkeys, 48)
         km["cipher"] = np.array([ciphers[i % len(ciphers)] for i in range(nkeys)], dtype=np.uint8)
         km["tls_minor"] = 4 if ver == M.VERSION_TLS1_3 else 3
-        km["fixed_ivlen"] = 12
+        km["fixed_ivlen"] = 4 if head else 12
         km["taglen"] = 16
         km["key"] = raw[:, :32]
         km["iv"][:, :12] = raw[:, 32:44]
@@ -117,7 +123,7 @@ def main():
     recs = M.records(n)
     recs["buf_off"] = np.arange(n, dtype=np.uint64) * stride
     recs["buf_len"] = stride
-    recs["data_offset"] = 0
+    recs["data_offset"] = head
     recs["data_len"] = content
     # records round-robin over keys: neighbours never share a
     # key; the engine's bucket pass groups them by key on the device
@@ -129,7 +135,7 @@ def main():
     recs_dev = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
     res_dev = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     sample = list(range(0, n, max(1, n // max(1, args.verify))))[:args.verify]
-    pt_sample = {i: arena[i * stride:i * stride + content].cpu().numpy().copy() for i in sample}
+    pt_sample = {i: arena[i * stride + head:i * stride + head + content].cpu().numpy().copy() for i in sample}
 
     if direction == "decrypt":
         # produce the ciphertexts with the (separately verified) encrypt kernel
@@ -138,6 +144,7 @@ def main():
         enc_status = res_dev.view(torch.int32)[0::4]
         assert int((enc_status != 0).sum()) == 0, "encrypt of the synthetic batch failed"
         dec = recs.copy()
+        dec["data_offset"] = 0
         dec["data_len"] = wire
         in_recs = torch.from_numpy(dec.view(np.uint8).copy()).to(dev)
         in_arena, out_arena = arena, torch.empty_like(arena)
@@ -179,7 +186,7 @@ def main():
     if direction == "decrypt":
         bad += int((lens != content).sum())
         for i in sample:
-            got = out_arena[i * stride:i * stride + content].cpu().numpy()
+            got = out_arena[i * stride + head:i * stride + head + content].cpu().numpy()
             bad += int(not np.array_equal(got, pt_sample[i]))
     bad_t = torch.tensor([bad], dtype=torch.int64, device=dev)
     if world > 1:
@@ -191,18 +198,20 @@ def main():
     oracle_ok = None
     if rank == 0 and args.verify:
         import oracle as O
-        oc = {M.CIPHER_AES_256_GCM: O.AES_256_GCM, M.CIPHER_CHACHA20_POLY1305: O.CHACHA20_POLY1305}
+        oc = {M.CIPHER_AES_128_GCM: O.AES_128_GCM, M.CIPHER_AES_256_GCM: O.AES_256_GCM,
+              M.CIPHER_CHACHA20_POLY1305: O.CHACHA20_POLY1305}
         oracle_ok = True
         src = arena if direction == "decrypt" else out_arena
         for i in sample[:16]:
             s = int(recs["slot"][i])
-            k = km[s] if rank == 0 else None
+            k = km[s]
+            klen = 16 if int(k["cipher"]) == M.CIPHER_AES_128_GCM else 32
             ot = O.Transform(O.TLS1_3 if ver == M.VERSION_TLS1_3 else O.TLS1_2, oc[int(k["cipher"])],
-                             bytes(k["key"]), bytes(k["key"]), bytes(k["iv"]), bytes(k["iv"]))
+                             bytes(k["key"][:klen]), bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
             buf = bytearray(stride)
-            buf[:content] = pt_sample[i].tobytes()
+            buf[head:head + content] = pt_sample[i].tobytes()
             orec = O.Record(ctr=bytes(recs["ctr"][i]), type=23, ver=b"\x03\x03", buf=buf,
-                            data_offset=0, data_len=content)
+                            data_offset=head, data_len=content)
             assert ot.encrypt_buf(orec) == 0
             got = src[i * stride:i * stride + wire].cpu().numpy().tobytes()
             oracle_ok &= got == orec.data()
@@ -268,13 +277,14 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
     """oracle/ (the CPU restatement, kind 'port') timed on this host's cores on
     a bounded sample of the same workload."""
     import oracle as O
-    cipher = O.CHACHA20_POLY1305 if cname == "CHACHA20-POLY1305" else O.AES_256_GCM
+    cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM}.get(cname, O.AES_256_GCM)
     k = km[0]
-    t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"]), bytes(k["key"]),
-                    bytes(k["iv"]), bytes(k["iv"]))
+    klen = 16 if cipher == O.AES_128_GCM else 32
+    t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"][:klen]),
+                    bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
     threads = min(16, os.cpu_count() or 1)
     from tests.prng import prng_array
-    n = 256
+    n = 1024
     while True:
         arena = np.zeros(n * stride, dtype=np.uint8)
         payload = prng_array(SEED ^ 0xC0FFEE, n * content).reshape(n, content)
@@ -289,9 +299,9 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
             st = np.zeros(n, dtype=np.int32)
             el = t.bench(1, arena, stride, content, n, 0, threads, st)
             assert (st == 0).all()
-        if el >= target_s or n >= (1 << 18):
+        if el >= target_s or n * stride >= (4 << 30):
             break
-        n = int(n * max(2.0, min(8.0, target_s / max(el, 1e-3))))
+        n = min(int(n * max(2.0, min(8.0, target_s / max(el, 1e-3)))), (4 << 30) // stride)
     gib = n * inner / el / 2**30
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{n} records x {inner} B inner plaintext, {direction}, oracle/liboracle.so "

@@ -218,3 +218,100 @@ class Transform:
         st = status.ctypes.data if status is not None else None
         return lib().orc_bench_records(self._mem, direction, a.ctypes.data, stride,
                                        data_len, n, seq0, threads, st)
+
+
+# ---- TLS 1.3 key schedule (oracle/keysched.c) ---------------------------------
+SHA256 = 0x02000009          # PSA_ALG_SHA_256
+SHA384 = 0x0200000a          # PSA_ALG_SHA_384
+HASHES = {"sha256": SHA256, "sha384": SHA384}
+CONTEXT_UNHASHED, CONTEXT_HASHED = 0, 1
+
+
+def hash_len(alg: int) -> int:
+    return {SHA256: 32, SHA384: 48}[alg]
+
+
+def _ks(fn, argtypes):
+    f = getattr(lib(), fn)
+    f.argtypes = argtypes
+    f.restype = ctypes.c_int
+    return f
+
+
+_P, _S = ctypes.c_char_p, ctypes.c_size_t
+
+
+def _chk(r, what):
+    if r != 0:
+        raise ValueError(f"{what} failed: {r}")
+
+
+def sha(alg: int, msg: bytes) -> bytes:
+    out = _buf(64)
+    _chk(_ks("orc_hash", [ctypes.c_int, _P, _S, ctypes.c_void_p])(alg, msg, len(msg), out), "orc_hash")
+    return out.raw[:hash_len(alg)]
+
+
+def hmac(alg: int, key: bytes, msg: bytes) -> bytes:
+    out = _buf(64)
+    _chk(_ks("orc_hmac", [ctypes.c_int, _P, _S, _P, _S, ctypes.c_void_p])(alg, key, len(key), msg, len(msg), out),
+         "orc_hmac")
+    return out.raw[:hash_len(alg)]
+
+
+def hkdf_expand(alg: int, prk: bytes, info: bytes, n: int) -> bytes:
+    out = _buf(max(1, n))
+    _chk(_ks("orc_hkdf_expand", [ctypes.c_int, _P, _S, _P, _S, ctypes.c_void_p, _S])(
+        alg, prk, len(prk), info, len(info), out, n), "orc_hkdf_expand")
+    return out.raw[:n]
+
+
+def tls13_encode_label(n: int, label: bytes, ctx: bytes) -> bytes:
+    out = _buf(2 + 1 + 6 + 249 + 1 + 64)
+    f = getattr(lib(), "orc_tls13_encode_label")
+    f.argtypes = [_S, _P, _S, _P, _S, ctypes.c_void_p]
+    f.restype = _S
+    k = f(n, label, len(label), ctx, len(ctx), out)
+    return out.raw[:k]
+
+
+def tls13_hkdf_expand_label(alg: int, secret: bytes, label: bytes, ctx: bytes, n: int) -> bytes:
+    out = _buf(max(1, n))
+    _chk(_ks("orc_tls13_hkdf_expand_label", [ctypes.c_int, _P, _S, _P, _S, _P, _S, ctypes.c_void_p, _S])(
+        alg, secret, len(secret), label, len(label), ctx, len(ctx), out, n), "expand_label")
+    return out.raw[:n]
+
+
+def tls13_derive_secret(alg: int, secret: bytes, label: bytes, ctx: bytes, ctx_hashed: int, n: int) -> bytes:
+    out = _buf(max(1, n))
+    _chk(_ks("orc_tls13_derive_secret", [ctypes.c_int, _P, _S, _P, _S, _P, _S, ctypes.c_int, ctypes.c_void_p, _S])(
+        alg, secret, len(secret), label, len(label), ctx, len(ctx), ctx_hashed, out, n), "derive_secret")
+    return out.raw[:n]
+
+
+def tls13_evolve_secret(alg: int, secret_old: bytes | None, inp: bytes | None) -> bytes:
+    out = _buf(64)
+    _chk(_ks("orc_tls13_evolve_secret", [ctypes.c_int, _P, _P, _S, ctypes.c_void_p])(
+        alg, secret_old or None, inp or None, len(inp or b""), out), "evolve_secret")
+    return out.raw[:hash_len(alg)]
+
+
+def tls13_make_traffic_keys(alg: int, client_secret: bytes, server_secret: bytes, key_len: int, iv_len: int):
+    ck, ci, sk, si = _buf(32), _buf(16), _buf(32), _buf(16)
+    _chk(_ks("orc_tls13_make_traffic_keys", [ctypes.c_int, _P, _P, _S, _S, _S] + [ctypes.c_void_p] * 4)(
+        alg, client_secret, server_secret, len(client_secret), key_len, iv_len, ck, ci, sk, si), "make_traffic_keys")
+    return ck.raw[:key_len], ci.raw[:iv_len], sk.raw[:key_len], si.raw[:iv_len]
+
+
+def tls13_exporter(alg: int, secret: bytes, label: bytes, context: bytes, n: int) -> bytes:
+    out = _buf(max(1, n))
+    _chk(_ks("orc_tls13_exporter", [ctypes.c_int, _P, _S, _P, _S, _P, _S, ctypes.c_void_p, _S])(
+        alg, secret, len(secret), label, len(label), context, len(context), out, n), "exporter")
+    return out.raw[:n]
+
+
+def tls13_update_traffic_secret(alg: int, secret: bytes) -> bytes:
+    out = _buf(64)
+    _chk(_ks("orc_tls13_update_traffic_secret", [ctypes.c_int, _P, ctypes.c_void_p])(alg, secret, out),
+         "update_traffic_secret")
+    return out.raw[:hash_len(alg)]

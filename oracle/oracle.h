@@ -156,6 +156,37 @@ double orc_bench_records(const orc_transform *t, int dir, uint8_t *arena,
                          size_t stride, size_t data_len, uint64_t n,
                          uint64_t seq0, int threads, int32_t *status);
 
+/* ---- TLS 1.3 key schedule (oracle/keysched.c) -------------------------- */
+/* hash identifiers: the psa_algorithm_t values PSA_ALG_SHA_256 / _384 of the
+ * PSA Crypto API (the reference passes psa_algorithm_t hash_alg) */
+#define ORC_HASH_SHA256 0x02000009
+#define ORC_HASH_SHA384 0x0200000a
+#define ORC_TLS13_CONTEXT_UNHASHED 0     /* MBEDTLS_SSL_TLS1_3_CONTEXT_UNHASHED, ssl_tls13_keys.h */
+#define ORC_TLS13_CONTEXT_HASHED   1
+
+size_t orc_hash_len(int alg);
+int orc_hash(int alg, const uint8_t *msg, size_t len, uint8_t *out);
+int orc_hmac(int alg, const uint8_t *key, size_t klen, const uint8_t *msg, size_t len, uint8_t *out);
+int orc_hkdf_extract(int alg, const uint8_t *salt, size_t salt_len, const uint8_t *ikm, size_t ikm_len,
+                     uint8_t *prk);
+int orc_hkdf_expand(int alg, const uint8_t *prk, size_t prk_len, const uint8_t *info, size_t info_len,
+                    uint8_t *out, size_t out_len);
+size_t orc_tls13_encode_label(size_t desired, const uint8_t *label, size_t label_len, const uint8_t *ctx,
+                              size_t ctx_len, uint8_t *dst);
+int orc_tls13_hkdf_expand_label(int alg, const uint8_t *secret, size_t secret_len, const uint8_t *label,
+                                size_t label_len, const uint8_t *ctx, size_t ctx_len, uint8_t *buf, size_t buf_len);
+int orc_tls13_derive_secret(int alg, const uint8_t *secret, size_t secret_len, const uint8_t *label,
+                            size_t label_len, const uint8_t *ctx, size_t ctx_len, int ctx_hashed, uint8_t *dst,
+                            size_t dst_len);
+int orc_tls13_evolve_secret(int alg, const uint8_t *secret_old, const uint8_t *input, size_t input_len,
+                            uint8_t *secret_new);
+int orc_tls13_make_traffic_keys(int alg, const uint8_t *client_secret, const uint8_t *server_secret,
+                                size_t secret_len, size_t key_len, size_t iv_len, uint8_t *client_key,
+                                uint8_t *client_iv, uint8_t *server_key, uint8_t *server_iv);
+int orc_tls13_exporter(int alg, const uint8_t *secret, size_t secret_len, const uint8_t *label, size_t label_len,
+                       const uint8_t *context, size_t context_len, uint8_t *out, size_t out_len);
+int orc_tls13_update_traffic_secret(int alg, const uint8_t *secret, uint8_t *next);
+
 #ifdef __cplusplus
 }
 #endif
