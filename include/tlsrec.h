@@ -201,6 +201,72 @@ int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
 int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_batch_rec *rec,
                        tlsrec_batch_res *early, uint32_t *aead_pos, uint32_t *aead_len);
 
+/* ---- TLS 1.3 key schedule (library/ssl_tls13_keys.c) --------------------
+ * HKDF-SHA256/384 on the GPU: the reference's single-shot functions with the
+ * same arguments and return codes, plus a batch that derives many
+ * connections' record keys straight into a device key table.  Hash
+ * identifiers are the psa_algorithm_t values the reference passes. */
+#define TLSREC_ALG_SHA_256   0x02000009   /* PSA_ALG_SHA_256 */
+#define TLSREC_ALG_SHA_384   0x0200000a   /* PSA_ALG_SHA_384 */
+#define TLSREC_TLS13_CONTEXT_UNHASHED 0   /* MBEDTLS_SSL_TLS1_3_CONTEXT_UNHASHED, ssl_tls13_keys.h:35 */
+#define TLSREC_TLS13_CONTEXT_HASHED   1   /* MBEDTLS_SSL_TLS1_3_CONTEXT_HASHED, ssl_tls13_keys.h:36 */
+
+/* struct mbedtls_ssl_key_set, library/ssl_misc.h:604-618 */
+typedef struct tlsrec_key_set {
+    unsigned char client_write_key[32];
+    unsigned char server_write_key[32];
+    unsigned char client_write_iv[16];
+    unsigned char server_write_iv[16];
+    size_t key_len;
+    size_t iv_len;
+} tlsrec_key_set;
+
+/* mbedtls_ssl_tls13_hkdf_expand_label, ssl_tls13_keys.c:138-217 (label
+ * without the "tls13 " prefix, <= 249 B; ctx <= 64 B; buf_len <= 255*64) */
+int tlsrec_tls13_hkdf_expand_label(int hash_alg, const unsigned char *secret, size_t secret_len,
+                                   const unsigned char *label, size_t label_len,
+                                   const unsigned char *ctx, size_t ctx_len,
+                                   unsigned char *buf, size_t buf_len);
+/* mbedtls_ssl_tls13_derive_secret, ssl_tls13_keys.c:293-330 */
+int tlsrec_tls13_derive_secret(int hash_alg, const unsigned char *secret, size_t secret_len,
+                               const unsigned char *label, size_t label_len,
+                               const unsigned char *ctx, size_t ctx_len, int ctx_hashed,
+                               unsigned char *dstbuf, size_t dstbuf_len);
+/* mbedtls_ssl_tls13_evolve_secret, ssl_tls13_keys.c:332-419 (secret_old may
+ * be NULL: initial stage; input NULL or empty: all-zero IKM) */
+int tlsrec_tls13_evolve_secret(int hash_alg, const unsigned char *secret_old,
+                               const unsigned char *input, size_t input_len,
+                               unsigned char *secret_new);
+/* mbedtls_ssl_tls13_make_traffic_keys, ssl_tls13_keys.c:262-291 */
+int tlsrec_tls13_make_traffic_keys(int hash_alg, const unsigned char *client_secret,
+                                   const unsigned char *server_secret, size_t secret_len,
+                                   size_t key_len, size_t iv_len, tlsrec_key_set *keys);
+/* mbedtls_ssl_tls13_exporter, ssl_tls13_keys.c:1828-1858 */
+int tlsrec_tls13_exporter(int hash_alg, const unsigned char *secret, size_t secret_len,
+                          const unsigned char *label, size_t label_len,
+                          const unsigned char *context_value, size_t context_len,
+                          unsigned char *out, size_t out_len);
+/* KeyUpdate (RFC 8446 7.2; label "traffic upd", ssl_tls13_keys.h:16):
+ * next = HKDF-Expand-Label(secret, "traffic upd", "", Hash.length) */
+int tlsrec_tls13_update_traffic_secret(int hash_alg, const unsigned char *secret,
+                                       unsigned char *next);
+
+/* One direction's traffic secret (client_application_traffic_secret_N or
+ * server_...), 48 bytes; SHA-256 suites use the first 32. */
+typedef struct tlsrec_tls13_secret {
+    uint8_t secret[48];
+} tlsrec_tls13_secret;
+
+/* Batch: for each of `count` device-resident secrets, optionally first apply
+ * a KeyUpdate in place (key_update != 0), then derive write_key / write_iv as
+ * ssl_tls13_make_traffic_key does (ssl_tls13_keys.c:219-246) and load them
+ * into slots first..first+count-1 of `kt` as TLS 1.3 keys of `cipher` (the
+ * suite fixes the hash: AES-256-GCM -> SHA-384, others -> SHA-256; key
+ * expansion and GHASH tables as tlsrec_keytab_load).  Asynchronous on
+ * `stream`; the secrets buffer must stay valid until the stream reaches it. */
+int tlsrec_tls13_keytab_derive(tlsrec_keytab *kt, uint32_t first, uint32_t count, int cipher,
+                               tlsrec_tls13_secret *secrets, int key_update, void *stream);
+
 /* ---- engine ------------------------------------------------------------- */
 /* 0 if a gfx950 device is usable, else TLSREC_ERR_SSL_HW_ACCEL_FAILED. */
 int tlsrec_device_check(void);

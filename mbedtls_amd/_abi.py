@@ -30,6 +30,10 @@ CIPHER_AES_128_GCM = 1
 CIPHER_AES_256_GCM = 2
 CIPHER_CHACHA20_POLY1305 = 3
 MSG_APPLICATION_DATA = 23
+ALG_SHA_256 = 0x02000009      # PSA_ALG_SHA_256
+ALG_SHA_384 = 0x0200000a      # PSA_ALG_SHA_384
+TLS13_CONTEXT_UNHASHED = 0
+TLS13_CONTEXT_HASHED = 1
 
 # ---- layouts -----------------------------------------------------------------
 KEY_MATERIAL = np.dtype([("cipher", "u1"), ("tls_minor", "u1"), ("fixed_ivlen", "u1"),
@@ -54,6 +58,13 @@ class CTransform(ctypes.Structure):
                 ("granularity", ctypes.c_uint32)]
 
 
+class CKeySet(ctypes.Structure):
+    """struct mbedtls_ssl_key_set (library/ssl_misc.h:604-618)"""
+    _fields_ = [("client_write_key", ctypes.c_ubyte * 32), ("server_write_key", ctypes.c_ubyte * 32),
+                ("client_write_iv", ctypes.c_ubyte * 16), ("server_write_iv", ctypes.c_ubyte * 16),
+                ("key_len", ctypes.c_size_t), ("iv_len", ctypes.c_size_t)]
+
+
 class CRecord(ctypes.Structure):
     _fields_ = [("ctr", ctypes.c_ubyte * 8), ("type", ctypes.c_ubyte), ("ver", ctypes.c_ubyte * 2),
                 ("buf", ctypes.c_void_p), ("buf_len", ctypes.c_size_t),
@@ -61,7 +72,7 @@ class CRecord(ctypes.Structure):
 
 
 # every function include/tlsrec.h declares, with its signature
-_VP, _U32, _INT = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+_VP, _U32, _INT, _SZ = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t
 SIGNATURES = {
     "tlsrec_transform_setup": (_INT, [_VP, _INT, _INT, _VP, _VP, _VP, _VP]),
     "tlsrec_transform_setup_ex": (_INT, [_VP, _INT, _INT, _VP, _VP, _VP, _VP, ctypes.c_uint]),
@@ -76,6 +87,13 @@ SIGNATURES = {
     "tlsrec_batch_decrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
     "tlsrec_frame_check": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP]),
     "tlsrec_device_check": (_INT, []),
+    "tlsrec_tls13_hkdf_expand_label": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _VP, _SZ]),
+    "tlsrec_tls13_derive_secret": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _INT, _VP, _SZ]),
+    "tlsrec_tls13_evolve_secret": (_INT, [_INT, _VP, _VP, _SZ, _VP]),
+    "tlsrec_tls13_make_traffic_keys": (_INT, [_INT, _VP, _VP, _SZ, _SZ, _SZ, _VP]),
+    "tlsrec_tls13_exporter": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _VP, _SZ]),
+    "tlsrec_tls13_update_traffic_secret": (_INT, [_INT, _VP, _VP]),
+    "tlsrec_tls13_keytab_derive": (_INT, [_VP, _U32, _U32, _INT, _VP, _INT, _VP]),
     "tlsrec_version_string": (ctypes.c_char_p, []),
 }
 

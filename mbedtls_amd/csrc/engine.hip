@@ -143,6 +143,22 @@ extern "C" int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t co
     return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, src, first, count, st));
 }
 
+/* Device-side producers of key material (keysched.hip) write into the
+ * table's staging area and then commit: bookkeeping as tlsrec_keytab_load,
+ * then the key-setup kernel on the staged slots. */
+extern "C" tlsrec_key_material *tlsrec__keytab_stage(tlsrec_keytab *kt) { return kt->d_stage; }
+
+extern "C" int tlsrec__keytab_commit_staged(tlsrec_keytab *kt, uint32_t first, uint32_t count, int cipher,
+                                            hipStream_t st)
+{
+    for (uint32_t i = 0; i < count; i++) {
+        if (kt->h_cipher[first + i] == 0) kt->nloaded++;
+        kt->h_cipher[first + i] = (uint8_t) cipher;
+    }
+    kt->cipher_mask |= 1u << cipher;
+    return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, kt->d_stage + first, first, count, st));
+}
+
 /* waves per GCM workgroup: 16 (default) or 8; TLSREC_GCM_WAVES overrides */
 static int gcm_waves(void)
 {

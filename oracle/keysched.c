@@ -261,7 +261,7 @@ int orc_tls13_hkdf_expand_label(int alg, const uint8_t *secret, size_t secret_le
                                 size_t label_len, const uint8_t *ctx, size_t ctx_len, uint8_t *buf, size_t buf_len)
 {
     if (label_len > ORC_TLS13_MAX_LABEL || ctx_len > ORC_TLS13_MAX_CONTEXT) return ORC_ERR_SSL_INTERNAL_ERROR;
-    if (buf_len > 255 * 32) return ORC_ERR_SSL_INTERNAL_ERROR;   /* MAX_EXPANSION_LEN, ssl_tls13_keys.h:78 */
+    if (buf_len > 255 * 64) return ORC_ERR_SSL_INTERNAL_ERROR;   /* MAX_EXPANSION_LEN = 255 * PSA_HASH_MAX_SIZE, ssl_tls13_keys.h:78 */
     if (!orc_hash_len(alg)) return ORC_ERR_SSL_BAD_INPUT_DATA;
     uint8_t info[2 + 1 + 6 + ORC_TLS13_MAX_LABEL + 1 + ORC_TLS13_MAX_CONTEXT];
     size_t n = orc_tls13_encode_label(buf_len, label, label_len, ctx, ctx_len, info);

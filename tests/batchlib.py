@@ -63,11 +63,14 @@ class Batch:
         km = np.concatenate([M.key_material(c, v, k, iv, g) for (c, v, k, iv, g) in self.slots])
         return km
 
-    def run_gpu(self, decrypt: bool, lanes=0, inplace=True):
+    def run_gpu(self, decrypt: bool, lanes=0, inplace=True, kt=None):
+        """kt: an already loaded key table (e.g. filled by keytab_derive)."""
         import torch
         dev = torch.device("cuda")
-        kt = M.KeyTable(max(1, len(self.slots)))
-        kt.load(self.key_materials())
+        own = kt is None
+        if own:
+            kt = M.KeyTable(max(1, len(self.slots)))
+            kt.load(self.key_materials())
         arena = torch.from_numpy(self.arena.copy()).to(dev)
         out = arena if inplace else torch.zeros_like(arena)
         recs = torch.from_numpy(self.desc.view(np.uint8).copy()).to(dev)
@@ -77,7 +80,8 @@ class Batch:
         torch.cuda.synchronize()
         out_np = out.cpu().numpy()
         res_np = res.cpu().numpy().view(M.BATCH_RES)
-        kt.close()
+        if own:
+            kt.close()
         return out_np, res_np
 
     def run_oracle(self, decrypt: bool):
