@@ -315,3 +315,60 @@ def tls13_update_traffic_secret(alg: int, secret: bytes) -> bytes:
     _chk(_ks("orc_tls13_update_traffic_secret", [ctypes.c_int, _P, ctypes.c_void_p])(alg, secret, out),
          "update_traffic_secret")
     return out.raw[:hash_len(alg)]
+
+
+# ---- stream record loops (oracle/stream.c) -------------------------------------
+ERR_COUNTER_WRAPPING = -0x6B80
+MAX_IN_RECORD = 16421
+OUT_BUF_SPACE = 16416
+
+
+class _StreamRec(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint32), ("data_offset", ctypes.c_uint32), ("data_len", ctypes.c_uint32),
+                ("type", ctypes.c_uint8)]
+
+
+class _StreamRes(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("nrec", ctypes.c_uint32), ("consumed", ctypes.c_uint32),
+                ("in_ctr", ctypes.c_uint8 * 8), ("nb_zero", ctypes.c_uint8)]
+
+
+def stream_decrypt(t: "Transform", data: bytes, in_ctr: bytes = bytes(8), nb_zero: int = 0,
+                   max_record: int = MAX_IN_RECORD, max_version: int = TLS1_3):
+    """Returns (res dict, [(off, data_offset, data_len, type)], buffer after)."""
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    cap = len(data) // 6 + 1
+    recs = (_StreamRec * cap)()
+    res = _StreamRes()
+    f = lib().orc_stream_decrypt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _S, ctypes.c_char_p, ctypes.c_uint8, _S, ctypes.c_int,
+                  ctypes.c_void_p, _S, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    f(t._mem, buf, len(data), bytes(in_ctr), nb_zero, max_record, max_version, recs, cap, ctypes.byref(res))
+    out = [(r.off, r.data_offset, r.data_len, r.type) for r in recs[:res.nrec]]
+    return ({"status": res.status, "nrec": res.nrec, "consumed": res.consumed, "in_ctr": bytes(res.in_ctr),
+             "nb_zero": res.nb_zero}, out, buf.raw[:len(data)])
+
+
+def stream_record_wire(t: "Transform", n: int) -> int:
+    f = lib().orc_stream_record_wire
+    f.argtypes = [ctypes.c_void_p, _S]
+    f.restype = _S
+    return f(t._mem, n)
+
+
+def stream_encrypt(t: "Transform", pt: bytes, rtype: int = 23, out_ctr: bytes = bytes(8), max_frag: int = 16384,
+                   out_buf_space: int = OUT_BUF_SPACE):
+    """Returns (status, record stream bytes, records, out_ctr after)."""
+    cap = sum(stream_record_wire(t, min(max_frag, len(pt) - o)) for o in range(0, len(pt), max_frag)) + 16
+    out = ctypes.create_string_buffer(cap)
+    ctr = (ctypes.c_uint8 * 8)(*out_ctr)
+    olen = _S()
+    nrec = ctypes.c_uint32()
+    f = lib().orc_stream_encrypt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, _S, ctypes.c_uint8, ctypes.c_void_p, _S, _S, ctypes.c_void_p, _S,
+                  ctypes.c_void_p, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    r = f(t._mem, bytes(pt), len(pt), rtype, ctr, max_frag, out_buf_space, out, cap, ctypes.byref(olen),
+          ctypes.byref(nrec))
+    return r, out.raw[:olen.value], nrec.value, bytes(ctr)

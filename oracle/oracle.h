@@ -187,6 +187,32 @@ int orc_tls13_exporter(int alg, const uint8_t *secret, size_t secret_len, const 
                        const uint8_t *context, size_t context_len, uint8_t *out, size_t out_len);
 int orc_tls13_update_traffic_secret(int alg, const uint8_t *secret, uint8_t *next);
 
+/* ---- stream record loops (oracle/stream.c) ------------------------------ */
+#define ORC_ERR_SSL_COUNTER_WRAPPING (-0x6B80)   /* ssl.h */
+#define ORC_IN_CONTENT_LEN 16384                 /* MBEDTLS_SSL_IN_CONTENT_LEN, ssl.h:405 */
+/* AEAD-only build: IN_BUFFER_LEN (13 + 16 + 16 + 16384) minus the 8-byte
+ * in_hdr offset = largest header+body fetch_input accepts; OUT buffer space
+ * from out_iv = 16416 (ssl_misc.h:300-392). */
+#define ORC_MAX_IN_RECORD 16421
+#define ORC_OUT_BUF_SPACE 16416
+
+typedef struct { uint32_t off, data_offset, data_len; uint8_t type; } orc_stream_rec;
+typedef struct {
+    int32_t status;          /* error that ended the stream, 0 = all complete records accepted */
+    uint32_t nrec;           /* records accepted */
+    uint32_t consumed;       /* bytes of the accepted records */
+    uint8_t in_ctr[8];
+    uint8_t nb_zero;
+} orc_stream_res;
+
+int orc_stream_decrypt(const orc_transform *t, uint8_t *buf, size_t len, const uint8_t in_ctr[8], uint8_t nb_zero,
+                       size_t max_record, int max_version, orc_stream_rec *out, size_t max_out,
+                       orc_stream_res *res);
+size_t orc_stream_record_wire(const orc_transform *t, size_t n);
+int orc_stream_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, uint8_t type, uint8_t out_ctr[8],
+                       size_t max_frag, size_t out_buf_space, uint8_t *out, size_t out_cap, size_t *out_len,
+                       uint32_t *nrec);
+
 #ifdef __cplusplus
 }
 #endif
