@@ -267,6 +267,83 @@ typedef struct tlsrec_tls13_secret {
 int tlsrec_tls13_keytab_derive(tlsrec_keytab *kt, uint32_t first, uint32_t count, int cipher,
                                tlsrec_tls13_secret *secrets, int key_update, void *stream);
 
+/* ---- TLS stream record layer --------------------------
+ * Whole-connection framing on the device: received byte streams are split at
+ * their 5-byte record headers, checked and decrypted in place; application
+ * data is split into records, framed and encrypted into record streams.  Per
+ * connection the result is what repeated ssl_get_next_record calls
+ * (ssl_msg.c:4700-4900: ssl_parse_record_header :3561-3776,
+ * ssl_prepare_record_content :3810-4017) or repeated mbedtls_ssl_write calls
+ * (mbedtls_ssl_write_record :2648-2793) produce.  All arrays are device
+ * memory; the calls synchronise `stream` once (to size the record batch). */
+#define TLSREC_MAX_IN_RECORD  16421  /* header + body limit of mbedtls_ssl_fetch_input (AEAD-only build:
+                                        MBEDTLS_SSL_IN_BUFFER_LEN 16429 minus the 8-byte in_hdr offset) */
+#define TLSREC_OUT_BUF_SPACE  16416  /* out_buf_len - (out_iv - out_buf), ssl_msg.c:2688 (AEAD-only build) */
+#define TLSREC_ERR_SSL_COUNTER_WRAPPING (-0x6B80)   /* ssl.h:119 */
+
+/* One connection's received bytes, starting at a record header (ssl->in_hdr). */
+typedef struct tlsrec_stream_in {
+    uint64_t off;            /* first byte in the arena */
+    uint32_t len;            /* bytes received (ssl->in_left) */
+    uint32_t slot;           /* key slot of transform_in */
+    uint8_t  in_ctr[8];      /* ssl->in_ctr */
+    uint8_t  nb_zero;        /* ssl->nb_zero */
+    uint8_t  reserved[7];
+} tlsrec_stream_in;
+
+typedef struct tlsrec_stream_in_res {
+    int32_t  status;         /* 0: every complete record accepted (a trailing partial record waits);
+                                else the error the reference returns for the first bad record */
+    uint32_t first;          /* this connection's records are recs/res[first .. first+nparsed) */
+    uint32_t nrec;           /* records accepted, in order; record k's plaintext is at
+                                arena + recs[first+k].buf_off + res[first+k].data_offset */
+    uint32_t consumed;       /* bytes of the accepted records (the next call starts there) */
+    uint8_t  in_ctr[8];      /* ssl->in_ctr afterwards */
+    uint8_t  nb_zero;
+    uint8_t  reserved[3];
+    uint32_t nparsed;        /* records framed (bytes of records after a failing one are unspecified) */
+} tlsrec_stream_in_res;
+
+/* `recs` / `res`: device arrays of max_records entries, filled by the call.
+ * *nrecords (host, may be NULL) = records framed over all connections.
+ * Returns TLSREC_ERR_SSL_BUFFER_TOO_SMALL (nothing decrypted) if the
+ * connections hold more than max_records complete records. */
+int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_stream_in *streams, uint32_t nstreams,
+                          uint8_t *arena, tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                          uint32_t max_records, tlsrec_stream_in_res *sres, uint32_t *nrecords,
+                          void *stream);
+
+/* One connection's application data to send. */
+typedef struct tlsrec_stream_out {
+    uint64_t in_off;         /* plaintext in the input arena */
+    uint32_t in_len;
+    uint32_t slot;           /* key slot of transform_out */
+    uint64_t out_off;        /* record stream destination in the output arena */
+    uint8_t  out_ctr[8];     /* ssl->cur_out_ctr */
+    uint32_t max_frag;       /* mbedtls_ssl_get_max_out_record_payload(); 0 = 16384 */
+    uint8_t  type;           /* ssl->out_msgtype, normally 23 */
+    uint8_t  reserved[3];
+} tlsrec_stream_out;
+
+typedef struct tlsrec_stream_out_res {
+    int32_t  status;         /* 0 or the first record's error (COUNTER_WRAPPING after the record) */
+    uint32_t first;          /* records recs/res[first .. first+nparsed) */
+    uint32_t nrec;           /* records written */
+    uint32_t out_len;        /* bytes of record stream written at out_off */
+    uint8_t  out_ctr[8];     /* cur_out_ctr afterwards */
+    uint32_t nparsed;
+    uint8_t  reserved[4];
+} tlsrec_stream_out_res;
+
+/* Bytes of record stream `in_len` bytes of application data become (host
+ * helper for sizing out_arena; 0 for an unsupported suite). */
+uint64_t tlsrec_stream_out_size(int tls_version, int cipher, uint32_t granularity, uint64_t in_len,
+                                uint32_t max_frag);
+int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_out *streams, uint32_t nstreams,
+                          const uint8_t *in_arena, uint8_t *out_arena, tlsrec_batch_rec *recs,
+                          tlsrec_batch_res *res, uint32_t max_records, tlsrec_stream_out_res *sres,
+                          uint32_t *nrecords, void *stream);
+
 /* ---- engine ------------------------------------------------------------- */
 /* 0 if a gfx950 device is usable, else TLSREC_ERR_SSL_HW_ACCEL_FAILED. */
 int tlsrec_device_check(void);

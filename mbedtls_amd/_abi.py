@@ -23,6 +23,9 @@ ERR_SSL_INVALID_MAC = -0x7180
 ERR_SSL_INVALID_RECORD = -0x7200
 ERR_SSL_HW_ACCEL_FAILED = -0x7F80
 ERR_SSL_INTERNAL_ERROR = -0x6C00
+ERR_SSL_COUNTER_WRAPPING = -0x6B80
+MAX_IN_RECORD = 16421
+OUT_BUF_SPACE = 16416
 
 VERSION_TLS1_2 = 0x0303
 VERSION_TLS1_3 = 0x0304
@@ -44,6 +47,16 @@ BATCH_REC = np.dtype([("buf_off", "<u8"), ("buf_len", "<u4"), ("data_offset", "<
                       ("ver", "u1", 2), ("reserved", "u1", 5)])
 BATCH_RES = np.dtype([("status", "<i4"), ("data_offset", "<u4"), ("data_len", "<u4"),
                       ("type", "u1"), ("reserved", "u1", 3)])
+STREAM_IN = np.dtype([("off", "<u8"), ("len", "<u4"), ("slot", "<u4"), ("in_ctr", "u1", 8),
+                      ("nb_zero", "u1"), ("reserved", "u1", 7)])
+STREAM_IN_RES = np.dtype([("status", "<i4"), ("first", "<u4"), ("nrec", "<u4"), ("consumed", "<u4"),
+                          ("in_ctr", "u1", 8), ("nb_zero", "u1"), ("reserved", "u1", 3), ("nparsed", "<u4")])
+STREAM_OUT = np.dtype([("in_off", "<u8"), ("in_len", "<u4"), ("slot", "<u4"), ("out_off", "<u8"),
+                       ("out_ctr", "u1", 8), ("max_frag", "<u4"), ("type", "u1"), ("reserved", "u1", 3)])
+STREAM_OUT_RES = np.dtype([("status", "<i4"), ("first", "<u4"), ("nrec", "<u4"), ("out_len", "<u4"),
+                           ("out_ctr", "u1", 8), ("nparsed", "<u4"), ("reserved", "u1", 4)])
+assert STREAM_IN.itemsize == 32 and STREAM_IN_RES.itemsize == 32
+assert STREAM_OUT.itemsize == 40 and STREAM_OUT_RES.itemsize == 32
 assert KEY_MATERIAL.itemsize == 64 and BATCH_REC.itemsize == 40 and BATCH_RES.itemsize == 16
 
 
@@ -94,6 +107,9 @@ SIGNATURES = {
     "tlsrec_tls13_exporter": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _VP, _SZ]),
     "tlsrec_tls13_update_traffic_secret": (_INT, [_INT, _VP, _VP]),
     "tlsrec_tls13_keytab_derive": (_INT, [_VP, _U32, _U32, _INT, _VP, _INT, _VP]),
+    "tlsrec_stream_decrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
+    "tlsrec_stream_out_size": (ctypes.c_uint64, [_INT, _INT, _U32, ctypes.c_uint64, _U32]),
+    "tlsrec_stream_encrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_version_string": (ctypes.c_char_p, []),
 }
 

@@ -1,0 +1,458 @@
+/*
+ * stream.hip -- the TLS record layer over whole connections.
+ *
+ * Receive: each connection's received bytes (a TLS byte stream starting at a
+ * record header) are split at their 5-byte headers and checked as
+ * ssl_parse_record_header does (library/ssl_msg.c:3561-3776, TLS branch, with
+ * the mbedtls_ssl_fetch_input size limit); every complete record becomes a
+ * batch descriptor (implicit sequence number = in_ctr + records before it,
+ * TLS 1.3 ChangeCipherSpec passed through undecrypted as at :3819-3825); the
+ * batch is decrypted in place by the AEAD kernels; a per-connection pass then
+ * applies ssl_prepare_record_content's post-decrypt rules in record order
+ * (:3870-3917 zero-length records, :3930-3963 in_ctr increment and
+ * COUNTER_WRAPPING, :4011-4014 IN_CONTENT_LEN) and stops at the first error.
+ *
+ * Send: each connection's application data is cut into records of at most
+ * max_frag bytes (one mbedtls_ssl_write call each), laid out back to back in
+ * the output stream with their headers (mbedtls_ssl_write_record
+ * :2648-2793: TLS 1.3 records carry version 0x0303, the length field is the
+ * protected length), and encrypted in place by the AEAD kernels.
+ *
+ * Header walking is one lane per connection (each header names the next);
+ * connections walk in parallel.  Bulk bytes move only in the AEAD kernels
+ * (receive: in place, nothing copied) and, on send, in one coalesced copy of
+ * the plaintext into its record slot.
+ */
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include <string.h>
+
+#include "tlsrec.h"
+#include "tlsrec_internal.h"
+
+using tlsrec::SlotState;
+
+/* engine.hip */
+extern "C" const SlotState *tlsrec__keytab_slots(const tlsrec_keytab *kt);
+
+namespace tlsst {
+
+constexpr uint32_t NO_SLOT = 0xFFFFFFFFu;
+constexpr int MAX_VERSION = 0x0304;          /* conf->max_tls_version (TLS 1.3 build) */
+
+__device__ __forceinline__ uint64_t be64(const uint8_t c[8])
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) v = (v << 8) | c[i];
+    return v;
+}
+
+__device__ __forceinline__ void put_be64(uint8_t c[8], uint64_t v)
+{
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+        c[i] = (uint8_t) v;
+        v >>= 8;
+    }
+}
+
+/* TLS minor version of a loaded slot (3 or 4), 0 if the slot is unusable */
+__device__ __forceinline__ uint32_t slot_minor(const SlotState *slots, uint32_t cap, uint32_t slot)
+{
+    if (slot >= cap) return 0;
+    const tlsrec_key_material &k = slots[slot].km;
+    return k.cipher ? k.tls_minor : 0;
+}
+
+/* ---------------- receive ---------------------------------------------- */
+struct HdrStop {
+    int32_t status;           /* header error that stopped the walk, 0 = out of bytes */
+    uint32_t pos;
+};
+
+/* Walk one connection's headers (ssl_parse_record_header + fetch_input);
+ * f(k, pos, type, ver, dlen) for each complete record. */
+template <typename F>
+__device__ HdrStop walk_in(const uint8_t *base, uint32_t len, F f)
+{
+    uint32_t pos = 0, k = 0;
+    HdrStop st = { 0, 0 };
+    while (len - pos >= 5) {
+        const uint8_t *h = base + pos;
+        const uint32_t type = h[0], ver = ((uint32_t) h[1] << 8) | h[2], dlen = ((uint32_t) h[3] << 8) | h[4];
+        if (type < 20 || type > 23) { st.status = TLSREC_ERR_SSL_INVALID_RECORD; break; }   /* :3529-3539 */
+        if (ver > (uint32_t) MAX_VERSION) { st.status = TLSREC_ERR_SSL_INVALID_RECORD; break; }
+        if (dlen == 0) { st.status = TLSREC_ERR_SSL_INVALID_RECORD; break; }                /* :3723-3726 */
+        if (5 + dlen > TLSREC_MAX_IN_RECORD) { st.status = TLSREC_ERR_SSL_BAD_INPUT_DATA; break; }
+        if (len - pos < 5 + dlen) break;                                                     /* wait */
+        f(k, pos, type, h[1], h[2], dlen);
+        k++;
+        pos += 5 + dlen;
+    }
+    st.pos = pos;
+    return st;
+}
+
+__global__ void in_count_kernel(const tlsrec_stream_in *s, uint32_t n, const uint8_t *arena, uint32_t *counts,
+                                HdrStop *stops)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {                       /* scan sentinel: offs[n] = total */
+        counts[n] = 0;
+        return;
+    }
+    uint32_t c = 0;
+    const HdrStop st = walk_in(arena + s[i].off, s[i].len,
+                               [&](uint32_t, uint32_t, uint32_t, uint8_t, uint8_t, uint32_t) { c++; });
+    counts[i] = c;
+    stops[i] = st;
+}
+
+__global__ void in_emit_kernel(const tlsrec_stream_in *s, uint32_t n, const uint8_t *arena, const uint32_t *offs,
+                               const SlotState *slots, uint32_t cap, tlsrec_batch_rec *recs)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tlsrec_stream_in si = s[i];
+    const bool tls13 = slot_minor(slots, cap, si.slot) == 4;
+    uint64_t seq = be64(si.in_ctr);
+    tlsrec_batch_rec *out = recs + offs[i];
+    walk_in(arena + si.off, si.len, [&](uint32_t k, uint32_t pos, uint32_t type, uint8_t v0, uint8_t v1, uint32_t dlen) {
+        tlsrec_batch_rec d;
+        memset(&d, 0, sizeof(d));
+        d.buf_off = si.off + pos;                 /* rec->buf = header (:3715-3716) */
+        d.buf_len = 5 + dlen;
+        d.data_offset = 5;
+        d.data_len = dlen;
+        const bool ccs = tls13 && type == 20;      /* TLS 1.3 CCS: not decrypted, no in_ctr step */
+        d.slot = ccs ? NO_SLOT : si.slot;
+        put_be64(d.ctr, seq);
+        d.type = (uint8_t) type;
+        d.ver[0] = v0;
+        d.ver[1] = v1;
+        if (!ccs) seq++;
+        out[k] = d;
+    });
+}
+
+__global__ void in_finish_kernel(const tlsrec_stream_in *s, uint32_t n, const uint32_t *offs, const uint32_t *counts,
+                                 const HdrStop *stops, const SlotState *slots, uint32_t cap,
+                                 const tlsrec_batch_rec *recs, tlsrec_batch_res *res, tlsrec_stream_in_res *sres)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tlsrec_stream_in si = s[i];
+    const uint32_t minor = slot_minor(slots, cap, si.slot);
+    uint64_t ctr = be64(si.in_ctr);
+    uint32_t nbz = si.nb_zero, nrec = 0, consumed = 0;
+    int32_t st = 0;
+    const uint32_t first = offs[i], cnt = counts[i];
+    uint32_t k = 0;
+    for (; k < cnt; k++) {
+        const tlsrec_batch_rec &d = recs[first + k];
+        tlsrec_batch_res r = res[first + k];
+        if (d.slot == NO_SLOT) {                  /* TLS 1.3 CCS passes as received */
+            r.status = 0;
+            r.data_offset = 5;
+            r.data_len = d.data_len;
+            r.type = d.type;
+            res[first + k] = r;
+        } else {
+            if (r.status) { st = r.status; break; }
+            if (r.data_len == 0) {                /* :3888-3906 */
+                if (minor == 3 && r.type != TLSREC_MSG_APPLICATION_DATA) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; }
+                if (++nbz > 3) { st = TLSREC_ERR_SSL_INVALID_MAC; break; }
+            } else {
+                nbz = 0;
+            }
+            if (++ctr == 0) { st = TLSREC_ERR_SSL_COUNTER_WRAPPING; break; }   /* :3954-3963 */
+        }
+        if (r.data_len > 16384) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; } /* IN_CONTENT_LEN, :4011-4014 */
+        nrec++;
+        consumed = (uint32_t) (d.buf_off - si.off) + d.buf_len;
+    }
+    if (st == 0 && k == cnt) st = stops[i].status;
+    tlsrec_stream_in_res o;
+    memset(&o, 0, sizeof(o));
+    o.status = st;
+    o.first = first;
+    o.nrec = nrec;
+    o.consumed = consumed;
+    put_be64(o.in_ctr, ctr);
+    o.nb_zero = (uint8_t) nbz;
+    o.nparsed = cnt;
+    sres[i] = o;
+}
+
+/* ---------------- send ------------------------------------------------- */
+struct OutShape {
+    uint32_t ok;              /* slot usable */
+    uint32_t head;            /* explicit-IV room before the content (8 for TLS 1.2 GCM) */
+    uint32_t tls13, gran;
+};
+
+__device__ __forceinline__ OutShape out_shape(const SlotState *slots, uint32_t cap, uint32_t slot)
+{
+    OutShape o = { 0, 0, 0, 16 };
+    if (slot >= cap) return o;
+    const tlsrec_key_material &k = slots[slot].km;
+    if (!k.cipher) return o;
+    o.ok = 1;
+    o.tls13 = k.tls_minor == 4;
+    o.head = (!o.tls13 && k.fixed_ivlen == 4) ? 8u : 0u;
+    o.gran = k.granularity ? k.granularity : 16;
+    return o;
+}
+
+/* protected length of an n-byte record (ssl_msg.c:853-868, :1066-1075) */
+__device__ __forceinline__ uint32_t out_body(const OutShape &o, uint32_t n)
+{
+    if (o.tls13) {
+        const uint32_t inner = n + 1;
+        return inner + (o.gran - inner % o.gran) % o.gran + 16;
+    }
+    return o.head + n + 16;
+}
+
+__device__ __forceinline__ uint32_t frag_of(const tlsrec_stream_out &s) { return s.max_frag ? s.max_frag : 16384u; }
+
+__global__ void out_count_kernel(const tlsrec_stream_out *s, uint32_t n, const SlotState *slots, uint32_t cap,
+                                 uint32_t *counts)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        counts[n] = 0;
+        return;
+    }
+    const uint32_t f = frag_of(s[i]);
+    counts[i] = out_shape(slots, cap, s[i].slot).ok ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
+}
+
+/* One workgroup per record: header, descriptor, and the plaintext copied
+ * into the record's slot of the output stream (16-B vector moves when both
+ * ends allow, bytes otherwise). */
+__global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs,
+                                                        const SlotState *slots, uint32_t cap, const uint8_t *in,
+                                                        uint8_t *out, tlsrec_batch_rec *recs)
+{
+    const uint32_t j = blockIdx.x;
+    /* connection of record j: the last i with offs[i] <= j */
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (offs[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t i = lo;
+    const tlsrec_stream_out si = s[i];
+    const uint32_t k = j - offs[i];
+    const uint32_t f = frag_of(si);
+    const OutShape sh = out_shape(slots, cap, si.slot);
+    const uint64_t src_off = (uint64_t) k * f;
+    const uint64_t left = (uint64_t) si.in_len - src_off;
+    const uint32_t len = left < f ? (uint32_t) left : f;
+    const uint64_t pos = si.out_off + (uint64_t) k * (5 + out_body(sh, f));
+    const uint8_t *src = in + si.in_off + src_off;
+    uint8_t *dst = out + pos + 5 + sh.head;
+    if (((uintptr_t) src & 15) == 0 && ((uintptr_t) dst & 15) == 0) {
+        const uint32_t nv = len / 16;
+        for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
+            reinterpret_cast<uint4 *>(dst)[v] = reinterpret_cast<const uint4 *>(src)[v];
+        for (uint32_t b = nv * 16 + threadIdx.x; b < len; b += blockDim.x) dst[b] = src[b];
+    } else {
+        for (uint32_t b = threadIdx.x; b < len; b += blockDim.x) dst[b] = src[b];
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t body = out_body(sh, len);
+        uint8_t *h = out + pos;
+        h[0] = sh.tls13 ? (uint8_t) TLSREC_MSG_APPLICATION_DATA : si.type;   /* final out_msgtype */
+        h[1] = 3;                                  /* mbedtls_ssl_write_version(TLS 1.2 for 1.3), :2669-2674 */
+        h[2] = 3;
+        h[3] = (uint8_t) (body >> 8);
+        h[4] = (uint8_t) body;
+        tlsrec_batch_rec d;
+        memset(&d, 0, sizeof(d));
+        d.buf_off = pos + 5;                       /* rec.buf = out_iv */
+        d.buf_len = TLSREC_OUT_BUF_SPACE;
+        d.data_offset = sh.head;                   /* out_msg - out_iv */
+        d.data_len = len;
+        d.slot = si.slot;
+        put_be64(d.ctr, be64(si.out_ctr) + k);
+        d.type = si.type;
+        d.ver[0] = 3;
+        d.ver[1] = 3;
+        recs[j] = d;
+    }
+}
+
+__global__ void out_finish_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs, const uint32_t *counts,
+                                  const SlotState *slots, uint32_t cap, const tlsrec_batch_res *res,
+                                  tlsrec_stream_out_res *sres)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tlsrec_stream_out si = s[i];
+    uint64_t ctr = be64(si.out_ctr);
+    int32_t st = out_shape(slots, cap, si.slot).ok || si.in_len == 0 ? 0 : TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    uint32_t nrec = 0, olen = 0;
+    const uint32_t first = offs[i], cnt = counts[i];
+    for (uint32_t k = 0; k < cnt && st == 0; k++) {
+        const tlsrec_batch_res &r = res[first + k];
+        if (r.status) { st = r.status; break; }
+        if (r.data_offset != 0) { st = TLSREC_ERR_SSL_INTERNAL_ERROR; break; }   /* :2704-2707 */
+        olen += 5 + r.data_len;
+        nrec++;
+        if (++ctr == 0) st = TLSREC_ERR_SSL_COUNTER_WRAPPING;                      /* :2749-2756 */
+    }
+    tlsrec_stream_out_res o;
+    memset(&o, 0, sizeof(o));
+    o.status = st;
+    o.first = first;
+    o.nrec = nrec;
+    o.out_len = olen;
+    put_be64(o.out_ctr, ctr);
+    o.nparsed = cnt;
+    sres[i] = o;
+}
+
+} /* namespace tlsst */
+
+using namespace tlsst;
+
+/* ======================================================================
+ * host side
+ * ==================================================================== */
+namespace {
+struct Scratch {
+    void *mem = nullptr;
+    uint32_t *counts = nullptr, *offs = nullptr;
+    HdrStop *stops = nullptr;
+    void *scan_tmp = nullptr;
+    size_t scan_bytes = 0;
+};
+}
+
+static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
+{
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, sc.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
+                                         (int) n + 1, st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    const size_t a = 256, sz4 = (((size_t) n + 1) * 4 + a - 1) / a * a, szs = ((size_t) n * sizeof(HdrStop) + a) / a * a;
+    if (hipMallocAsync(&sc.mem, 2 * sz4 + szs + sc.scan_bytes + a, st) != hipSuccess) return TLSREC_ERR_SSL_ALLOC_FAILED;
+    uint8_t *m = (uint8_t *) sc.mem;
+    sc.counts = (uint32_t *) m;
+    sc.offs = (uint32_t *) (m + sz4);
+    sc.stops = (HdrStop *) (m + 2 * sz4);
+    sc.scan_tmp = m + 2 * sz4 + szs;
+    return 0;
+}
+
+/* exclusive scan of counts[0..n] -> offs; returns offs[n] (the total) on the host */
+static int scan_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total)
+{
+    if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, sc.scan_bytes, sc.counts, sc.offs, (int) n + 1, st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    return 0;
+}
+
+static inline uint32_t blocks(uint32_t n, uint32_t t) { return (n + t - 1) / t; }
+
+extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_stream_in *streams, uint32_t nstreams,
+                                     uint8_t *arena, tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                     uint32_t max_records, tlsrec_stream_in_res *sres, uint32_t *nrecords,
+                                     void *stream)
+{
+    if (nrecords) *nrecords = 0;
+    if (!kt || (nstreams && (!streams || !arena || !sres))) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (nstreams == 0) return 0;
+    hipStream_t st = (hipStream_t) stream;
+    const SlotState *slots = tlsrec__keytab_slots(kt);
+    const uint32_t cap = tlsrec_keytab_capacity(kt);
+    Scratch sc;
+    int r = scratch_alloc(sc, nstreams, st);
+    uint32_t total = 0;
+    if (r == 0) {
+        hipLaunchKernelGGL(in_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
+                           (const uint8_t *) arena, sc.counts, sc.stops);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
+    if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (r == 0 && total) {
+        hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
+                           (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) r = tlsrec_batch_decrypt(kt, recs, res, total, arena, arena, 0, stream);
+    }
+    if (r == 0) {
+        hipLaunchKernelGGL(in_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams, sc.offs,
+                           sc.counts, sc.stops, slots, cap, recs, res, sres);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (sc.mem && hipFreeAsync(sc.mem, st) != hipSuccess && r == 0) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (r == 0 && nrecords) *nrecords = total;
+    return r;
+}
+
+extern "C" uint64_t tlsrec_stream_out_size(int tls_version, int cipher, uint32_t granularity, uint64_t in_len,
+                                           uint32_t max_frag)
+{
+    if (cipher < TLSREC_CIPHER_AES_128_GCM || cipher > TLSREC_CIPHER_CHACHA20_POLY1305) return 0;
+    if (tls_version != TLSREC_VERSION_TLS1_2 && tls_version != TLSREC_VERSION_TLS1_3) return 0;
+    const uint64_t f = max_frag ? max_frag : 16384;
+    const uint64_t g = granularity ? granularity : 16;
+    const uint64_t head = (tls_version == TLSREC_VERSION_TLS1_2 && cipher != TLSREC_CIPHER_CHACHA20_POLY1305) ? 8 : 0;
+    auto body = [&](uint64_t n) -> uint64_t {
+        if (tls_version == TLSREC_VERSION_TLS1_3) {
+            const uint64_t inner = n + 1;
+            return inner + (g - inner % g) % g + 16;
+        }
+        return head + n + 16;
+    };
+    const uint64_t full = in_len / f, rest = in_len % f;
+    return full * (5 + body(f)) + (rest ? 5 + body(rest) : 0);
+}
+
+extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_out *streams, uint32_t nstreams,
+                                     const uint8_t *in_arena, uint8_t *out_arena, tlsrec_batch_rec *recs,
+                                     tlsrec_batch_res *res, uint32_t max_records, tlsrec_stream_out_res *sres,
+                                     uint32_t *nrecords, void *stream)
+{
+    if (nrecords) *nrecords = 0;
+    if (!kt || (nstreams && (!streams || !in_arena || !out_arena || !sres))) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (nstreams == 0) return 0;
+    hipStream_t st = (hipStream_t) stream;
+    const SlotState *slots = tlsrec__keytab_slots(kt);
+    const uint32_t cap = tlsrec_keytab_capacity(kt);
+    Scratch sc;
+    int r = scratch_alloc(sc, nstreams, st);
+    uint32_t total = 0;
+    if (r == 0) {
+        hipLaunchKernelGGL(out_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
+                           slots, cap, sc.counts);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
+    if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (r == 0 && total) {
+        hipLaunchKernelGGL(out_frame_kernel, dim3(total), dim3(256), 0, st, streams, nstreams, sc.offs, slots, cap,
+                           in_arena, out_arena, recs);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) r = tlsrec_batch_encrypt(kt, recs, res, total, out_arena, out_arena, 0, stream);
+    }
+    if (r == 0) {
+        hipLaunchKernelGGL(out_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
+                           sc.offs, sc.counts, slots, cap, res, sres);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (sc.mem && hipFreeAsync(sc.mem, st) != hipSuccess && r == 0) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (r == 0 && nrecords) *nrecords = total;
+    return r;
+}

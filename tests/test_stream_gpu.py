@@ -1,0 +1,208 @@
+"""GPU parity of the TLS stream record layer (stream.hip through the C ABI)
+against the oracle's restatement of the ssl_get_next_record /
+mbedtls_ssl_write_record loops: byte-exact record streams, per-connection
+status / consumed / sequence numbers, and every stop condition."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import mbedtls_amd as M  # noqa: E402
+from mbedtls_amd import stream as S  # noqa: E402
+import oracle as O  # noqa: E402
+from tests import batchlib as B  # noqa: E402
+from tests.prng import prng_bytes  # noqa: E402
+
+KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
+X = bytes.fromhex
+OC = {M.CIPHER_AES_128_GCM: O.AES_128_GCM, M.CIPHER_AES_256_GCM: O.AES_256_GCM,
+      M.CIPHER_CHACHA20_POLY1305: O.CHACHA20_POLY1305}
+
+
+def _al(x, a=128):
+    return (x + a - 1) // a * a
+
+
+class Conns:
+    """slots: list of (cipher, version, key, iv, granularity); one key table."""
+
+    def __init__(self, slots):
+        self.slots = slots
+        self.kt = M.KeyTable(len(slots))
+        self.kt.load(np.concatenate([M.key_material(c, v, k, iv, g) for c, v, k, iv, g in slots]))
+        self.ot = [O.Transform(v, OC[c], k, k, iv, iv, granularity=g or 16) for c, v, k, iv, g in slots]
+
+    def encrypt(self, jobs):
+        """jobs: list of (slot, plaintext, out_ctr(int), max_frag, type)"""
+        ins, outs, pos_in, pos_out = [], [], 0, 0
+        d = np.zeros(len(jobs), dtype=S.STREAM_OUT)
+        for i, (slot, pt, ctr, frag, typ) in enumerate(jobs):
+            c, v, _, _, g = self.slots[slot]
+            size = S.out_size(v, c, g, len(pt), frag)
+            d[i]["in_off"], d[i]["in_len"], d[i]["slot"] = pos_in, len(pt), slot
+            d[i]["out_off"], d[i]["max_frag"], d[i]["type"] = pos_out, frag, typ
+            d[i]["out_ctr"] = np.frombuffer(ctr.to_bytes(8, "big"), dtype=np.uint8)
+            ins.append(pos_in)
+            outs.append((pos_out, size))
+            pos_in += _al(len(pt) + 1)
+            pos_out += _al(size + 1)
+        ina = np.zeros(max(pos_in, 16), dtype=np.uint8)
+        for (slot, pt, *_), o in zip(jobs, ins):
+            ina[o:o + len(pt)] = np.frombuffer(pt, dtype=np.uint8)
+        dev = torch.device("cuda")
+        tin = torch.from_numpy(ina).to(dev)
+        tout = torch.zeros(max(pos_out, 16), dtype=torch.uint8, device=dev)
+        nmax = sum((len(j[1]) + (j[3] or 16384) - 1) // (j[3] or 16384) for j in jobs) + 1
+        recs = torch.zeros(nmax * 40, dtype=torch.uint8, device=dev)
+        res = torch.zeros(nmax * 16, dtype=torch.uint8, device=dev)
+        sres = torch.zeros(len(jobs) * 32, dtype=torch.uint8, device=dev)
+        S.encrypt(self.kt, d, len(jobs), tin, tout, recs, res, nmax, sres)
+        torch.cuda.synchronize()
+        o = tout.cpu().numpy()
+        sr = sres.cpu().numpy().view(S.STREAM_OUT_RES)
+        return [(sr[i], o[p:p + int(sr[i]["out_len"])].tobytes()) for i, (p, _) in enumerate(outs)]
+
+    def decrypt(self, conns):
+        """conns: list of (slot, bytes, in_ctr(int), nb_zero)"""
+        d = np.zeros(len(conns), dtype=S.STREAM_IN)
+        pos, offs = 0, []
+        for i, (slot, data, ctr, nbz) in enumerate(conns):
+            d[i]["off"], d[i]["len"], d[i]["slot"], d[i]["nb_zero"] = pos, len(data), slot, nbz
+            d[i]["in_ctr"] = np.frombuffer(ctr.to_bytes(8, "big"), dtype=np.uint8)
+            offs.append(pos)
+            pos += _al(len(data) + 1)
+        a = np.zeros(max(pos, 16), dtype=np.uint8)
+        for (slot, data, *_), o in zip(conns, offs):
+            a[o:o + len(data)] = np.frombuffer(data, dtype=np.uint8)
+        dev = torch.device("cuda")
+        ta = torch.from_numpy(a).to(dev)
+        nmax = sum(len(c[1]) // 6 + 1 for c in conns)
+        recs = torch.zeros(nmax * 40, dtype=torch.uint8, device=dev)
+        res = torch.zeros(nmax * 16, dtype=torch.uint8, device=dev)
+        sres = torch.zeros(len(conns) * 32, dtype=torch.uint8, device=dev)
+        S.decrypt(self.kt, d, len(conns), ta, recs, res, nmax, sres)
+        torch.cuda.synchronize()
+        return (ta.cpu().numpy(), recs.cpu().numpy().view(M.BATCH_REC), res.cpu().numpy().view(M.BATCH_RES),
+                sres.cpu().numpy().view(S.STREAM_IN_RES), offs)
+
+    def close(self):
+        self.kt.close()
+
+
+@pytest.mark.parametrize("kat", KATS, ids=lambda k: k["name"])
+def test_reference_complete_records(kat):
+    sk, si, ck, ci = (X(kat[x]) for x in ("server_key", "server_iv", "client_key", "client_iv"))
+    wk, wi, rk, ri = (ck, ci, sk, si) if kat["endpoint"] == "client" else (sk, si, ck, ci)
+    c = Conns([(M.CIPHER_AES_128_GCM, M.VERSION_TLS1_3, wk, wi, 1), (M.CIPHER_AES_128_GCM, M.VERSION_TLS1_3, rk, ri, 1)])
+    ct = X(kat["ciphertext"])
+    wire = bytes([23, 3, 3]) + len(ct).to_bytes(2, "big") + ct
+    [(r, out)] = c.encrypt([(0, X(kat["plaintext"]), kat["ctr"], 0, 23)])
+    assert r["status"] == 0 and r["nrec"] == 1 and out == wire
+    # the receiver side of the same connection decrypts with the peer's keys
+    c2 = Conns([(M.CIPHER_AES_128_GCM, M.VERSION_TLS1_3, wk, wi, 1)])
+    a, recs, res, sres, offs = c2.decrypt([(0, wire, kat["ctr"], 0)])
+    assert sres[0]["status"] == 0 and sres[0]["nrec"] == 1 and sres[0]["consumed"] == len(wire)
+    o = int(recs[0]["buf_off"]) + int(res[0]["data_offset"])
+    assert a[o:o + int(res[0]["data_len"])].tobytes() == X(kat["plaintext"]) and res[0]["type"] == 23
+    c.close()
+    c2.close()
+
+
+def _slots(seed):
+    return B.random_slots(seed, list(B.CIPHERS.values()), list(B.VERSIONS.values()), 6)
+
+
+def test_encrypt_then_decrypt_many_connections():
+    slots = _slots(41)
+    c = Conns(slots)
+    rng = np.random.default_rng(7)
+    jobs = []
+    for i in range(48):
+        n = int(rng.choice([0, 1, 15, 300, 16383, 16384, 16385, 40000]))
+        frag = int(rng.choice([0, 0, 1000, 4096]))
+        jobs.append((i % 6, prng_bytes(1000 + i, n), int(rng.integers(0, 1 << 40)), frag, 23 if i % 7 else 22))
+    got = c.encrypt(jobs)
+    for (slot, pt, ctr, frag, typ), (r, out) in zip(jobs, got):
+        st, want, nrec, ctr2 = O.stream_encrypt(c.ot[slot], pt, typ, ctr.to_bytes(8, "big"), frag or 16384)
+        assert (int(r["status"]), int(r["nrec"]), out, bytes(r["out_ctr"])) == (st, nrec, want, ctr2)
+    # receive the same streams, some with a partial trailing record
+    conns = []
+    for i, ((slot, pt, ctr, frag, typ), (r, out)) in enumerate(zip(jobs, got)):
+        extra = out[:7] if (i % 3 == 0 and len(out) > 7) else b""
+        conns.append((slot, out + extra, ctr, i % 2))
+    a, recs, res, sres, offs = c.decrypt(conns)
+    for i, (slot, data, ctr, nbz) in enumerate(conns):
+        want, wrecs, wbuf = O.stream_decrypt(c.ot[slot], data, ctr.to_bytes(8, "big"), nbz)
+        g = sres[i]
+        assert (int(g["status"]), int(g["nrec"]), int(g["consumed"]), bytes(g["in_ctr"]), int(g["nb_zero"])) == \
+            (want["status"], want["nrec"], want["consumed"], want["in_ctr"], want["nb_zero"]), i
+        f = int(g["first"])
+        for k, (off, doff, dlen, typ) in enumerate(wrecs):
+            rr = res[f + k]
+            assert (int(rr["data_offset"]), int(rr["data_len"]), int(rr["type"])) == (doff, dlen, typ)
+            assert int(recs[f + k]["buf_off"]) == offs[i] + off
+            s0 = offs[i] + off + doff
+            assert a[s0:s0 + dlen].tobytes() == wbuf[off + doff:off + doff + dlen]
+    c.close()
+
+
+def _empty_record(t, ctr):
+    buf = bytearray(64)
+    head = 8 if (t.tls_version == O.TLS1_2 and t.cipher != O.CHACHA20_POLY1305) else 0
+    rec = O.Record(ctr=ctr.to_bytes(8, "big"), type=23, ver=b"\x03\x03", buf=buf, data_offset=head, data_len=0)
+    assert t.encrypt_buf(rec) == 0 and rec.data_offset == 0
+    return bytes([23, 3, 3]) + rec.data_len.to_bytes(2, "big") + rec.data()
+
+
+def test_stop_conditions_match_oracle():
+    slots = [(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, prng_bytes(1, 32), prng_bytes(2, 12), 0),
+             (M.CIPHER_AES_128_GCM, M.VERSION_TLS1_2, prng_bytes(3, 16), prng_bytes(4, 12), 0),
+             (M.CIPHER_CHACHA20_POLY1305, M.VERSION_TLS1_3, prng_bytes(5, 32), prng_bytes(6, 12), 0)]
+    c = Conns(slots)
+    conns = []
+    for slot in range(3):
+        t = c.ot[slot]
+        _, w, n, _ = O.stream_encrypt(t, prng_bytes(10 + slot, 300), 23, bytes(8), 100)
+        one = len(w) // 3
+        conns += [(slot, w[:one] + bytes([24]) + w[one + 1:], 0, 0),                       # type
+                  (slot, w[:one] + w[one:one + 1] + b"\x03\x05" + w[one + 3:], 0, 0),     # version
+                  (slot, w[:one] + w[one:one + 3] + b"\x00\x00" + w[one + 5:], 0, 0),     # zero length
+                  (slot, w[:one] + w[one:one + 3] + b"\x40\x21" + w[one + 5:], 0, 0),     # too long
+                  (slot, w[:one + 20] + bytes([w[one + 20] ^ 0x80]) + w[one + 21:], 0, 0),  # MAC
+                  (slot, w[:4], 0, 0), (slot, b"", 0, 0),                                  # incomplete
+                  (slot, bytes([20, 3, 3, 0, 1, 1]) + w, 0, 0),                           # CCS first
+                  (slot, b"".join(_empty_record(t, k) for k in range(4)), 0, 0),          # 4 empty
+                  (slot, b"".join(_empty_record(t, k) for k in range(2)), 0, 2),          # nb_zero carried
+                  (slot, _empty_record(t, (1 << 64) - 1), (1 << 64) - 1, 0)]              # ctr wrap
+    a, recs, res, sres, offs = c.decrypt(conns)
+    for i, (slot, data, ctr, nbz) in enumerate(conns):
+        want, wrecs, _ = O.stream_decrypt(c.ot[slot], data, ctr.to_bytes(8, "big"), nbz)
+        g = sres[i]
+        assert (int(g["status"]), int(g["nrec"]), int(g["consumed"]), bytes(g["in_ctr"]), int(g["nb_zero"])) == \
+            (want["status"], want["nrec"], want["consumed"], want["in_ctr"], want["nb_zero"]), (i, want)
+    c.close()
+
+
+def test_too_many_records_is_buffer_too_small():
+    slots = [(M.CIPHER_AES_128_GCM, M.VERSION_TLS1_3, bytes(16), bytes(12), 0)]
+    c = Conns(slots)
+    _, w, n, _ = O.stream_encrypt(c.ot[0], bytes(500), 23, bytes(8), 100)
+    dev = torch.device("cuda")
+    d = np.zeros(1, dtype=S.STREAM_IN)
+    d[0]["len"] = len(w)
+    ta = torch.from_numpy(np.frombuffer(w, dtype=np.uint8).copy()).to(dev)
+    recs = torch.zeros(4 * 40, dtype=torch.uint8, device=dev)
+    res = torch.zeros(4 * 16, dtype=torch.uint8, device=dev)
+    sres = torch.zeros(32, dtype=torch.uint8, device=dev)
+    with pytest.raises(S.StreamError) as e:
+        S.decrypt(c.kt, d, 1, ta, recs, res, 4, sres)
+    assert e.value.code == M.ERR_SSL_BUFFER_TOO_SMALL
+    assert ta.cpu().numpy().tobytes() == w          # nothing decrypted
+    c.close()
