@@ -252,10 +252,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     int rc = 0;
     for (int cipher = TLSREC_CIPHER_AES_128_GCM; cipher <= TLSREC_CIPHER_AES_256_GCM && !rc; cipher++) {
         if (!(kt->cipher_mask & (1u << cipher))) continue;
-        /* lanes per record: 8; 16 when keys average fewer than 256 records of
-         * this batch (a key pass then still fills 16 waves x 4 records) */
+        /* lanes per record: a key pass should still fill the 16 waves of a
+         * workgroup.  8 for a single key or >= 128 records per key; 16
+         * (4 records per wave) down to 48 records per key; 64 (one record per
+         * wave) below that -- the many-connections, few-records regime of
+         * the stream path. */
+        const uint32_t rpk = kt->nloaded > 1 ? n / kt->nloaded : n;
         int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
-                : (kt->nloaded > 1 && n / kt->nloaded < 256 ? 16 : 8);
+                : (kt->nloaded <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;

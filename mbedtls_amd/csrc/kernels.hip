@@ -476,6 +476,11 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint32_t slot_in_chunk = rr + (uint32_t) g;
             const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
             const bool active = slot_in_chunk < a.rpw && owner_slot == s;
+            /* a key's records sit in a contiguous run of each wave's chunk
+             * positions: rounds holding none of them are skipped (wave-uniform,
+             * no barrier inside the round) -- with many keys of few records
+             * each, the pass would otherwise walk all rpw positions */
+            if (__ballot(active) == 0) continue;
             const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
             /* Only what the AEAD loop needs stays live across it; the plan is
              * re-derived from the (cached) descriptor afterwards. */
