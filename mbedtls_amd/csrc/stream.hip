@@ -20,8 +20,8 @@
  *
  * Header walking is one lane per connection (each header names the next);
  * connections walk in parallel.  Bulk bytes move only in the AEAD kernels
- * (receive: in place, nothing copied) and, on send, in one coalesced copy of
- * the plaintext into its record slot.
+ * (receive: in place, nothing copied) and, on send, in one copy of the
+ * plaintext into its record slot (one wave per record).
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -232,14 +232,15 @@ __global__ void out_count_kernel(const tlsrec_stream_out *s, uint32_t n, const S
     counts[i] = out_shape(slots, cap, s[i].slot).ok ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
 }
 
-/* One workgroup per record: header, descriptor, and the plaintext copied
- * into the record's slot of the output stream (16-B vector moves when both
- * ends allow, bytes otherwise). */
+/* One wave per record (4 per workgroup): header, descriptor, and the
+ * plaintext copied into the record's slot of the output stream with 16-byte
+ * accesses at any byte alignment (unaligned-access mode, see kernels.hip). */
 __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs,
-                                                        const SlotState *slots, uint32_t cap, const uint8_t *in,
-                                                        uint8_t *out, tlsrec_batch_rec *recs)
+                                                        uint32_t total, const SlotState *slots, uint32_t cap,
+                                                        const uint8_t *in, uint8_t *out, tlsrec_batch_rec *recs)
 {
-    const uint32_t j = blockIdx.x;
+    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= total) return;
     /* connection of record j: the last i with offs[i] <= j */
     uint32_t lo = 0, hi = n;
     while (hi - lo > 1) {
@@ -258,15 +259,14 @@ __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out 
     const uint64_t pos = si.out_off + (uint64_t) k * (5 + out_body(sh, f));
     const uint8_t *src = in + si.in_off + src_off;
     uint8_t *dst = out + pos + 5 + sh.head;
-    if (((uintptr_t) src & 15) == 0 && ((uintptr_t) dst & 15) == 0) {
-        const uint32_t nv = len / 16;
-        for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
-            reinterpret_cast<uint4 *>(dst)[v] = reinterpret_cast<const uint4 *>(src)[v];
-        for (uint32_t b = nv * 16 + threadIdx.x; b < len; b += blockDim.x) dst[b] = src[b];
-    } else {
-        for (uint32_t b = threadIdx.x; b < len; b += blockDim.x) dst[b] = src[b];
+    const uint32_t nv = len / 16;
+    for (uint32_t v = lane; v < nv; v += 64) {
+        uint4 w;
+        __builtin_memcpy(&w, src + 16 * v, 16);
+        __builtin_memcpy(dst + 16 * v, &w, 16);
     }
-    if (threadIdx.x == 0) {
+    for (uint32_t b = nv * 16 + lane; b < len; b += 64) dst[b] = src[b];
+    if (lane == 0) {
         const uint32_t body = out_body(sh, len);
         uint8_t *h = out + pos;
         h[0] = sh.tls13 ? (uint8_t) TLSREC_MSG_APPLICATION_DATA : si.type;   /* final out_msgtype */
@@ -442,8 +442,8 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        hipLaunchKernelGGL(out_frame_kernel, dim3(total), dim3(256), 0, st, streams, nstreams, sc.offs, slots, cap,
-                           in_arena, out_arena, recs);
+        hipLaunchKernelGGL(out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
+                           total, slots, cap, in_arena, out_arena, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) r = tlsrec_batch_encrypt(kt, recs, res, total, out_arena, out_arena, 0, stream);
     }

@@ -27,6 +27,12 @@ TLS1_3 = 0x0304
 AES_128_GCM = 1
 AES_256_GCM = 2
 CHACHA20_POLY1305 = 3
+AES_192_GCM = 4
+AES_128_CCM, AES_192_CCM, AES_256_CCM = 5, 6, 7
+AES_128_CCM_8, AES_192_CCM_8, AES_256_CCM_8 = 8, 9, 10
+KEYLEN = {AES_128_GCM: 16, AES_256_GCM: 32, CHACHA20_POLY1305: 32, AES_192_GCM: 24, AES_128_CCM: 16,
+          AES_192_CCM: 24, AES_256_CCM: 32, AES_128_CCM_8: 16, AES_192_CCM_8: 24, AES_256_CCM_8: 32}
+TAGLEN = {c: (8 if c >= AES_128_CCM_8 else 16) for c in KEYLEN}
 
 _lib = None
 
@@ -132,6 +138,17 @@ def poly1305(key: bytes, msg: bytes) -> bytes:
     out = _buf(16)
     lib().orc_poly1305(key, msg, len(msg), out)
     return out.raw
+
+
+def ccm_encrypt(key: bytes, nonce: bytes, aad: bytes, pt: bytes, tag_len: int = 16):
+    ctx = _buf(_GCM_CTX)
+    assert lib().orc_aes_setkey_enc(ctx, key, len(key) * 8) == 0
+    f = lib().orc_ccm_encrypt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                  ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    out, tag = _buf(max(1, len(pt))), _buf(16)
+    f(ctx, nonce, aad, len(aad), pt, len(pt), out, tag, tag_len)
+    return out.raw[:len(pt)], tag.raw[:tag_len]
 
 
 def chachapoly_encrypt(key: bytes, nonce: bytes, aad: bytes, pt: bytes):

@@ -312,6 +312,96 @@ int orc_gcm_decrypt(const orc_gcm_ctx *ctx, const uint8_t iv[12],
 }
 
 /* ======================================================================
+ * CCM (NIST SP 800-38C, RFC 3610 formatting) with a 12-byte nonce:
+ *   B0 = flags(Adata, t, q=3) || N || Q(3)      (A.2.1)
+ *   AAD block(s) = len16(a) || a || 0-pad       (A.2.2, a < 2^16 - 2^8)
+ *   payload blocks zero-padded                  (A.2.3)
+ *   T = MSB_t(CBC-MAC), C = P ^ S_1.., U = T ^ MSB_t(S_0), S_i = E(ctr_i),
+ *   ctr_i = (q-1) || N || i(3)                  (A.3)
+ * ==================================================================== */
+static void ccm_mac(const orc_aes_ctx *aes, const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                    const uint8_t *pt, size_t len, size_t tag_len, uint8_t x[16])
+{
+    uint8_t b[16];
+    b[0] = (uint8_t) ((aad_len ? 0x40 : 0) | (((tag_len - 2) / 2) << 3) | 2);
+    memcpy(b + 1, nonce, 12);
+    b[13] = (uint8_t) (len >> 16);
+    b[14] = (uint8_t) (len >> 8);
+    b[15] = (uint8_t) len;
+    orc_aes_encrypt_block(aes, b, x);
+    if (aad_len) {
+        /* len16 || aad, then zero padding, in 16-byte blocks */
+        uint8_t buf[16];
+        size_t fill = 2, i = 0;
+        memset(buf, 0, 16);
+        buf[0] = (uint8_t) (aad_len >> 8);
+        buf[1] = (uint8_t) aad_len;
+        while (i < aad_len) {
+            buf[fill++] = aad[i++];
+            if (fill == 16) {
+                for (int k = 0; k < 16; k++) x[k] ^= buf[k];
+                orc_aes_encrypt_block(aes, x, x);
+                memset(buf, 0, 16);
+                fill = 0;
+            }
+        }
+        if (fill) {
+            for (int k = 0; k < 16; k++) x[k] ^= buf[k];
+            orc_aes_encrypt_block(aes, x, x);
+        }
+    }
+    for (size_t off = 0; off < len; off += 16) {
+        size_t n = len - off < 16 ? len - off : 16;
+        for (size_t k = 0; k < n; k++) x[k] ^= pt[off + k];
+        orc_aes_encrypt_block(aes, x, x);
+    }
+}
+
+static void ccm_ctr(const orc_aes_ctx *aes, const uint8_t nonce[12], uint32_t i, uint8_t s[16])
+{
+    uint8_t a[16];
+    a[0] = 2;
+    memcpy(a + 1, nonce, 12);
+    a[13] = (uint8_t) (i >> 16);
+    a[14] = (uint8_t) (i >> 8);
+    a[15] = (uint8_t) i;
+    orc_aes_encrypt_block(aes, a, s);
+}
+
+static void ccm_crypt(const orc_aes_ctx *aes, const uint8_t nonce[12], const uint8_t *in, size_t len, uint8_t *out)
+{
+    uint8_t s[16];
+    uint32_t i = 1;
+    for (size_t off = 0; off < len; off += 16, i++) {
+        ccm_ctr(aes, nonce, i, s);
+        size_t n = len - off < 16 ? len - off : 16;
+        for (size_t k = 0; k < n; k++) out[off + k] = in[off + k] ^ s[k];
+    }
+}
+
+void orc_ccm_encrypt(const orc_aes_ctx *aes, const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                     const uint8_t *in, size_t len, uint8_t *out, uint8_t *tag, size_t tag_len)
+{
+    uint8_t x[16], s0[16];
+    ccm_mac(aes, nonce, aad, aad_len, in, len, tag_len, x);
+    ccm_crypt(aes, nonce, in, len, out);
+    ccm_ctr(aes, nonce, 0, s0);
+    for (size_t k = 0; k < tag_len; k++) tag[k] = x[k] ^ s0[k];
+}
+
+int orc_ccm_decrypt(const orc_aes_ctx *aes, const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                    const uint8_t *in, size_t len, uint8_t *out, const uint8_t *tag, size_t tag_len)
+{
+    uint8_t x[16], s0[16];
+    ccm_crypt(aes, nonce, in, len, out);
+    ccm_mac(aes, nonce, aad, aad_len, out, len, tag_len, x);
+    ccm_ctr(aes, nonce, 0, s0);
+    uint8_t diff = 0;
+    for (size_t k = 0; k < tag_len; k++) diff |= (uint8_t) (tag[k] ^ x[k] ^ s0[k]);
+    return diff ? ORC_ERR_SSL_INVALID_MAC : 0;
+}
+
+/* ======================================================================
  * ChaCha20 (RFC 8439 2.3) and Poly1305 (RFC 8439 2.5) with 44-bit limbs.
  * ==================================================================== */
 #define QR(a, b, c, d) do { \
@@ -527,14 +617,18 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
     t->tls_version = tls_version;
     t->cipher = cipher;
     t->granularity = granularity ? granularity : 16;
-    switch (cipher) {
-        case ORC_CIPHER_AES_128_GCM: t->keylen = 16; break;
-        case ORC_CIPHER_AES_256_GCM:
+    switch (cipher) {                 /* mbedtls_ssl_cipher_to_psa, ssl_tls.c:2168-2363 */
+        case ORC_CIPHER_AES_128_GCM: case ORC_CIPHER_AES_128_CCM: case ORC_CIPHER_AES_128_CCM_8:
+            t->keylen = 16; break;
+        case ORC_CIPHER_AES_192_GCM: case ORC_CIPHER_AES_192_CCM: case ORC_CIPHER_AES_192_CCM_8:
+            t->keylen = 24; break;
+        case ORC_CIPHER_AES_256_GCM: case ORC_CIPHER_AES_256_CCM: case ORC_CIPHER_AES_256_CCM_8:
         case ORC_CIPHER_CHACHA20_POLY1305: t->keylen = 32; break;
         default: return ORC_ERR_SSL_FEATURE_UNAVAILABLE;
     }
     t->ivlen = 12;
-    t->taglen = 16;
+    /* MBEDTLS_CIPHERSUITE_SHORT_TAG: ssl_tls.c:7707-7708, ssl_tls13_keys.c:981-985 */
+    t->taglen = (cipher >= ORC_CIPHER_AES_128_CCM_8) ? 8 : 16;
     t->maclen = 0;
     if (tls_version == ORC_VERSION_TLS1_3) {
         t->fixed_ivlen = t->ivlen;
@@ -583,11 +677,15 @@ static size_t build_aad(uint8_t aad[13], const orc_record *rec, int tls_version,
     return n;
 }
 
+static int is_ccm(int c) { return c >= ORC_CIPHER_AES_128_CCM && c <= ORC_CIPHER_AES_256_CCM_8; }
+
 static void aead_seal(const orc_transform *t, const uint8_t nonce[12],
                       const uint8_t *aad, size_t aad_len, uint8_t *data, size_t len)
 {
     if (t->cipher == ORC_CIPHER_CHACHA20_POLY1305) {
         orc_chachapoly_encrypt(t->key_enc, nonce, aad, aad_len, data, len, data, data + len);
+    } else if (is_ccm(t->cipher)) {
+        orc_ccm_encrypt(&t->gcm_enc.aes, nonce, aad, aad_len, data, len, data, data + len, t->taglen);
     } else {
         orc_gcm_encrypt(&t->gcm_enc, nonce, aad, aad_len, data, len, data, data + len, 16);
     }
@@ -599,6 +697,8 @@ static int aead_open(const orc_transform *t, const uint8_t nonce[12],
     if (t->cipher == ORC_CIPHER_CHACHA20_POLY1305) {
         return orc_chachapoly_decrypt(t->key_dec, nonce, aad, aad_len, data, len, data, data + len);
     }
+    if (is_ccm(t->cipher))
+        return orc_ccm_decrypt(&t->gcm_dec.aes, nonce, aad, aad_len, data, len, data, data + len, t->taglen);
     return orc_gcm_decrypt(&t->gcm_dec, nonce, aad, aad_len, data, len, data, data + len, 16);
 }
 
@@ -634,7 +734,7 @@ int orc_encrypt_buf(const orc_transform *t, orc_record *rec)
     build_nonce(nonce, t->iv_enc, t->fixed_ivlen, rec->ctr);             /* :1012-1019 */
     size_t aad_len = build_aad(aad, rec, t->tls_version, t->taglen);    /* :1025-1027 */
     aead_seal(t, nonce, aad, aad_len, data, rec->data_len);             /* :1043-1049 */
-    rec->data_len += 16;
+    rec->data_len += t->taglen;
     if (t->ivlen != t->fixed_ivlen) {                                   /* :1066-1075 */
         if (rec->data_offset < 8) return ORC_ERR_SSL_BUFFER_TOO_SMALL;
         memcpy(data - 8, rec->ctr, 8);

@@ -60,6 +60,16 @@ extern "C" {
 #define ORC_CIPHER_AES_128_GCM        1
 #define ORC_CIPHER_AES_256_GCM        2
 #define ORC_CIPHER_CHACHA20_POLY1305  3
+/* the remaining AES AEADs of mbedtls_ssl_cipher_to_psa
+ * (ssl_tls.c:2168-2363); *_CCM_8 = the MBEDTLS_CIPHERSUITE_SHORT_TAG suites
+ * (taglen 8, ssl_tls.c:7707-7708, ssl_tls13_keys.c:981-985) */
+#define ORC_CIPHER_AES_192_GCM        4
+#define ORC_CIPHER_AES_128_CCM        5
+#define ORC_CIPHER_AES_192_CCM        6
+#define ORC_CIPHER_AES_256_CCM        7
+#define ORC_CIPHER_AES_128_CCM_8      8
+#define ORC_CIPHER_AES_192_CCM_8      9
+#define ORC_CIPHER_AES_256_CCM_8      10
 
 #define ORC_OUT_CONTENT_LEN 16384     /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
 
@@ -96,6 +106,12 @@ void orc_ghash(const orc_gcm_ctx *ctx, const uint8_t *aad, size_t aad_len,
                const uint8_t *ct, size_t ct_len, uint8_t out[16]);
 void orc_gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
 
+/* CCM (NIST SP 800-38C) with a 12-byte nonce (q = 3), tag_len 4..16 */
+void orc_ccm_encrypt(const orc_aes_ctx *aes, const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                     const uint8_t *in, size_t len, uint8_t *out, uint8_t *tag, size_t tag_len);
+int  orc_ccm_decrypt(const orc_aes_ctx *aes, const uint8_t nonce[12], const uint8_t *aad, size_t aad_len,
+                     const uint8_t *in, size_t len, uint8_t *out, const uint8_t *tag, size_t tag_len);
+
 void orc_chacha20_block(const uint8_t key[32], uint32_t counter,
                         const uint8_t nonce[12], uint8_t out[64]);
 void orc_chacha20_xor(const uint8_t key[32], uint32_t counter,
@@ -123,7 +139,7 @@ typedef struct {
     int cipher;
     size_t keylen;
     uint8_t key_enc[32], key_dec[32];
-    orc_gcm_ctx gcm_enc, gcm_dec;   /* expanded GCM state */
+    orc_gcm_ctx gcm_enc, gcm_dec;   /* expanded GCM state (its AES context serves CCM) */
     size_t granularity;             /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY */
 } orc_transform;
 

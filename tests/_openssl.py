@@ -29,7 +29,8 @@ def lib():
         L = _lib
         L.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
         L.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
-        for f in ("EVP_aes_128_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305"):
+        for f in ("EVP_aes_128_gcm", "EVP_aes_192_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305",
+                  "EVP_aes_128_ccm", "EVP_aes_192_ccm", "EVP_aes_256_ccm"):
             getattr(L, f).restype = ctypes.c_void_p
         L.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_char_p, ctypes.c_char_p]
@@ -52,7 +53,9 @@ EVP_CTRL_AEAD_SET_TAG = 0x11
 def _cipher(name: str, keylen: int):
     L = lib()
     if name == "gcm":
-        return L.EVP_aes_128_gcm() if keylen == 16 else L.EVP_aes_256_gcm()
+        return {16: L.EVP_aes_128_gcm, 24: L.EVP_aes_192_gcm, 32: L.EVP_aes_256_gcm}[keylen]()
+    if name == "ccm":
+        return {16: L.EVP_aes_128_ccm, 24: L.EVP_aes_192_ccm, 32: L.EVP_aes_256_ccm}[keylen]()
     return L.EVP_chacha20_poly1305()
 
 
@@ -104,5 +107,29 @@ def open_(name: str, key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes
         if ok != 1:
             return None
         return out.raw[:total]
+    finally:
+        L.EVP_CIPHER_CTX_free(ctx)
+
+
+def ccm_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes, tag_len: int):
+    """AES-CCM through EVP (length-first call sequence of the CCM mode)."""
+    L = lib()
+    ctx = L.EVP_CIPHER_CTX_new()
+    try:
+        assert L.EVP_EncryptInit_ex(ctx, _cipher("ccm", len(key)), None, None, None) == 1
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_IVLEN, len(nonce), None) == 1
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_TAG, tag_len, None) == 1
+        assert L.EVP_EncryptInit_ex(ctx, None, None, key, nonce) == 1
+        n = ctypes.c_int(0)
+        assert L.EVP_EncryptUpdate(ctx, None, ctypes.byref(n), None, len(pt)) == 1
+        if aad:
+            assert L.EVP_EncryptUpdate(ctx, None, ctypes.byref(n), aad, len(aad)) == 1
+        out = ctypes.create_string_buffer(len(pt) + 32)
+        assert L.EVP_EncryptUpdate(ctx, out, ctypes.byref(n), pt, len(pt)) == 1
+        total = n.value
+        assert L.EVP_EncryptFinal_ex(ctx, ctypes.byref(out, total), ctypes.byref(n)) == 1
+        tag = ctypes.create_string_buffer(16)
+        assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, tag_len, tag) == 1
+        return out.raw[:total], tag.raw[:tag_len]
     finally:
         L.EVP_CIPHER_CTX_free(ctx)

@@ -76,6 +76,13 @@ STANDARD = {
          "pt": "00000000000000000000000000000000", "ct": "cea7403d4d606b6e074ec5d3baf39d18",
          "tag": "d0d1c8a799996bf0265b98b5d48ab919"},
     ],
+    "ccm": [
+        # NIST SP 800-38C Appendix C, Example 3 (12-byte nonce, 8-byte tag)
+        {"key": "404142434445464748494a4b4c4d4e4f", "nonce": "101112131415161718191a1b",
+         "aad": "000102030405060708090a0b0c0d0e0f10111213",
+         "pt": "202122232425262728292a2b2c2d2e2f3031323334353637",
+         "ct": "e3b201a9f5b71a7a9b1ceaeccd97e70b6176aad9a4428aa5", "tag": "484392fbc1b09951"},
+    ],
     "chacha20_block": [
         # RFC 8439 2.3.2 (first 16 bytes of the serialized block)
         {"key": "000102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f",
@@ -99,14 +106,18 @@ STANDARD = {
 }
 
 CIPHERS = {"AES-128-GCM": O.AES_128_GCM, "AES-256-GCM": O.AES_256_GCM,
-           "CHACHA20-POLY1305": O.CHACHA20_POLY1305}
+           "CHACHA20-POLY1305": O.CHACHA20_POLY1305,
+           # SURVEY 8(f)-2 (appended: the seeds of the cases above stay unchanged)
+           "AES-192-GCM": O.AES_192_GCM, "AES-128-CCM": O.AES_128_CCM, "AES-192-CCM": O.AES_192_CCM,
+           "AES-256-CCM": O.AES_256_CCM, "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-CCM-8": O.AES_192_CCM_8,
+           "AES-256-CCM-8": O.AES_256_CCM_8}
 VERSIONS = {"TLS1.2": O.TLS1_2, "TLS1.3": O.TLS1_3}
 LENGTHS = [0, 1, 15, 16, 17, 1400, 16383]
 SEED = 0x7115EC0DE
 
 
 def _keylen(c):
-    return 16 if c == O.AES_128_GCM else 32
+    return O.KEYLEN[c]
 
 
 def make_records():
@@ -139,7 +150,7 @@ def make_records():
                         g = 16
                         pad = (g - (L + 1) % g) % g
                         inner = payload + bytes([rtype]) + bytes(pad)
-                        aad = bytes([23, 3, 3]) + (len(inner) + 16).to_bytes(2, "big")
+                        aad = bytes([23, 3, 3]) + (len(inner) + O.TAGLEN[c]).to_bytes(2, "big")
                         nonce = bytes(a ^ b for a, b in zip(iv_enc[:12], bytes(4) + ctr))
                         body = wire
                     else:
@@ -152,8 +163,12 @@ def make_records():
                             nonce = iv_enc[:4] + ctr
                             assert wire[:8] == ctr
                             body = wire[8:]
-                    name = "gcm" if c != O.CHACHA20_POLY1305 else "chacha"
-                    ct, tag = S.seal(name, key_enc, nonce, aad, inner)
+                    tl = O.TAGLEN[c]
+                    if O.AES_128_CCM <= c <= O.AES_256_CCM_8:
+                        ct, tag = S.ccm_seal(key_enc, nonce, aad, inner, tl)
+                    else:
+                        name = "gcm" if c != O.CHACHA20_POLY1305 else "chacha"
+                        ct, tag = S.seal(name, key_enc, nonce, aad, inner)
                     assert body == ct + tag, (cname, vname, L)
                     ent = {"cipher": cname, "version": vname, "len": L, "seed": seed,
                            "key_enc": key_enc.hex(), "key_dec": key_dec.hex(),
@@ -162,7 +177,7 @@ def make_records():
                            "out_offset": rec.data_offset, "out_len": rec.data_len,
                            "out_type": rec.type,
                            "wire_sha256": hashlib.sha256(wire).hexdigest(),
-                           "tag": wire[-16:].hex()}
+                           "tag": wire[-O.TAGLEN[c]:].hex()}
                     if L <= 64:
                         ent["payload"] = payload.hex()
                         ent["wire"] = wire.hex()

@@ -61,6 +61,9 @@ def test_standard_vectors():
         assert (ct.hex(), tag.hex()) == (v["ct"], v["tag"])
         r, pt = O.gcm_decrypt(h(v["key"]), h(v["iv"]), h(v["aad"]), ct, tag)
         assert r == 0 and pt.hex() == v["pt"]
+    for v in s["ccm"]:
+        ct, tag = O.ccm_encrypt(h(v["key"]), h(v["nonce"]), h(v["aad"]), h(v["pt"]), len(h(v["tag"])))
+        assert (ct.hex(), tag.hex()) == (v["ct"], v["tag"])
     for v in s["chacha20_block"]:
         assert O.chacha20_block(h(v["key"]), v["counter"], h(v["nonce"]))[:16].hex() == v["out16"]
     for v in s["poly1305"]:
@@ -71,7 +74,9 @@ def test_standard_vectors():
 
 
 CIPHERS = {"AES-128-GCM": O.AES_128_GCM, "AES-256-GCM": O.AES_256_GCM,
-           "CHACHA20-POLY1305": O.CHACHA20_POLY1305}
+           "CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-192-GCM": O.AES_192_GCM,
+           "AES-128-CCM": O.AES_128_CCM, "AES-192-CCM": O.AES_192_CCM, "AES-256-CCM": O.AES_256_CCM,
+           "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-CCM-8": O.AES_192_CCM_8, "AES-256-CCM-8": O.AES_256_CCM_8}
 VERSIONS = {"TLS1.2": O.TLS1_2, "TLS1.3": O.TLS1_3}
 
 
@@ -99,7 +104,7 @@ def test_record_fixtures():
 def _build_transforms(cipher, ver):
     """mbedtls_test_ssl_build_transforms (ssl_helpers.c:1361-1651): key0 =
     0x01.., key1 = 0x02.., iv_enc = 0x03.., iv_dec = 0x04.."""
-    kl = 16 if cipher == O.AES_128_GCM else 32
+    kl = O.KEYLEN[cipher]
     key0, key1 = bytes([1]) * kl, bytes([2]) * kl
     ive, ivd = bytes([3]) * 16, bytes([4]) * 16
     t_in = O.Transform(ver, cipher, key0, key1, ive, ivd)
