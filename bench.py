@@ -205,7 +205,7 @@ def main():
         for i in sample[:16]:
             s = int(recs["slot"][i])
             k = km[s]
-            klen = 16 if int(k["cipher"]) == M.CIPHER_AES_128_GCM else 32
+            klen = M.KEYLEN[int(k["cipher"])]
             ot = O.Transform(O.TLS1_3 if ver == M.VERSION_TLS1_3 else O.TLS1_2, oc[int(k["cipher"])],
                              bytes(k["key"][:klen]), bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
             buf = bytearray(stride)
@@ -279,7 +279,7 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
     import oracle as O
     cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM}.get(cname, O.AES_256_GCM)
     k = km[0]
-    klen = 16 if cipher == O.AES_128_GCM else 32
+    klen = O.KEYLEN[cipher]
     t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"][:klen]),
                     bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
     threads = min(16, os.cpu_count() or 1)

@@ -27,7 +27,8 @@
  * negative MBEDTLS_ERR_SSL_* value (include/mbedtls/ssl.h:40-125); the record
  * is transformed in place and its data_offset / data_len / type are updated
  * exactly as the reference updates them.  Only the AEAD suites are supported
- * (AES-128-GCM, AES-256-GCM, ChaCha20-Poly1305; TLS 1.2 and 1.3, no CID).
+ * (AES-128/192/256-GCM, AES-128/192/256-CCM and CCM_8, ChaCha20-Poly1305;
+ * TLS 1.2 and 1.3, no CID).
  *
  * Every entry point that touches record data runs on the GPU; there is no CPU
  * fallback.  Without a usable HIP device they return
@@ -59,6 +60,17 @@ extern "C" {
 #define TLSREC_CIPHER_AES_128_GCM        1
 #define TLSREC_CIPHER_AES_256_GCM        2
 #define TLSREC_CIPHER_CHACHA20_POLY1305  3
+/* the other AES AEADs of mbedtls_ssl_cipher_to_psa
+ * (ssl_tls.c:2168-2363).  The _CCM_8 ids are the MBEDTLS_CIPHERSUITE_SHORT_TAG
+ * suites (taglen 8: ssl_tls.c:7707-7708, ssl_tls13_keys.c:981-985). */
+#define TLSREC_CIPHER_AES_192_GCM        4
+#define TLSREC_CIPHER_AES_128_CCM        5
+#define TLSREC_CIPHER_AES_192_CCM        6
+#define TLSREC_CIPHER_AES_256_CCM        7
+#define TLSREC_CIPHER_AES_128_CCM_8      8
+#define TLSREC_CIPHER_AES_192_CCM_8      9
+#define TLSREC_CIPHER_AES_256_CCM_8      10
+#define TLSREC_CIPHER_MAX                10
 
 #define TLSREC_MSG_APPLICATION_DATA  23      /* ssl.h:527 */
 #define TLSREC_OUT_CONTENT_LEN       16384   /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
@@ -78,7 +90,7 @@ typedef struct tlsrec_transform {
     unsigned char iv_dec[16];
     int tls_version;         /* TLSREC_VERSION_* */
     int cipher;              /* TLSREC_CIPHER_* */
-    size_t keylen;           /* 16 or 32 */
+    size_t keylen;           /* 16, 24 or 32 */
     unsigned char key_enc[32];
     unsigned char key_dec[32];
     int32_t slot_enc;        /* device key slots (engine key table), -1 = none */
@@ -128,11 +140,11 @@ typedef struct tlsrec_key_material {
     uint8_t cipher;          /* TLSREC_CIPHER_* */
     uint8_t tls_minor;       /* 3 = TLS 1.2, 4 = TLS 1.3 */
     uint8_t fixed_ivlen;     /* 12, or 4 for TLS 1.2 GCM */
-    uint8_t taglen;          /* 16 */
+    uint8_t taglen;          /* 16, or 8 for TLSREC_CIPHER_AES_*_CCM_8 */
     uint8_t granularity;     /* TLS 1.3 padding granularity, 0 = 16 (ssl.h:432) */
     uint8_t reserved[11];
     uint8_t iv[16];          /* static IV, first fixed_ivlen bytes used */
-    uint8_t key[32];         /* 16 or 32 bytes used */
+    uint8_t key[32];         /* 16, 24 or 32 bytes used */
 } tlsrec_key_material;
 
 typedef struct tlsrec_keytab tlsrec_keytab;

@@ -32,6 +32,11 @@ VERSION_TLS1_3 = 0x0304
 CIPHER_AES_128_GCM = 1
 CIPHER_AES_256_GCM = 2
 CIPHER_CHACHA20_POLY1305 = 3
+CIPHER_AES_192_GCM = 4
+CIPHER_AES_128_CCM, CIPHER_AES_192_CCM, CIPHER_AES_256_CCM = 5, 6, 7
+CIPHER_AES_128_CCM_8, CIPHER_AES_192_CCM_8, CIPHER_AES_256_CCM_8 = 8, 9, 10
+KEYLEN = {1: 16, 2: 32, 3: 32, 4: 24, 5: 16, 6: 24, 7: 32, 8: 16, 9: 24, 10: 32}
+TAGLEN = {c: (8 if c >= 8 else 16) for c in KEYLEN}
 MSG_APPLICATION_DATA = 23
 ALG_SHA_256 = 0x02000009      # PSA_ALG_SHA_256
 ALG_SHA_384 = 0x0200000a      # PSA_ALG_SHA_384

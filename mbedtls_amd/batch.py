@@ -47,7 +47,7 @@ def key_material(cipher: int, tls_version: int, key: bytes, iv: bytes, granulari
     km["tls_minor"] = 4 if tls_version == _abi.VERSION_TLS1_3 else 3
     fixed = 12 if (tls_version == _abi.VERSION_TLS1_3 or cipher == _abi.CIPHER_CHACHA20_POLY1305) else 4
     km["fixed_ivlen"] = fixed
-    km["taglen"] = 16
+    km["taglen"] = _abi.TAGLEN[cipher]
     km["granularity"] = granularity
     km["iv"][0, :fixed] = np.frombuffer(bytes(iv)[:fixed], dtype=np.uint8)
     km["key"][0, :len(key)] = np.frombuffer(bytes(key), dtype=np.uint8)

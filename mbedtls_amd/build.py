@@ -25,8 +25,8 @@ HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wno-unuse
              "-Wno-unused-value", "-I" + INC, "-I" + CSRC]
 C_FLAGS = ["-O2", "-fPIC", "-std=c11", "-Wall", "-Wextra", "-I" + INC, "-I" + CSRC]
 
-HEADERS = ["tlsrec_device.h", "tlsrec_frame.h", "tlsrec_internal.h"]
-UNITS = [("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("tlsrec_host.c", "c")]
+HEADERS = ["tlsrec_device.h", "tlsrec_frame.h", "tlsrec_internal.h", "tlsrec_recdev.h"]
+UNITS = [("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("ccm.hip", "hip"), ("tlsrec_host.c", "c")]
 
 
 def _mtime(p):
@@ -40,7 +40,7 @@ def _deps():
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
     dep_time = max(_mtime(p) for p in _deps())
-    objs = []
+    objs, cmds = [], []
     for src, kind in UNITS:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src.rsplit(".", 1)[0] + ".o")
@@ -48,12 +48,17 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if not force and _mtime(o) > max(_mtime(s), dep_time):
             continue
         if kind == "hip":
-            cmd = [HIPCC] + HIP_FLAGS + ["-c", s, "-o", o]
+            cmds.append([HIPCC] + HIP_FLAGS + ["-c", s, "-o", o])
         else:
-            cmd = ["gcc"] + C_FLAGS + ["-c", s, "-o", o]
+            cmds.append(["gcc"] + C_FLAGS + ["-c", s, "-o", o])
+    # translation units compile in parallel (kernels.hip dominates)
+    from concurrent.futures import ThreadPoolExecutor
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(cmds)))) as ex:
+        list(ex.map(run, cmds))
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs
         if verbose:

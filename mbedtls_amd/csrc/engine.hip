@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include "tlsrec.h"
+#include "tlsrec_frame.h"
 #include "tlsrec_internal.h"
 
 using namespace tlsrec;
@@ -45,8 +46,9 @@ extern "C" int tlsrec_device_check(void)
 
 extern "C" const char *tlsrec_version_string(void)
 {
-    return "tlsrec 0.1 gfx950: aes-gcm(L=4/8/16/64, T-tables in LDS, GHASH 4-bit position tables) "
-           "chacha20-poly1305(L=1/2/4/8, 26-bit limbs)";
+    return "tlsrec 0.2 gfx950: aes-128/192/256-gcm(L=4/8/16/64, T-tables in LDS, GHASH 4-bit position tables) "
+           "aes-ccm/ccm_8(lane per record) chacha20-poly1305(L=1/2/4/8, 26-bit limbs) "
+           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer";
 }
 
 extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
@@ -94,10 +96,10 @@ extern "C" void tlsrec_keytab_free(tlsrec_keytab *kt)
 
 static int check_material(const tlsrec_key_material *k)
 {
-    if (k->cipher < TLSREC_CIPHER_AES_128_GCM || k->cipher > TLSREC_CIPHER_CHACHA20_POLY1305)
+    if (k->cipher < TLSREC_CIPHER_AES_128_GCM || k->cipher > TLSREC_CIPHER_MAX)
         return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
     if (k->tls_minor != 3 && k->tls_minor != 4) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    if (k->taglen != 16) return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
+    if (k->taglen != tlsrec_cipher_taglen(k->cipher)) return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
     if (k->fixed_ivlen != 12 && k->fixed_ivlen != 4) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     return 0;
 }
@@ -191,7 +193,8 @@ struct BucketScratch {
 static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
                   hipStream_t st, BucketScratch &b)
 {
-    const size_t nk = 2 * (size_t) kt->capacity + 2;   /* AES-128 slots, AES-256 slots, ChaCha, end */
+    /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, end */
+    const size_t nk = 4 * (size_t) kt->capacity + 2;
     b.scan_bytes = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, b.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
                                          (int) nk, st) != hipSuccess)
@@ -250,7 +253,10 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     }
     const uint32_t cap = kt->capacity;
     int rc = 0;
-    for (int cipher = TLSREC_CIPHER_AES_128_GCM; cipher <= TLSREC_CIPHER_AES_256_GCM && !rc; cipher++) {
+    static const int gcm_ciphers[3] = { TLSREC_CIPHER_AES_128_GCM, TLSREC_CIPHER_AES_256_GCM,
+                                        TLSREC_CIPHER_AES_192_GCM };
+    for (int ci = 0; ci < 3 && !rc; ci++) {
+        const int cipher = gcm_ciphers[ci];     /* bucket class ci: keys [ci * cap, (ci + 1) * cap) */
         if (!(kt->cipher_mask & (1u << cipher))) continue;
         /* lanes per record: a key pass should still fill the 16 waves of a
          * workgroup.  8 for a single key or >= 128 records per key; 16
@@ -267,8 +273,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.res = res;
         a.n = n;
         a.perm = identity ? nullptr : bs.perm;
-        a.lo = identity ? nullptr : bs.offs + (cipher == TLSREC_CIPHER_AES_128_GCM ? 0 : cap);
-        a.hi = identity ? nullptr : bs.offs + (cipher == TLSREC_CIPHER_AES_128_GCM ? cap : 2 * cap);
+        a.lo = identity ? nullptr : bs.offs + (size_t) ci * cap;
+        a.hi = identity ? nullptr : bs.offs + (size_t) (ci + 1) * cap;
         a.in = in;
         a.out = out;
         const int waves = gcm_waves();
@@ -277,8 +283,26 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.cipher = (uint32_t) cipher;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
-        int nr = cipher == TLSREC_CIPHER_AES_128_GCM ? 10 : 14;
+        int nr = (int) tlsrec_cipher_nr(cipher);
         if (tlsrec__launch_gcm(&a, dec, L, nr, waves, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    uint32_t ccm_nr = 0;
+    for (int c = TLSREC_CIPHER_AES_128_CCM; c <= TLSREC_CIPHER_AES_256_CCM_8; c++)
+        if (kt->cipher_mask & (1u << c)) ccm_nr |= 1u << tlsrec_cipher_nr(c);
+    if (!rc && ccm_nr) {
+        CcmArgs a;
+        a.slots = kt->d_slots;
+        a.recs = recs;
+        a.res = res;
+        a.n = n;
+        a.perm = identity ? nullptr : bs.perm;
+        a.lo = identity ? nullptr : bs.offs + 3 * (size_t) cap;
+        a.hi = identity ? nullptr : bs.offs + 4 * (size_t) cap;
+        a.in = in;
+        a.out = out;
+        a.capacity = cap;
+        a.flag_nr = 0;
+        if (tlsrec__launch_ccm(&a, dec, ccm_nr, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (!rc && (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
         int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;
@@ -288,8 +312,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.res = res;
         a.n = n;
         a.perm = identity ? nullptr : bs.perm;
-        a.lo = identity ? nullptr : bs.offs + 2 * cap;
-        a.hi = identity ? nullptr : bs.offs + 2 * cap + 1;
+        a.lo = identity ? nullptr : bs.offs + 4 * (size_t) cap;
+        a.hi = identity ? nullptr : bs.offs + 4 * (size_t) cap + 1;
         a.in = in;
         a.out = out;
         a.rpw = pick_rpw(n, CP_WAVES, 64 / L, (uint32_t) cu * 4);

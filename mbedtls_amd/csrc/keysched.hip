@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include "tlsrec.h"
+#include "tlsrec_frame.h"
 #include "tlsrec_internal.h"
 
 namespace tlsks {
@@ -322,7 +323,7 @@ __global__ void __launch_bounds__(64) tls13_derive_kernel(DeriveArgs a)
     km.cipher = (uint8_t) a.cipher;
     km.tls_minor = 4;
     km.fixed_ivlen = 12;      /* TLS 1.3: fixed_ivlen = ivlen = 12, ssl_tls13_keys.c:985-998 */
-    km.taglen = 16;
+    km.taglen = (uint8_t) tlsrec_cipher_taglen((int) a.cipher);
     /* ssl_tls13_make_traffic_key, ssl_tls13_keys.c:219-246 */
     hkdf_expand(a.alg, s, H, a.infos + a.len_upd, a.len_key, nullptr, 0, km.key, a.key_len);
     hkdf_expand(a.alg, s, H, a.infos + a.len_upd + a.len_key, a.len_iv, nullptr, 0, km.iv, 12);
@@ -655,12 +656,11 @@ extern "C" int tlsrec_tls13_keytab_derive(tlsrec_keytab *kt, uint32_t first, uin
     if (first > tlsrec_keytab_capacity(kt) || count > tlsrec_keytab_capacity(kt) - first)
         return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     uint32_t key_len, alg;
-    switch (cipher) {      /* TLS 1.3 suites: the AEAD fixes the hash (RFC 8446 B.4) */
-        case TLSREC_CIPHER_AES_128_GCM: key_len = 16; alg = H_SHA256; break;
-        case TLSREC_CIPHER_AES_256_GCM: key_len = 32; alg = H_SHA384; break;
-        case TLSREC_CIPHER_CHACHA20_POLY1305: key_len = 32; alg = H_SHA256; break;
-        default: return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
-    }
+    /* TLS 1.3 suites fix the hash with the AEAD (RFC 8446 B.4):
+     * TLS_AES_256_GCM_SHA384, every other suite SHA-256 */
+    key_len = tlsrec_cipher_keylen(cipher);
+    if (key_len == 0) return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
+    alg = cipher == TLSREC_CIPHER_AES_256_GCM ? H_SHA384 : H_SHA256;
     if (count == 0) return 0;
     hipStream_t st = (hipStream_t) stream;
     uint8_t infos[96];

@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include "tlsrec.h"
+#include "tlsrec_frame.h"
 #include "tlsrec_internal.h"
 
 using tlsrec::SlotState;
@@ -190,13 +191,13 @@ __global__ void in_finish_kernel(const tlsrec_stream_in *s, uint32_t n, const ui
 /* ---------------- send ------------------------------------------------- */
 struct OutShape {
     uint32_t ok;              /* slot usable */
-    uint32_t head;            /* explicit-IV room before the content (8 for TLS 1.2 GCM) */
-    uint32_t tls13, gran;
+    uint32_t head;            /* explicit-IV room before the content (8 for TLS 1.2 GCM / CCM) */
+    uint32_t tls13, gran, tag;
 };
 
 __device__ __forceinline__ OutShape out_shape(const SlotState *slots, uint32_t cap, uint32_t slot)
 {
-    OutShape o = { 0, 0, 0, 16 };
+    OutShape o = { 0, 0, 0, 16, 16 };
     if (slot >= cap) return o;
     const tlsrec_key_material &k = slots[slot].km;
     if (!k.cipher) return o;
@@ -204,6 +205,7 @@ __device__ __forceinline__ OutShape out_shape(const SlotState *slots, uint32_t c
     o.tls13 = k.tls_minor == 4;
     o.head = (!o.tls13 && k.fixed_ivlen == 4) ? 8u : 0u;
     o.gran = k.granularity ? k.granularity : 16;
+    o.tag = k.taglen;
     return o;
 }
 
@@ -212,9 +214,9 @@ __device__ __forceinline__ uint32_t out_body(const OutShape &o, uint32_t n)
 {
     if (o.tls13) {
         const uint32_t inner = n + 1;
-        return inner + (o.gran - inner % o.gran) % o.gran + 16;
+        return inner + (o.gran - inner % o.gran) % o.gran + o.tag;
     }
-    return o.head + n + 16;
+    return o.head + n + o.tag;
 }
 
 __device__ __forceinline__ uint32_t frag_of(const tlsrec_stream_out &s) { return s.max_frag ? s.max_frag : 16384u; }
@@ -404,7 +406,8 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
 extern "C" uint64_t tlsrec_stream_out_size(int tls_version, int cipher, uint32_t granularity, uint64_t in_len,
                                            uint32_t max_frag)
 {
-    if (cipher < TLSREC_CIPHER_AES_128_GCM || cipher > TLSREC_CIPHER_CHACHA20_POLY1305) return 0;
+    if (tlsrec_cipher_keylen(cipher) == 0) return 0;
+    const uint64_t tag = tlsrec_cipher_taglen(cipher);
     if (tls_version != TLSREC_VERSION_TLS1_2 && tls_version != TLSREC_VERSION_TLS1_3) return 0;
     const uint64_t f = max_frag ? max_frag : 16384;
     const uint64_t g = granularity ? granularity : 16;
@@ -412,9 +415,9 @@ extern "C" uint64_t tlsrec_stream_out_size(int tls_version, int cipher, uint32_t
     auto body = [&](uint64_t n) -> uint64_t {
         if (tls_version == TLSREC_VERSION_TLS1_3) {
             const uint64_t inner = n + 1;
-            return inner + (g - inner % g) % g + 16;
+            return inner + (g - inner % g) % g + tag;
         }
-        return head + n + 16;
+        return head + n + tag;
     };
     const uint64_t full = in_len / f, rest = in_len % f;
     return full * (5 + body(f)) + (rest ? 5 + body(rest) : 0);

@@ -36,6 +36,23 @@
 #define TLSREC_E_INVALID_RECORD   (-0x7200)
 #define TLSREC_E_INTERNAL_ERROR   (-0x6C00)
 
+/* Cipher properties (mbedtls_ssl_cipher_to_psa, ssl_tls.c:2168-2363; the
+ * _CCM_8 ids are the short-tag suites).  Ids: include/tlsrec.h. */
+TLSREC_HD uint32_t tlsrec_cipher_keylen(int c)
+{
+    switch (c) {
+        case 1: case 5: case 8: return 16;              /* AES-128 GCM / CCM / CCM_8 */
+        case 4: case 6: case 9: return 24;              /* AES-192 */
+        case 2: case 3: case 7: case 10: return 32;     /* AES-256, ChaCha20-Poly1305 */
+        default: return 0;
+    }
+}
+TLSREC_HD uint32_t tlsrec_cipher_taglen(int c) { return (c >= 8 && c <= 10) ? 8u : 16u; }
+TLSREC_HD int tlsrec_cipher_is_gcm(int c) { return c == 1 || c == 2 || c == 4; }
+TLSREC_HD int tlsrec_cipher_is_ccm(int c) { return c >= 5 && c <= 10; }
+/* AES rounds of an AES-based cipher, 0 otherwise */
+TLSREC_HD uint32_t tlsrec_cipher_nr(int c) { return c == 3 ? 0u : tlsrec_cipher_keylen(c) / 4 + 6; }
+
 typedef struct tlsrec_plan {
     int32_t  status;          /* error found before the AEAD (no AEAD runs) */
     int32_t  post_status;     /* error the reference returns after its AEAD */
@@ -64,7 +81,7 @@ typedef struct tlsrec_plan {
 typedef struct tlsrec_plan_key {
     int tls13;
     uint32_t fixed_ivlen;     /* 12 or 4 */
-    uint32_t taglen;          /* 16 */
+    uint32_t taglen;          /* 16, or 8 for the CCM_8 suites */
     const uint8_t *iv;        /* fixed IV (iv_enc for encrypt, iv_dec for decrypt) */
 } tlsrec_plan_key;
 
@@ -162,7 +179,7 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     p->aad_len = tlsrec__aad(p->aad, k->tls13, ctr, p->type, ver,
                              (uint32_t) (k->tls13 ? len + k->taglen : len));
     p->aead_len = (uint32_t) len;
-    p->data_len = (uint32_t) (len + 16);                               /* psa_aead_encrypt output */
+    p->data_len = (uint32_t) (len + k->taglen);                        /* psa_aead_encrypt output */
     if (p->explicit_iv) {                                              /* :1066-1075 */
         if (data_offset < 8) {
             p->post_status = TLSREC_E_BUFFER_TOO_SMALL;

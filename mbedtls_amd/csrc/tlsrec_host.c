@@ -46,16 +46,12 @@ int tlsrec_transform_setup_ex(tlsrec_transform *t, int tls_version, int cipher,
     memset(t, 0, sizeof(*t));
     t->slot_enc = t->slot_dec = -1;
     t->granularity = granularity;
-    switch (cipher) {                      /* mbedtls_ssl_cipher_to_psa, ssl_tls.c:2168-2363 */
-        case TLSREC_CIPHER_AES_128_GCM: t->keylen = 16; break;
-        case TLSREC_CIPHER_AES_256_GCM:
-        case TLSREC_CIPHER_CHACHA20_POLY1305: t->keylen = 32; break;
-        default: return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
-    }
+    t->keylen = tlsrec_cipher_keylen(cipher);   /* mbedtls_ssl_cipher_to_psa, ssl_tls.c:2168-2363 */
+    if (t->keylen == 0) return TLSREC_ERR_SSL_FEATURE_UNAVAILABLE;
     t->cipher = cipher;
     t->tls_version = tls_version;
     t->ivlen = 12;
-    t->taglen = 16;
+    t->taglen = tlsrec_cipher_taglen(cipher);   /* short-tag suites: ssl_tls.c:7707-7708 */
     t->maclen = 0;
     if (tls_version == TLSREC_VERSION_TLS1_3) {           /* ssl_tls13_keys.c:985-998 */
         t->fixed_ivlen = t->ivlen;

@@ -49,7 +49,7 @@ struct GcmArgs {
     uint8_t *out;
     uint32_t rpw;             /* records per wavefront chunk (<= 64) */
     uint32_t capacity;
-    uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM */
+    uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM / _192_GCM */
 };
 
 struct CpArgs {
@@ -65,23 +65,39 @@ struct CpArgs {
     uint32_t capacity;
 };
 
-/* Bucket pass: key class of a record = 0 (AES-128-GCM slot), 1 (AES-256-GCM
- * slot), 2 (ChaCha20-Poly1305), 3 (no usable slot: BAD_INPUT_DATA). */
+/* Bucket pass: key index of a record = AES-128-GCM slot, AES-256-GCM slot,
+ * AES-192-GCM slot, AES-CCM slot (cap-sized classes, in this order), then one
+ * ChaCha20-Poly1305 class; no usable slot: BAD_INPUT_DATA. */
 struct BucketArgs {
     const SlotState *slots;
     const tlsrec_batch_rec *recs;
     tlsrec_batch_res *res;
     uint32_t n;
     uint32_t capacity;
-    uint32_t *counts;         /* [2 * capacity + 1] records per (class, slot), then exclusive offsets */
+    uint32_t *counts;         /* [4 * capacity + 1] records per (class, slot), then exclusive offsets */
     uint32_t *cursor;         /* copy of the offsets, consumed by the scatter */
     uint32_t *cp_cursor;      /* ChaCha records appended after the GCM ones */
     uint32_t *perm;           /* [n] */
 };
 
+/* AES-CCM records (ccm.hip): one lane per record, key passes per wave. */
+struct CcmArgs {
+    const SlotState *slots;
+    const tlsrec_batch_rec *recs;
+    tlsrec_batch_res *res;
+    uint64_t n;
+    const uint32_t *perm;
+    const uint32_t *lo, *hi;
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t capacity;
+    uint32_t flag_nr;         /* identity order: the launch (AES rounds) that flags unusable slots */
+};
+
 } /* namespace tlsrec */
 
 extern "C" {
+hipError_t tlsrec__launch_ccm(const tlsrec::CcmArgs *a, int dec, uint32_t nr_mask, hipStream_t st);
 hipError_t tlsrec__launch_keysetup(tlsrec::SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
                                    uint32_t first, uint32_t count, hipStream_t st);
 hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int nr, int waves, uint32_t grid,

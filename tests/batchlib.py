@@ -11,12 +11,15 @@ import oracle as O
 from tests.prng import prng_bytes
 
 CIPHERS = {"AES-128-GCM": M.CIPHER_AES_128_GCM, "AES-256-GCM": M.CIPHER_AES_256_GCM,
-           "CHACHA20-POLY1305": M.CIPHER_CHACHA20_POLY1305}
+           "CHACHA20-POLY1305": M.CIPHER_CHACHA20_POLY1305, "AES-192-GCM": M.CIPHER_AES_192_GCM,
+           "AES-128-CCM": M.CIPHER_AES_128_CCM, "AES-192-CCM": M.CIPHER_AES_192_CCM,
+           "AES-256-CCM": M.CIPHER_AES_256_CCM, "AES-128-CCM-8": M.CIPHER_AES_128_CCM_8,
+           "AES-192-CCM-8": M.CIPHER_AES_192_CCM_8, "AES-256-CCM-8": M.CIPHER_AES_256_CCM_8}
 VERSIONS = {"TLS1.2": M.VERSION_TLS1_2, "TLS1.3": M.VERSION_TLS1_3}
 
 
 def keylen(cipher):
-    return 16 if cipher == M.CIPHER_AES_128_GCM else 32
+    return M.KEYLEN[cipher]
 
 
 def explicit(cipher, ver):

@@ -93,7 +93,12 @@ def test_batch_vs_oracle(cipher, ver, decrypt):
     else:
         recs = B.plaintext_records(slots, lengths, seed=cipher * 7 + ver)
     b = B.Batch(slots, recs)
-    lane_opts = [0, 4, 16, 64] if cipher != M.CIPHER_CHACHA20_POLY1305 else [0, 1, 4, 8]
+    if cipher == M.CIPHER_CHACHA20_POLY1305:
+        lane_opts = [0, 1, 4, 8]
+    elif cipher in (M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_AES_192_GCM):
+        lane_opts = [0, 4, 16, 64]
+    else:
+        lane_opts = [0]              # CCM: one lane per record, no lane option
     for lanes in lane_opts:
         out, res = b.run_gpu(decrypt, lanes=lanes)
         bad = b.compare(decrypt, out, res)
@@ -185,22 +190,23 @@ def test_large_roundtrip_16k():
     encrypt then decrypt restores every payload; a sample is bit-exact vs the
     oracle."""
     n = 512
-    for cipher in (M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305):
+    for cipher in (M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305, M.CIPHER_AES_128_CCM_8):
         slots = B.random_slots(5 + cipher, [cipher], [M.VERSION_TLS1_3], 1)
         recs = B.plaintext_records(slots, [16383] * n, seed=9, head=0, tail=17)
         b = B.Batch(slots, recs)
         out, res = b.run_gpu(False)
-        assert (res["status"] == 0).all() and (res["data_len"] == 16400).all()
+        wire = 16384 + M.TAGLEN[cipher]
+        assert (res["status"] == 0).all() and (res["data_len"] == wire).all()
         sample = B.Batch(slots, recs[:8])
         o_recs, _ = sample.run_oracle(False)
         for i in range(8):
             o = b.offs[i]
-            assert bytes(out[o:o + 16400]) == o_recs[i].data()
+            assert bytes(out[o:o + wire]) == o_recs[i].data()
         # decrypt the GPU ciphertext
         b.arena[:] = out
         d = b.desc.copy()
         d["data_offset"] = 0
-        d["data_len"] = 16400
+        d["data_len"] = wire
         d["type"] = 23
         b.desc = d
         out2, res2 = b.run_gpu(True)
@@ -235,12 +241,11 @@ def test_gcm_counter_boundary(cipher):
 
 @pytest.mark.parametrize("lanes", [0, 8, 16])
 def test_many_keys_all_ciphers_round_robin(lanes):
-    """Bucket pass: 3 ciphers x 2 TLS versions over 150 keys, records
+    """Bucket pass: all 10 AEADs x 2 TLS versions over 150 keys, records
     round-robin over keys (every neighbour has another key), ragged lengths;
     bit-exact vs the oracle for both directions and several lane counts."""
     nkeys = 150
-    slots = B.random_slots(9001, [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305],
-                           [M.VERSION_TLS1_2, M.VERSION_TLS1_3], nkeys)
+    slots = B.random_slots(9001, ALL_C, [M.VERSION_TLS1_2, M.VERSION_TLS1_3], nkeys)
     lengths = [int(x) for x in np.frombuffer(prng_bytes(31337, 2 * nkeys * 5), np.uint16) % 3000]
     for decrypt in (False, True):
         recs = (B.sealed_records(slots, lengths, seed=5)[0] if decrypt
@@ -251,14 +256,18 @@ def test_many_keys_all_ciphers_round_robin(lanes):
         assert not bad, "; ".join(bad[:5])
 
 
-@pytest.mark.parametrize("nslots", [1, 4], ids=["identity", "bucket"])
-def test_unusable_slot_gets_bad_input(nslots):
+@pytest.mark.parametrize("nslots,ciphers", [(1, [M.CIPHER_AES_256_GCM]), (1, [M.CIPHER_AES_128_CCM]),
+                                            (1, [M.CIPHER_CHACHA20_POLY1305]),
+                                            (4, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]),
+                                            (4, [M.CIPHER_AES_128_CCM_8, M.CIPHER_AES_192_GCM])],
+                         ids=["identity-gcm", "identity-ccm", "identity-chacha", "bucket", "bucket-ccm"])
+def test_unusable_slot_gets_bad_input(nslots, ciphers):
     """Records naming a slot past the table or never loaded are reported
     BAD_INPUT_DATA with their buffer untouched; the other records are
     processed normally -- with a single-key table (kernels walk the
     descriptors in order) and a multi-key one (bucket pass)."""
     import torch
-    slots = B.random_slots(123, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305], [M.VERSION_TLS1_3], nslots)
+    slots = B.random_slots(123, ciphers, [M.VERSION_TLS1_3], nslots)
     recs = B.plaintext_records(slots, [100, 2000, 17, 500, 64, 1400], seed=3)
     b = B.Batch(slots, recs)
     d = b.desc.copy()

@@ -107,7 +107,7 @@ def test_keytab_derive_end_to_end(cipher, update):
     torch.cuda.synchronize()
     got_secrets = secrets.cpu().numpy().tobytes()
     slots = [(cipher, M.VERSION_TLS1_3, bytes(16), bytes(12), 0)] * 5
-    klen = 16 if cipher == M.CIPHER_AES_128_GCM else 32
+    klen = M.KEYLEN[cipher]
     for i in range(n):
         s = raw[48 * i:48 * i + H]
         if update:

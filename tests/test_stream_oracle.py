@@ -44,7 +44,7 @@ CFGS = [(O.TLS1_3, O.AES_256_GCM), (O.TLS1_3, O.CHACHA20_POLY1305), (O.TLS1_2, O
 
 
 def _t(v, c, seed=1):
-    k = prng_bytes(seed, 32)[:16 if c == O.AES_128_GCM else 32]
+    k = prng_bytes(seed, 32)[:O.KEYLEN[c]]
     iv = prng_bytes(seed + 1, 12)
     return O.Transform(v, c, k, k, iv, iv)
 
