@@ -41,6 +41,13 @@ CONFIGS = {
            "ChaCha20-Poly1305 encrypt, 1M x 1.4 KiB TLS 1.3 records, single key"),
     "c4": ("MIX", "TLS1.3", "decrypt", 16383, 1 << 22, 1 << 16,
            "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 16 KiB TLS 1.3 decrypt"),
+    # SURVEY 8(f)-2 rows, same shape as c2 (not BASELINE configs)
+    "ccm": ("AES-128-CCM", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
+            "AES-128-CCM decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
+    "ccm8": ("AES-128-CCM-8", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
+             "AES-128-CCM_8 decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
+    "gcm192": ("AES-192-GCM", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
+               "AES-192-GCM decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
     "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
             "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 1.4 KiB TLS 1.3 decrypt"),
 }
@@ -92,9 +99,12 @@ def main():
     ver = M.VERSION_TLS1_3 if tls == "TLS1.3" else M.VERSION_TLS1_2
     inner = inner_len(content, tls)
     head = 8 if tls == "TLS1.2" and cname != "CHACHA20-POLY1305" else 0   # TLS 1.2 GCM explicit nonce
-    wire = head + inner + 16
+    taglen = 8 if cname.endswith("CCM-8") else 16
+    wire = head + inner + taglen
     stride = (wire + args.align - 1) // args.align * args.align
-    ciphers = {"AES-128-GCM": [M.CIPHER_AES_128_GCM], "AES-256-GCM": [M.CIPHER_AES_256_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
+    ciphers = {"AES-128-GCM": [M.CIPHER_AES_128_GCM], "AES-256-GCM": [M.CIPHER_AES_256_GCM],
+               "AES-128-CCM": [M.CIPHER_AES_128_CCM], "AES-128-CCM-8": [M.CIPHER_AES_128_CCM_8],
+               "AES-192-GCM": [M.CIPHER_AES_192_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
                "MIX": [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]}[cname]
     nkeys = min(nkeys, n)
 
@@ -106,7 +116,7 @@ def main():
         km["cipher"] = np.array([ciphers[i % len(ciphers)] for i in range(nkeys)], dtype=np.uint8)
         km["tls_minor"] = 4 if ver == M.VERSION_TLS1_3 else 3
         km["fixed_ivlen"] = 4 if head else 12
-        km["taglen"] = 16
+        km["taglen"] = [M.TAGLEN[c] for c in km["cipher"]]
         km["key"] = raw[:, :32]
         km["iv"][:, :12] = raw[:, 32:44]
     keys_dev = M.broadcast_keys(km, dev)          # RCCL broadcast when world > 1
@@ -198,8 +208,7 @@ def main():
     oracle_ok = None
     if rank == 0 and args.verify:
         import oracle as O
-        oc = {M.CIPHER_AES_128_GCM: O.AES_128_GCM, M.CIPHER_AES_256_GCM: O.AES_256_GCM,
-              M.CIPHER_CHACHA20_POLY1305: O.CHACHA20_POLY1305}
+        oc = {c: c for c in M.KEYLEN}      # the oracle shares the cipher ids
         oracle_ok = True
         src = arena if direction == "decrypt" else out_arena
         for i in sample[:16]:
@@ -277,7 +286,8 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
     """oracle/ (the CPU restatement, kind 'port') timed on this host's cores on
     a bounded sample of the same workload."""
     import oracle as O
-    cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM}.get(cname, O.AES_256_GCM)
+    cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM, "AES-128-CCM": O.AES_128_CCM,
+              "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-GCM": O.AES_192_GCM}.get(cname, O.AES_256_GCM)
     k = km[0]
     klen = O.KEYLEN[cipher]
     t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"][:klen]),
