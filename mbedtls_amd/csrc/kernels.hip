@@ -648,7 +648,7 @@ __device__ __forceinline__ void chacha_block_kn(const uint32_t *kn, uint32_t cou
 }
 
 template <int L, bool DEC>
-__global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void tlsrec_chachapoly_kernel(CpArgs a)
+__global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void tlsrec_chachapoly_kernel(CpArgs a)
 {
     constexpr int R = 64 / L;
     constexpr int LOGL = Log2<L>::v;
@@ -814,18 +814,9 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const uint32_t jl = jh ? 1u : Jmax;
         uint32_t j = 0;
         for (; j < jl; j++) general(j);
-        for (; j < jh; j++) {
-            const uint32_t b = L * j + q - z;
-            const uint8_t *sp = src + (size_t) b * 64;
-            uint4 c[4];
-#pragma unroll
-            for (int t = 0; t < 4; t++) c[t] = gload16(sp + 16 * t);
-            /* keep the loads here, a ChaCha20 block ahead of their use: left
-             * alone, the scheduler sinks each to just before its XOR and the
-             * step pays four serial memory latencies */
-            asm volatile("" ::: "memory");
-            uint32_t ks[16];
-            chacha_block_kn(cr.key, b + 1u, ks);
+        /* one body chunk: load (a ChaCha20 block ahead of use), XOR, store,
+         * Horner step acc*r^(4L) + c0 r^3 + c1 r^2 + c2 r + c3 */
+        auto absorb = [&](uint4 (&c)[4], const uint32_t (&ks)[16], uint32_t b) {
             uint8_t *dp = dst + (size_t) b * 64;
 #pragma unroll
             for (int t = 0; t < 4; t++) {
@@ -843,6 +834,42 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             p_mac(dd, p_from_words(c[1]), p_lds(cr.r2));
             p_mac(dd, p_from_words(c[2]), p_lds(cr.r1));
             acc = p_reduce(dd);
+        };
+        /* two chunks per lane per step: two key-stream blocks in lockstep */
+        for (; j + 1 < jh; j += 2) {
+            const uint32_t b0 = L * j + q - z, b1 = b0 + L;
+            uint4 c0[4], c1[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                c0[t] = gload16(src + (size_t) b0 * 64 + 16 * t);
+                c1[t] = gload16(src + (size_t) b1 * 64 + 16 * t);
+            }
+            asm volatile("" ::: "memory");
+            uint32_t ks0[16], ks1[16];
+            {
+                uint32_t key[8], nw[3];
+#pragma unroll
+                for (int i = 0; i < 8; i++) key[i] = cr.key[i];
+#pragma unroll
+                for (int i = 0; i < 3; i++) nw[i] = cr.nonce[i];
+                chacha_block2(key, b0 + 1u, b1 + 1u, nw, ks0, ks1);
+            }
+            absorb(c0, ks0, b0);
+            absorb(c1, ks1, b1);
+        }
+        for (; j < jh; j++) {
+            const uint32_t b = L * j + q - z;
+            const uint8_t *sp = src + (size_t) b * 64;
+            uint4 c[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) c[t] = gload16(sp + 16 * t);
+            /* keep the loads here, a ChaCha20 block ahead of their use: left
+             * alone, the scheduler sinks each to just before its XOR and the
+             * step pays four serial memory latencies */
+            asm volatile("" ::: "memory");
+            uint32_t ks[16];
+            chacha_block_kn(cr.key, b + 1u, ks);
+            absorb(c, ks, b);
         }
         for (; j < Jmax; j++) general(j);
 

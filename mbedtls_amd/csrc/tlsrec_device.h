@@ -460,6 +460,40 @@ __device__ __forceinline__ void chacha_block(const uint32_t key[8], uint32_t cou
     for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
 }
 
+/* Two blocks of one key stream (counters c0, c1) in lockstep: the eight
+ * independent quarter-round chains of a double round interleave, twice the
+ * ILP of chacha_block for the dependency-bound VALU pipeline. */
+__device__ __forceinline__ void chacha_block2(const uint32_t key[8], uint32_t c0, uint32_t c1, const uint32_t nonce[3],
+                                              uint32_t o0[16], uint32_t o1[16])
+{
+    const uint32_t in[16] = { 0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                              key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                              0u, nonce[0], nonce[1], nonce[2] };
+    uint32_t x[16], y[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) { x[i] = in[i]; y[i] = in[i]; }
+    x[12] = c0;
+    y[12] = c1;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        TLSREC_QR(x[0], x[4], x[8], x[12]);  TLSREC_QR(y[0], y[4], y[8], y[12]);
+        TLSREC_QR(x[1], x[5], x[9], x[13]);  TLSREC_QR(y[1], y[5], y[9], y[13]);
+        TLSREC_QR(x[2], x[6], x[10], x[14]); TLSREC_QR(y[2], y[6], y[10], y[14]);
+        TLSREC_QR(x[3], x[7], x[11], x[15]); TLSREC_QR(y[3], y[7], y[11], y[15]);
+        TLSREC_QR(x[0], x[5], x[10], x[15]); TLSREC_QR(y[0], y[5], y[10], y[15]);
+        TLSREC_QR(x[1], x[6], x[11], x[12]); TLSREC_QR(y[1], y[6], y[11], y[12]);
+        TLSREC_QR(x[2], x[7], x[8], x[13]);  TLSREC_QR(y[2], y[7], y[8], y[13]);
+        TLSREC_QR(x[3], x[4], x[9], x[14]);  TLSREC_QR(y[3], y[4], y[9], y[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        o0[i] = x[i] + in[i];
+        o1[i] = y[i] + in[i];
+    }
+    o0[12] += c0;
+    o1[12] += c1;
+}
+
 /* ---------------- Poly1305 in 26-bit limbs ----------------------------- */
 struct P5 { uint32_t v[5]; };
 
