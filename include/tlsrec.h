@@ -356,6 +356,40 @@ int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_out *stre
                           tlsrec_batch_res *res, uint32_t max_records, tlsrec_stream_out_res *sres,
                           uint32_t *nrecords, void *stream);
 
+/* ---- session tickets (library/ssl_ticket.c) ------------
+ * mbedtls_ssl_ticket_write / mbedtls_ssl_ticket_parse for a batch of tickets
+ * in device memory.  Ticket = key_name[4] || iv[12] || len16 || state ||
+ * tag[16] (ssl_ticket.c:44-55); AEAD nonce = iv, AAD = the 18 header bytes.
+ * The ticket keys are key-table slots holding an AES-GCM, AES-CCM (16-byte
+ * tag) or ChaCha20-Poly1305 key (the cipher of mbedtls_ssl_ticket_setup). */
+#define TLSREC_ERR_SSL_SESSION_TICKET_EXPIRED (-0x6D80)   /* ssl.h:111 */
+#define TLSREC_TICKET_MIN_LEN 34                          /* TICKET_MIN_LEN, ssl_ticket.c:49-52 */
+
+/* the keys[2] / active fields of mbedtls_ssl_ticket_context */
+typedef struct tlsrec_ticket_keys {
+    uint32_t slot[2];        /* key-table slots of keys[0], keys[1] */
+    uint8_t  name[2][4];     /* their key names */
+    uint32_t active;         /* ctx->active: the key new tickets use */
+} tlsrec_ticket_keys;
+
+typedef struct tlsrec_ticket {
+    uint64_t off;            /* ticket start in the arena */
+    uint32_t len;            /* write: end - start (space); parse: ticket length */
+    uint32_t clear_len;      /* write: serialized session length; the state is at off + 18 and the caller's
+                                random IV at off + 4 (psa_generate_random, ssl_ticket.c:255) */
+} tlsrec_ticket;
+
+typedef struct tlsrec_ticket_res {
+    int32_t  status;         /* 0 or MBEDTLS_ERR_SSL_* as the reference returns it */
+    uint32_t tlen;           /* write: *tlen; parse: clear_len (state decrypted in place at off + 18) */
+    uint32_t reserved[2];
+} tlsrec_ticket_res;
+
+int tlsrec_ticket_write(const tlsrec_keytab *kt, const tlsrec_ticket_keys *keys, const tlsrec_ticket *tickets,
+                        uint32_t n, uint8_t *arena, tlsrec_ticket_res *res, void *stream);
+int tlsrec_ticket_parse(const tlsrec_keytab *kt, const tlsrec_ticket_keys *keys, const tlsrec_ticket *tickets,
+                        uint32_t n, uint8_t *arena, tlsrec_ticket_res *res, void *stream);
+
 /* ---- engine ------------------------------------------------------------- */
 /* 0 if a gfx950 device is usable, else TLSREC_ERR_SSL_HW_ACCEL_FAILED. */
 int tlsrec_device_check(void);

@@ -24,6 +24,7 @@ ERR_SSL_INVALID_RECORD = -0x7200
 ERR_SSL_HW_ACCEL_FAILED = -0x7F80
 ERR_SSL_INTERNAL_ERROR = -0x6C00
 ERR_SSL_COUNTER_WRAPPING = -0x6B80
+ERR_SSL_SESSION_TICKET_EXPIRED = -0x6D80
 MAX_IN_RECORD = 16421
 OUT_BUF_SPACE = 16416
 
@@ -60,6 +61,9 @@ STREAM_OUT = np.dtype([("in_off", "<u8"), ("in_len", "<u4"), ("slot", "<u4"), ("
                        ("out_ctr", "u1", 8), ("max_frag", "<u4"), ("type", "u1"), ("reserved", "u1", 3)])
 STREAM_OUT_RES = np.dtype([("status", "<i4"), ("first", "<u4"), ("nrec", "<u4"), ("out_len", "<u4"),
                            ("out_ctr", "u1", 8), ("nparsed", "<u4"), ("reserved", "u1", 4)])
+TICKET = np.dtype([("off", "<u8"), ("len", "<u4"), ("clear_len", "<u4")])
+TICKET_RES = np.dtype([("status", "<i4"), ("tlen", "<u4"), ("reserved", "<u4", 2)])
+assert TICKET.itemsize == 16 and TICKET_RES.itemsize == 16
 assert STREAM_IN.itemsize == 32 and STREAM_IN_RES.itemsize == 32
 assert STREAM_OUT.itemsize == 40 and STREAM_OUT_RES.itemsize == 32
 assert KEY_MATERIAL.itemsize == 64 and BATCH_REC.itemsize == 40 and BATCH_RES.itemsize == 16
@@ -81,6 +85,11 @@ class CKeySet(ctypes.Structure):
     _fields_ = [("client_write_key", ctypes.c_ubyte * 32), ("server_write_key", ctypes.c_ubyte * 32),
                 ("client_write_iv", ctypes.c_ubyte * 16), ("server_write_iv", ctypes.c_ubyte * 16),
                 ("key_len", ctypes.c_size_t), ("iv_len", ctypes.c_size_t)]
+
+
+class CTicketKeys(ctypes.Structure):
+    """the keys[2] / active fields of mbedtls_ssl_ticket_context"""
+    _fields_ = [("slot", ctypes.c_uint32 * 2), ("name", (ctypes.c_uint8 * 4) * 2), ("active", ctypes.c_uint32)]
 
 
 class CRecord(ctypes.Structure):
@@ -112,6 +121,8 @@ SIGNATURES = {
     "tlsrec_tls13_exporter": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _VP, _SZ]),
     "tlsrec_tls13_update_traffic_secret": (_INT, [_INT, _VP, _VP]),
     "tlsrec_tls13_keytab_derive": (_INT, [_VP, _U32, _U32, _INT, _VP, _INT, _VP]),
+    "tlsrec_ticket_write": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _VP]),
+    "tlsrec_ticket_parse": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_stream_decrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_stream_out_size": (ctypes.c_uint64, [_INT, _INT, _U32, ctypes.c_uint64, _U32]),
     "tlsrec_stream_encrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),

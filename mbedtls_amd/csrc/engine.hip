@@ -150,6 +150,7 @@ extern "C" int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t co
  * then the key-setup kernel on the staged slots. */
 extern "C" tlsrec_key_material *tlsrec__keytab_stage(tlsrec_keytab *kt) { return kt->d_stage; }
 extern "C" const SlotState *tlsrec__keytab_slots(const tlsrec_keytab *kt) { return kt->d_slots; }
+extern "C" const uint4 *tlsrec__keytab_ghtab(const tlsrec_keytab *kt) { return kt->d_ghtab; }
 
 extern "C" int tlsrec__keytab_commit_staged(tlsrec_keytab *kt, uint32_t first, uint32_t count, int cipher,
                                             hipStream_t st)

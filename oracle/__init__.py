@@ -389,3 +389,45 @@ def stream_encrypt(t: "Transform", pt: bytes, rtype: int = 23, out_ctr: bytes = 
     r = f(t._mem, bytes(pt), len(pt), rtype, ctr, max_frag, out_buf_space, out, cap, ctypes.byref(olen),
           ctypes.byref(nrec))
     return r, out.raw[:olen.value], nrec.value, bytes(ctr)
+
+
+# ---- session tickets (oracle/ticket.c) -------------------------------------------
+ERR_SESSION_TICKET_EXPIRED = -0x6D80
+
+
+class _TicketKey(ctypes.Structure):
+    _fields_ = [("cipher", ctypes.c_int), ("key", ctypes.c_uint8 * 32), ("name", ctypes.c_uint8 * 4)]
+
+
+def _tkeys(keys):
+    arr = (_TicketKey * 2)()
+    for i, (c, k, name) in enumerate(keys):
+        arr[i].cipher = c
+        arr[i].key[:len(k)] = list(k)
+        arr[i].name[:] = list(name)
+    return arr
+
+
+def ticket_write(keys, active: int, iv: bytes, state: bytes, space: int):
+    """keys: [(cipher, key, name4)] x 2.  Returns (status, ticket bytes)."""
+    buf = ctypes.create_string_buffer(max(space, 18 + len(state), 16))
+    buf[4:16] = bytes(iv)
+    buf[18:18 + len(state)] = bytes(state)
+    tlen = _S()
+    f = lib().orc_ticket_write
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _S, _S, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    r = f(_tkeys(keys), active, buf, space, len(state), ctypes.byref(tlen))
+    return r, buf.raw[:tlen.value] if r == 0 else b""
+
+
+def ticket_parse(keys, ticket: bytes):
+    """Returns (status, clear state bytes, buffer after)."""
+    buf = ctypes.create_string_buffer(bytes(ticket), max(1, len(ticket)))
+    cl = _S()
+    f = lib().orc_ticket_parse
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _S, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    r = f(_tkeys(keys), buf, len(ticket), ctypes.byref(cl))
+    raw = buf.raw[:len(ticket)]
+    return r, (raw[18:18 + cl.value] if r == 0 else b""), raw

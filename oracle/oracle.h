@@ -229,6 +229,17 @@ int orc_stream_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, ui
                        size_t max_frag, size_t out_buf_space, uint8_t *out, size_t out_cap, size_t *out_len,
                        uint32_t *nrec);
 
+/* ---- session tickets (oracle/ticket.c) ----------------------------------- */
+#define ORC_ERR_SSL_SESSION_TICKET_EXPIRED (-0x6D80)   /* ssl.h:111 */
+typedef struct {
+    int cipher;              /* ORC_CIPHER_AES_*_GCM / _CCM (16-byte tag) / CHACHA20_POLY1305 */
+    uint8_t key[32];
+    uint8_t name[4];
+} orc_ticket_key;
+int orc_ticket_write(const orc_ticket_key keys[2], int active, uint8_t *start, size_t space, size_t clear_len,
+                     size_t *tlen);
+int orc_ticket_parse(const orc_ticket_key keys[2], uint8_t *buf, size_t len, size_t *clear_len);
+
 #ifdef __cplusplus
 }
 #endif
