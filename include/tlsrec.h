@@ -325,6 +325,29 @@ int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_stream_in *strea
                           uint32_t max_records, tlsrec_stream_in_res *sres, uint32_t *nrecords,
                           void *stream);
 
+/* Read side of mbedtls_ssl_read over the records tlsrec_stream_decrypt
+ * accepted: per connection, ssl_read_application_data (ssl_msg.c:5627-5650)
+ * in record order -- copy at most out_cap bytes of application data (type 23
+ * records; other content types are the caller's) to out_arena + out_off and
+ * zeroize the plaintext handed out; a record only partly consumed keeps its
+ * tail (in_offt += n). */
+typedef struct tlsrec_stream_read_req {
+    uint64_t out_off;        /* the caller's buffer (buf of mbedtls_ssl_read) in out_arena */
+    uint32_t out_cap;        /* len */
+    uint32_t reserved;
+} tlsrec_stream_read_req;
+
+typedef struct tlsrec_stream_read_res {
+    uint32_t copied;         /* bytes written to the caller's buffer */
+    uint32_t records;        /* accepted records fully consumed (non-application ones included) */
+    uint32_t left;           /* bytes still unread in the next record (in_msglen) */
+    uint32_t reserved;
+} tlsrec_stream_read_res;
+
+int tlsrec_stream_read(const tlsrec_stream_in_res *sres, uint32_t nstreams, const tlsrec_batch_rec *recs,
+                       const tlsrec_batch_res *res, uint8_t *arena, const tlsrec_stream_read_req *req,
+                       uint8_t *out_arena, tlsrec_stream_read_res *rres, void *stream);
+
 /* One connection's application data to send. */
 typedef struct tlsrec_stream_out {
     uint64_t in_off;         /* plaintext in the input arena */

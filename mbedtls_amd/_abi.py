@@ -64,6 +64,9 @@ STREAM_OUT_RES = np.dtype([("status", "<i4"), ("first", "<u4"), ("nrec", "<u4"),
 TICKET = np.dtype([("off", "<u8"), ("len", "<u4"), ("clear_len", "<u4")])
 TICKET_RES = np.dtype([("status", "<i4"), ("tlen", "<u4"), ("reserved", "<u4", 2)])
 assert TICKET.itemsize == 16 and TICKET_RES.itemsize == 16
+STREAM_READ_REQ = np.dtype([("out_off", "<u8"), ("out_cap", "<u4"), ("reserved", "<u4")])
+STREAM_READ_RES = np.dtype([("copied", "<u4"), ("records", "<u4"), ("left", "<u4"), ("reserved", "<u4")])
+assert STREAM_READ_REQ.itemsize == 16 and STREAM_READ_RES.itemsize == 16
 assert STREAM_IN.itemsize == 32 and STREAM_IN_RES.itemsize == 32
 assert STREAM_OUT.itemsize == 40 and STREAM_OUT_RES.itemsize == 32
 assert KEY_MATERIAL.itemsize == 64 and BATCH_REC.itemsize == 40 and BATCH_RES.itemsize == 16
@@ -124,6 +127,7 @@ SIGNATURES = {
     "tlsrec_ticket_write": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_ticket_parse": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_stream_decrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
+    "tlsrec_stream_read": (_INT, [_VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "tlsrec_stream_out_size": (ctypes.c_uint64, [_INT, _INT, _U32, ctypes.c_uint64, _U32]),
     "tlsrec_stream_encrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_version_string": (ctypes.c_char_p, []),

@@ -321,6 +321,57 @@ __global__ void out_finish_kernel(const tlsrec_stream_out *s, uint32_t n, const 
     sres[i] = o;
 }
 
+/* ---------------- read (ssl_read_application_data) -------------------- */
+/* One workgroup per connection: every thread walks the (few) records to the
+ * same copy plan; the copies move 16 bytes per thread at any alignment. */
+__global__ void __launch_bounds__(256) read_kernel(const tlsrec_stream_in_res *sres, uint32_t n,
+                                                   const tlsrec_batch_rec *recs, const tlsrec_batch_res *res,
+                                                   uint8_t *arena, const tlsrec_stream_read_req *req, uint8_t *out,
+                                                   tlsrec_stream_read_res *rres)
+{
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const uint32_t first = sres[i].first, nrec = sres[i].nrec, cap = req[i].out_cap;
+    uint8_t *dst0 = out + req[i].out_off;
+    uint32_t done = 0, full = 0, rest = 0;
+    for (uint32_t k = 0; k < nrec; k++) {
+        const tlsrec_batch_res r = res[first + k];
+        if (r.type != TLSREC_MSG_APPLICATION_DATA) {
+            full++;
+            continue;
+        }
+        uint8_t *src = arena + recs[first + k].buf_off + r.data_offset;
+        const uint32_t m = r.data_len < cap - done ? r.data_len : cap - done;
+        uint8_t *dst = dst0 + done;
+        const uint32_t nv = m / 16;
+        for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+            uint4 w;
+            __builtin_memcpy(&w, src + 16 * v, 16);
+            __builtin_memcpy(dst + 16 * v, &w, 16);
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            __builtin_memcpy(src + 16 * v, &z, 16);          /* mbedtls_platform_zeroize(in_offt, n) */
+        }
+        for (uint32_t b = nv * 16 + threadIdx.x; b < m; b += blockDim.x) {
+            dst[b] = src[b];
+            src[b] = 0;
+        }
+        done += m;
+        if (m < r.data_len) {
+            rest = r.data_len - m;
+            break;
+        }
+        full++;
+    }
+    if (threadIdx.x == 0) {
+        tlsrec_stream_read_res o;
+        o.copied = done;
+        o.records = full;
+        o.left = rest;
+        o.reserved = 0;
+        rres[i] = o;
+    }
+}
+
 } /* namespace tlsst */
 
 using namespace tlsst;
@@ -458,4 +509,15 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
     if (sc.mem && hipFreeAsync(sc.mem, st) != hipSuccess && r == 0) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     if (r == 0 && nrecords) *nrecords = total;
     return r;
+}
+
+extern "C" int tlsrec_stream_read(const tlsrec_stream_in_res *sres, uint32_t nstreams, const tlsrec_batch_rec *recs,
+                                  const tlsrec_batch_res *res, uint8_t *arena, const tlsrec_stream_read_req *req,
+                                  uint8_t *out_arena, tlsrec_stream_read_res *rres, void *stream)
+{
+    if (nstreams && (!sres || !recs || !res || !arena || !req || !out_arena || !rres)) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (nstreams == 0) return 0;
+    hipLaunchKernelGGL(read_kernel, dim3(nstreams), dim3(256), 0, (hipStream_t) stream, sres, nstreams, recs, res,
+                       arena, req, out_arena, rres);
+    return hipGetLastError() == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
 }

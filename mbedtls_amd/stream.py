@@ -17,6 +17,7 @@ from .batch import KeyTable, _ptr, _stream
 
 STREAM_IN, STREAM_IN_RES = _abi.STREAM_IN, _abi.STREAM_IN_RES
 STREAM_OUT, STREAM_OUT_RES = _abi.STREAM_OUT, _abi.STREAM_OUT_RES
+STREAM_READ_REQ, STREAM_READ_RES = _abi.STREAM_READ_REQ, _abi.STREAM_READ_RES
 
 
 class StreamError(RuntimeError):
@@ -59,3 +60,15 @@ def encrypt(kt: KeyTable, streams, n: int, in_arena, out_arena, recs, res, max_r
     if r != 0:
         raise StreamError("tlsrec_stream_encrypt", r)
     return total.value
+
+
+def read(sres, n: int, recs, res, arena, req, out_arena, rres, stream=None) -> None:
+    """ssl_read_application_data over the accepted records of each connection
+    (tlsrec_stream_read): application data gathered into the callers'
+    buffers, the plaintext handed out zeroized in the arena."""
+    dev = arena.device if hasattr(arena, "device") else None
+    req = _dev(req, dev)
+    r = _abi.load().tlsrec_stream_read(_ptr(sres), n, _ptr(recs), _ptr(res), _ptr(arena), _ptr(req),
+                                       _ptr(out_arena), _ptr(rres), _stream(stream))
+    if r != 0:
+        raise StreamError("tlsrec_stream_read", r)

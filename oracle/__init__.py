@@ -367,6 +367,23 @@ def stream_decrypt(t: "Transform", data: bytes, in_ctr: bytes = bytes(8), nb_zer
              "nb_zero": res.nb_zero}, out, buf.raw[:len(data)])
 
 
+def stream_read(buf: bytes, recs, cap: int):
+    """ssl_read_application_data over accepted records [(off, data_offset,
+    data_len, type)]: returns (copied bytes, records fully consumed, bytes
+    left in the last record, buffer after zeroization)."""
+    b = ctypes.create_string_buffer(bytes(buf), max(1, len(buf)))
+    arr = (_StreamRec * max(1, len(recs)))()
+    for i, (o, d, L, t) in enumerate(recs):
+        arr[i].off, arr[i].data_offset, arr[i].data_len, arr[i].type = o, d, L, t
+    out = ctypes.create_string_buffer(max(1, cap))
+    c, r, lft = _S(), _S(), _S()
+    f = lib().orc_stream_read
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _S, ctypes.c_void_p, _S, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p]
+    f(b, arr, len(recs), out, cap, ctypes.byref(c), ctypes.byref(r), ctypes.byref(lft))
+    return out.raw[:c.value], r.value, lft.value, b.raw[:len(buf)]
+
+
 def stream_record_wire(t: "Transform", n: int) -> int:
     f = lib().orc_stream_record_wire
     f.argtypes = [ctypes.c_void_p, _S]

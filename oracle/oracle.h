@@ -225,6 +225,8 @@ int orc_stream_decrypt(const orc_transform *t, uint8_t *buf, size_t len, const u
                        size_t max_record, int max_version, orc_stream_rec *out, size_t max_out,
                        orc_stream_res *res);
 size_t orc_stream_record_wire(const orc_transform *t, size_t n);
+int orc_stream_read(uint8_t *buf, const orc_stream_rec *recs, size_t nrec, uint8_t *out, size_t cap,
+                    size_t *copied, size_t *records, size_t *left);
 int orc_stream_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, uint8_t type, uint8_t out_ctr[8],
                        size_t max_frag, size_t out_buf_space, uint8_t *out, size_t out_cap, size_t *out_len,
                        uint32_t *nrec);

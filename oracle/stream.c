@@ -170,3 +170,35 @@ int orc_stream_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, ui
     }
     return 0;
 }
+
+/* The read side of mbedtls_ssl_read over a connection's accepted records:
+ * ssl_read_application_data (ssl_msg.c:5627-5650) copies at most the
+ * caller's remaining space from each application-data record in order and
+ * zeroizes the bytes it handed out (mbedtls_platform_zeroize(in_offt, n));
+ * a record only partly consumed keeps its tail (in_offt += n).  Records of
+ * other content types are left to the caller (not application data). */
+int orc_stream_read(uint8_t *buf, const orc_stream_rec *recs, size_t nrec, uint8_t *out, size_t cap,
+                    size_t *copied, size_t *records, size_t *left)
+{
+    size_t done = 0, full = 0, rest = 0;
+    for (size_t k = 0; k < nrec; k++) {
+        if (recs[k].type != 23) {
+            full++;
+            continue;
+        }
+        uint8_t *src = buf + recs[k].off + recs[k].data_offset;
+        size_t n = recs[k].data_len < cap - done ? recs[k].data_len : cap - done;
+        memcpy(out + done, src, n);
+        memset(src, 0, n);
+        done += n;
+        if (n < recs[k].data_len) {
+            rest = recs[k].data_len - n;
+            break;
+        }
+        full++;
+    }
+    *copied = done;
+    *records = full;
+    *left = rest;
+    return 0;
+}

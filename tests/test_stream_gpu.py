@@ -206,3 +206,49 @@ def test_too_many_records_is_buffer_too_small():
     assert e.value.code == M.ERR_SSL_BUFFER_TOO_SMALL
     assert ta.cpu().numpy().tobytes() == w          # nothing decrypted
     c.close()
+
+
+def test_stream_read_matches_oracle():
+    """tlsrec_stream_read (ssl_read_application_data over the accepted
+    records) against the oracle: bytes handed out, zeroization in place,
+    records consumed and bytes left, for several buffer sizes."""
+    slots = _slots(77)
+    c = Conns(slots)
+    rng = np.random.default_rng(3)
+    jobs = []
+    for i in range(40):
+        n = int(rng.choice([1, 300, 5000, 16384, 30000]))
+        jobs.append((i % 20, prng_bytes(3000 + i, n), int(rng.integers(0, 1 << 30)), int(rng.choice([0, 1000])),
+                     23 if i % 4 else 22))
+    got = c.encrypt(jobs)
+    conns = [(slot, out, ctr, 0) for (slot, _, ctr, _, _), (_, out) in zip(jobs, got)]
+    a, recs, res, sres, offs = c.decrypt(conns)
+    dev = torch.device("cuda")
+    for cap_kind in (0, 1, 2):
+        caps = [[0, 17, 1000][cap_kind] if k % 3 else len(j[1]) + 5 for k, j in enumerate(jobs)]
+        req = np.zeros(len(jobs), dtype=S.STREAM_READ_REQ)
+        pos, outs = 0, []
+        for k, cap in enumerate(caps):
+            req[k] = (pos, cap, 0)
+            outs.append(pos)
+            pos += (cap + 127) // 128 * 128 + 128
+        ta = torch.from_numpy(a.copy()).to(dev)
+        tout = torch.zeros(max(pos, 16), dtype=torch.uint8, device=dev)
+        rres = torch.zeros(len(jobs) * 16, dtype=torch.uint8, device=dev)
+        S.read(torch.from_numpy(sres.view(np.uint8).copy()).to(dev), len(jobs),
+               torch.from_numpy(recs.view(np.uint8).copy()).to(dev), torch.from_numpy(res.view(np.uint8).copy()).to(dev),
+               ta, req, tout, rres)
+        torch.cuda.synchronize()
+        a2, o2 = ta.cpu().numpy(), tout.cpu().numpy()
+        rr = rres.cpu().numpy().view(S.STREAM_READ_RES)
+        for k, (slot, data, ctr, nbz) in enumerate(conns):
+            g = sres[k]
+            f, nrec = int(g["first"]), int(g["nrec"])
+            wrecs = [(int(recs[f + j]["buf_off"]) - offs[k], int(res[f + j]["data_offset"]),
+                      int(res[f + j]["data_len"]), int(res[f + j]["type"])) for j in range(nrec)]
+            region = a[offs[k]:offs[k] + len(data)].tobytes()
+            out, full, left, after = O.stream_read(region, wrecs, caps[k])
+            assert (int(rr["copied"][k]), int(rr["records"][k]), int(rr["left"][k])) == (len(out), full, left), k
+            assert o2[outs[k]:outs[k] + len(out)].tobytes() == out
+            assert a2[offs[k]:offs[k] + len(data)].tobytes() == after
+    c.close()

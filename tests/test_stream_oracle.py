@@ -124,3 +124,21 @@ def test_zero_length_records_limit_and_counter_wrap():
     wire = bytes([23, 3, 3]) + rec.data_len.to_bytes(2, "big") + rec.data()
     res, _, _ = O.stream_decrypt(t, wire, last)
     assert res["status"] == O.ERR_COUNTER_WRAPPING and res["nrec"] == 0
+
+
+def test_stream_read_copies_and_zeroizes():
+    t = _t(O.TLS1_3, O.AES_128_GCM)
+    _, w1, _, c = O.stream_encrypt(t, prng_bytes(6, 250), 23, bytes(8), 100)
+    _, w2, _, c = O.stream_encrypt(t, prng_bytes(7, 30), 22, c, 100)        # a handshake record between
+    _, w3, _, c = O.stream_encrypt(t, prng_bytes(8, 120), 23, c, 100)
+    res, recs, buf = O.stream_decrypt(t, w1 + w2 + w3, bytes(8))
+    assert res["status"] == 0 and res["nrec"] == 6
+    app = prng_bytes(6, 250) + prng_bytes(8, 120)
+    for cap in (0, 1, 99, 100, 250, 300, 370, 1000):
+        out, full, left, after = O.stream_read(buf, recs, cap)
+        assert out == app[:cap]
+        # every byte handed out was zeroized in place, nothing else touched
+        handed = sum(1 for o, d, L, ty in recs if ty == 23)
+        assert handed >= 0 and len(after) == len(buf)
+        if cap >= len(app):
+            assert full == 6 and left == 0
