@@ -174,6 +174,17 @@ static int gcm_waves(void)
     return w;
 }
 
+/* wave-pass GCM variant (per-wave key passes, H^L per wave in LDS) for
+ * tables of many keys with very few records each (auto: < 8 per key, where
+ * a workgroup-wide key pass leaves most waves idle; measured +17-20 % at 4
+ * x 16 KiB per key, -45 % at 16 per key).  TLSREC_GCM_WP=1 forces it, =0
+ * disables it. */
+static int gcm_wp_env(void)
+{
+    const char *e = getenv("TLSREC_GCM_WP");   /* read per batch: tests switch it */
+    return e ? atoi(e) : -1;
+}
+
 static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t target_wgs)
 {
     uint64_t want = (n + (uint64_t) waves_per_wg * target_wgs - 1) / ((uint64_t) waves_per_wg * target_wgs);
@@ -278,14 +289,16 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.hi = identity ? nullptr : bs.offs + (size_t) (ci + 1) * cap;
         a.in = in;
         a.out = out;
-        const int waves = gcm_waves();
+        int nr = (int) tlsrec_cipher_nr(cipher);
+        const int wpe = gcm_wp_env();
+        const bool wp = !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && rpk < 8));
+        const int waves = wp ? 8 : gcm_waves();
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
-        int nr = (int) tlsrec_cipher_nr(cipher);
-        if (tlsrec__launch_gcm(&a, dec, L, nr, waves, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : waves, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     uint32_t ccm_nr = 0;
     for (int c = TLSREC_CIPHER_AES_128_CCM; c <= TLSREC_CIPHER_AES_256_CCM_8; c++)

@@ -149,9 +149,12 @@ template <> struct Log2<16> { static constexpr int v = 4; };
 template <> struct Log2<32> { static constexpr int v = 5; };
 template <> struct Log2<64> { static constexpr int v = 6; };
 
-template <int L, int W>
+/* WP (wave passes): each wave keeps only its current key's H^L table in its
+ * own 8 KiB of LDS; the once-per-record multiplies (AAD fold, tree, final)
+ * read the key's tables in global memory. */
+template <int L, int W, bool WP = false>
 struct GcmLds {
-    static constexpr int NT = Log2<L>::v + 1;           /* GHASH tables H^1 .. H^L */
+    static constexpr int NT = WP ? W : Log2<L>::v + 1;  /* GHASH tables H^1 .. H^L, or one H^L per wave */
     static constexpr int GH = 0;
     static constexpr int AES = NT * 8192;               /* T0/T1 x 32 copies */
     static constexpr int EJ0 = AES + 65536;             /* W waves x 64 x 16 B */
@@ -210,10 +213,10 @@ __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
     }
 }
 
-template <int L, int NR, bool DEC, int W, int B>
+template <int L, int NR, bool DEC, int W, int B, bool WP = false>
 __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 {
-    using LY = GcmLds<L, W>;
+    using LY = GcmLds<L, W, WP>;
     constexpr int NTHR = W * 64;
     constexpr int LOGL = Log2<L>::v;
     constexpr int R = 64 / L;
@@ -238,7 +241,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     /* pass membership: lane l tracks the record at chunk position k = l */
     uint32_t my_slot = 0xffffffffu, my_rec = 0;
     {
-        const uint64_t pos = wg_base + (uint64_t) lane * W + wave;
+        /* WP: a wave's positions are contiguous (its key runs stay together) */
+        const uint64_t pos = WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const uint32_t s = a.recs[my_rec].slot;
@@ -253,20 +257,37 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
     __syncthreads();
 
+    /* Horner multiplier table H^L (hor) and the per-record tables H^1..H^(L/2) (gp) */
+    constexpr int HPI = WP ? 0 : LOGL;                   /* H^L table index from hor */
+    const uint8_t *hor = WP ? lds + LY::GH + wave * 8192 : lds + LY::GH;
     for (int iter = 0;; iter++) {
-        uint32_t *cur = &ctl[iter & 1];
-        if (my_slot != 0xffffffffu) atomicMin(cur, my_slot);
-        __syncthreads();
-        const uint32_t s = __builtin_amdgcn_readfirstlane(*cur);
-        if (s == 0xffffffffu) break;
-        if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
-        /* stage the slot's GHASH tables and round keys */
-        {
-            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
-            uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
-            for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
+        uint32_t s;
+        if constexpr (WP) {
+            /* wave pass: the wave's smallest pending slot; stage its H^L table
+             * into the wave's LDS (in-order LDS queue: the wave's writes land
+             * before its reads; the asm keeps the compiler from hoisting) */
+            s = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
+            if (s == 0xffffffffu) break;
+            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
+            uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
+            for (int i = lane; i < 512; i += 64) dst[i] = src[i];
+            asm volatile("" ::: "memory");
+        } else {
+            uint32_t *cur = &ctl[iter & 1];
+            if (my_slot != 0xffffffffu) atomicMin(cur, my_slot);
+            __syncthreads();
+            s = __builtin_amdgcn_readfirstlane(*cur);
+            if (s == 0xffffffffu) break;
+            if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
+            /* stage the slot's GHASH tables and round keys */
+            {
+                const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
+                uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
+                for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
+            }
+            __syncthreads();
         }
-        __syncthreads();
+        const uint8_t *gp = WP ? reinterpret_cast<const uint8_t *>(a.ghtab + (size_t) s * KEY_TABLE_WORDS) : lds + LY::GH;
         /* Round keys through the constant address space: scalar loads.  (Read
          * through a.slots they compile to vector loads + vmcnt(0) waits in
          * every round, since the kernel's own stores might alias the table.) */
@@ -326,7 +347,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * only the step with cc == 0 reads it. */
             uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + wave * 64 + lane;
             {
-                const uint4 aadh = gmul<0>(lds, jb.aadw);
+                const uint4 aadh = gmul<0>(gp, jb.aadw);
                 *fold = m ? aadh : jb.aadw;
             }
             /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
@@ -356,10 +377,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 auto crypt = [&](int32_t cc, uint4 y, uint4 &ks, uint4 &Zn) {
                     const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
                     if constexpr (CACHED) {
-                        aes_ghash<NR, LY::AES, LOGL>(lds, lanebase, rk, ccache, ctrw, y, ks, Zn);
+                        aes_ghash<NR, LY::AES, HPI>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
                     } else {
                         ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
-                        Zn = gmul<LOGL>(lds, y);
+                        Zn = gmul<HPI>(hor, y);
                     }
                 };
                 auto general = [&](uint32_t j) {
@@ -428,10 +449,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
             }
             /* tree: sum_q Y_q H^(L-q) */
-            Y = gtree<L / 2>(lds, Y, lane);
-            Y = gmul<0>(lds, Y);                                     /* T */
+            Y = gtree<L / 2>(gp, Y, lane);
+            Y = gmul<0>(gp, Y);                                      /* T */
             uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
-            Y = gmul<0>(lds, xor4(Y, lenw));                         /* GHASH */
+            Y = gmul<0>(gp, xor4(Y, lenw));                          /* GHASH */
             if (!jb.run) continue;
             const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
             const uint4 tag = xor4(Y, ej0);
@@ -951,6 +972,14 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
 /* ======================================================================
  * Launchers
  * ==================================================================== */
+template <int L, int NR, bool DEC>
+static hipError_t launch_gcm_wp(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    /* wave passes: 8 waves x 2 blocks per lane (LDS: 8 x 8 KiB H^L + 64 KiB T-tables) */
+    hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 8, 2, true>), dim3(grid), dim3(8 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
 template <int L, int NR, bool DEC, int W>
 static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
 {
@@ -965,6 +994,13 @@ static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
 template <int L, bool DEC>
 static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t grid, hipStream_t st)
 {
+    if (waves == -8) {   /* wave-pass variant (engine: many keys, few records each) */
+        if constexpr (L == 16 || L == 64) {
+            if (nr == 10) return launch_gcm_wp<L, 10, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_wp<L, 14, DEC>(a, grid, st);
+        }
+        return hipErrorInvalidValue;
+    }
     if (nr == 12) return launch_gcm_t<L, 12, DEC, 16>(a, grid, st);   /* AES-192: 16-wave variant only */
     if (waves == 8)
         return nr == 10 ? launch_gcm_t<L, 10, DEC, 8>(a, grid, st) : launch_gcm_t<L, 14, DEC, 8>(a, grid, st);

@@ -271,8 +271,8 @@ __device__ __forceinline__ CtrCache ctr_cache(const uint8_t *lds, uint32_t lb, R
  * accumulator and the source words still to be read, so no read moves into an
  * earlier phase (bounded reads in flight and VGPRs, no memory clobber). */
 template <int NR, int AES_OFF, int PI, int R0 = 2, int RS = 1, typename RK>
-__device__ __forceinline__ void aes_ghash(const uint8_t *lds, uint32_t lb, RK rk, const CtrCache &cc, uint32_t ctrw,
-                                          uint4 y, uint4 &ks, uint4 &prod)
+__device__ __forceinline__ void aes_ghash(const uint8_t *lds, const uint8_t *gh, uint32_t lb, RK rk,
+                                          const CtrCache &cc, uint32_t ctrw, uint4 y, uint4 &ks, uint4 &prod)
 {
     static_assert(R0 >= 2 && R0 + 7 * RS <= NR - 1, "GHASH groups must fall on middle rounds 2..NR-1");
 #define TA(x, k) tlook<AES_OFF>(lds, (x), lb, (k), 0)
@@ -296,7 +296,7 @@ __device__ __forceinline__ void aes_ghash(const uint8_t *lds, uint32_t lb, RK rk
         if (r > 2) aes_round<AES_OFF>(lds, lb, rk, r, s0, s1, s2, s3);
         const int g = (r - R0) / RS;
         if (r >= R0 && (r - R0) % RS == 0 && g < 8) {
-            gmul_word<PI, 2>(lds, w[g >> 1], g >> 1, acc, 2 * (g & 1));
+            gmul_word<PI, 2>(gh, w[g >> 1], g >> 1, acc, 2 * (g & 1));
             asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(acc.x), "+v"(acc.y), "+v"(acc.z),
                          "+v"(acc.w));
             /* the words still to be read enter the next phase through the barrier */

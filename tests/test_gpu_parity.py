@@ -256,6 +256,31 @@ def test_many_keys_all_ciphers_round_robin(lanes):
         assert not bad, "; ".join(bad[:5])
 
 
+@pytest.mark.parametrize("lanes", [16, 64])
+def test_gcm_wave_pass(lanes, monkeypatch):
+    """Wave-pass GCM variant (TLSREC_GCM_WP=1: per-wave key passes, H^L per
+    wave in LDS, per-record tables from HBM): 200 keys of GCM-128/192/256 and
+    ChaCha, both TLS versions, ragged lengths incl. the edge list, tampered
+    records -- bit-exact vs the oracle in both directions."""
+    monkeypatch.setenv("TLSREC_GCM_WP", "1")
+    nkeys = 200
+    slots = B.random_slots(777 + lanes, [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_AES_192_GCM,
+                                         M.CIPHER_CHACHA20_POLY1305],
+                           [M.VERSION_TLS1_2, M.VERSION_TLS1_3], nkeys)
+    lengths = EDGE_LENGTHS + [int(x) for x in np.frombuffer(prng_bytes(4711, 2 * 3 * nkeys), np.uint16) % 5000]
+    for decrypt in (False, True):
+        recs = (B.sealed_records(slots, lengths, seed=8)[0] if decrypt
+                else B.plaintext_records(slots, lengths, seed=8))
+        if decrypt:
+            for i in range(0, len(recs), 11):
+                r = recs[i]
+                r.buf[r.data_offset + (i * 7) % r.data_len] ^= 4
+        b = B.Batch(slots, recs)
+        out, res = b.run_gpu(decrypt, lanes=lanes)
+        bad = b.compare(decrypt, out, res)
+        assert not bad, "; ".join(bad[:5])
+
+
 @pytest.mark.parametrize("nslots,ciphers", [(1, [M.CIPHER_AES_256_GCM]), (1, [M.CIPHER_AES_128_CCM]),
                                             (1, [M.CIPHER_CHACHA20_POLY1305]),
                                             (4, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]),
