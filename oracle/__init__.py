@@ -168,12 +168,13 @@ class _CRecord(ctypes.Structure):
     _fields_ = [("ctr", ctypes.c_uint8 * 8), ("type", ctypes.c_uint8),
                 ("ver", ctypes.c_uint8 * 2), ("buf", ctypes.c_void_p),
                 ("buf_len", ctypes.c_size_t), ("data_offset", ctypes.c_size_t),
-                ("data_len", ctypes.c_size_t)]
+                ("data_len", ctypes.c_size_t), ("cid_len", ctypes.c_uint8),
+                ("cid", ctypes.c_uint8 * 32)]
 
 
 @dataclass
 class Record:
-    """Python mirror of mbedtls_record (library/ssl_misc.h:1163-1188), non-CID."""
+    """Python mirror of mbedtls_record (library/ssl_misc.h:1163-1188)."""
     ctr: bytes
     type: int
     ver: bytes
@@ -181,6 +182,7 @@ class Record:
     data_offset: int
     data_len: int
     buf_len: int = field(default=-1)
+    cid: bytes = b""           # DTLS 1.2 connection ID (rec->cid / cid_len)
 
     def __post_init__(self):
         if self.buf_len < 0:
@@ -204,6 +206,14 @@ class Transform:
             raise ValueError(f"orc_transform_setup failed: {r}")
         self.tls_version, self.cipher = tls_version, cipher
 
+    def set_cid(self, in_cid: bytes, out_cid: bytes) -> None:
+        """DTLS 1.2 connection IDs of the transform (in_cid / out_cid)."""
+        f = lib().orc_transform_set_cid
+        f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        r = f(self._mem, bytes(in_cid), len(in_cid), bytes(out_cid), len(out_cid))
+        if r != 0:
+            raise ValueError(f"orc_transform_set_cid failed: {r}")
+
     def _call(self, fn, rec: Record) -> int:
         c = _CRecord()
         c.ctr[:] = list(rec.ctr)
@@ -214,10 +224,13 @@ class Transform:
         c.buf_len = rec.buf_len
         c.data_offset = rec.data_offset
         c.data_len = rec.data_len
+        c.cid_len = len(rec.cid)
+        c.cid[:len(rec.cid)] = list(rec.cid)
         r = fn(self._mem, ctypes.byref(c))
         del cbuf
         rec.type, rec.ver = c.type, bytes(c.ver)
         rec.data_offset, rec.data_len = c.data_offset, c.data_len
+        rec.cid = bytes(c.cid[:c.cid_len])
         return r
 
     def encrypt_buf(self, rec: Record) -> int:

@@ -659,22 +659,75 @@ static void build_nonce(uint8_t nonce[12], const uint8_t *fixed, size_t fixed_le
     for (int i = 0; i < 8; i++) nonce[4 + i] ^= dyn[i];
 }
 
-/* ssl_msg.c:568-735, non-CID branches */
-static size_t build_aad(uint8_t aad[13], const orc_record *rec, int tls_version, size_t taglen)
+/* ssl_msg.c:568-735.  Non-CID: TLS 1.3 type || ver || len(TLSCiphertext),
+ * TLS 1.2 seq || type || ver || len.  DTLS 1.2 + CID (RFC 9146, :683-724):
+ * 0xff x 8 || type || cid_len || type || ver || epoch+seq || cid || len. */
+static size_t build_aad(uint8_t aad[23 + ORC_CID_LEN_MAX], const orc_record *rec, int tls_version, size_t taglen)
 {
     size_t n = 0, len_field = rec->data_len;
     if (tls_version == ORC_VERSION_TLS1_3) {
         len_field += taglen;           /* :671-677 */
+    } else if (rec->cid_len != 0) {
+        memset(aad, 0xff, 8);          /* seq_num_placeholder, :685-687 */
+        n = 8;
+        aad[n++] = rec->type;          /* tls12_cid, :690-691 */
+        aad[n++] = rec->cid_len;       /* :694-695 */
     } else {
         memcpy(aad, rec->ctr, 8);      /* :700-703 */
         n = 8;
     }
-    aad[n++] = rec->type;
-    aad[n++] = rec->ver[0];
+    aad[n++] = rec->type;              /* :707-709 */
+    aad[n++] = rec->ver[0];            /* :711-713 */
     aad[n++] = rec->ver[1];
-    aad[n++] = (uint8_t) (len_field >> 8);
+    if (tls_version != ORC_VERSION_TLS1_3 && rec->cid_len != 0) {
+        memcpy(aad + n, rec->ctr, 8);  /* :717-720 */
+        n += 8;
+        memcpy(aad + n, rec->cid, rec->cid_len);   /* :722-724 */
+        n += rec->cid_len;
+    }
+    aad[n++] = (uint8_t) (len_field >> 8);         /* :727-731 */
     aad[n++] = (uint8_t) len_field;
     return n;
+}
+
+int orc_transform_set_cid(orc_transform *t, const uint8_t *in_cid, size_t in_len,
+                          const uint8_t *out_cid, size_t out_len)
+{
+    if (in_len > ORC_CID_LEN_MAX || out_len > ORC_CID_LEN_MAX) return ORC_ERR_SSL_BAD_INPUT_DATA;
+    t->in_cid_len = (uint8_t) in_len;
+    t->out_cid_len = (uint8_t) out_len;
+    memset(t->in_cid, 0, sizeof(t->in_cid));
+    memset(t->out_cid, 0, sizeof(t->out_cid));
+    if (in_len) memcpy(t->in_cid, in_cid, in_len);
+    if (out_len) memcpy(t->out_cid, out_cid, out_len);
+    return 0;
+}
+
+/* ssl_build_inner_plaintext (ssl_msg.c:466-491) with the padding of
+ * ssl_compute_padding_length (:431-435) */
+static int build_inner(uint8_t *data, size_t *len, size_t remaining, uint8_t type, size_t g)
+{
+    size_t pad = (g - (*len + 1) % g) % g, n = *len;
+    if (remaining == 0) return -1;
+    data[n++] = type;
+    remaining--;
+    if (remaining < pad) return -1;
+    memset(data + n, 0, pad);
+    *len = n + pad;
+    return 0;
+}
+
+/* ssl_parse_inner_plaintext (ssl_msg.c:496-514) */
+static int parse_inner(const uint8_t *data, size_t *len, uint8_t *type)
+{
+    size_t remaining = *len;
+    do {
+        if (remaining == 0) return -1;
+        remaining--;
+    } while (data[remaining] == 0);
+    *len = remaining;
+    *type = data[remaining];
+    return 0;
 }
 
 static int is_ccm(int c) { return c >= ORC_CIPHER_AES_128_CCM && c <= ORC_CIPHER_AES_256_CCM_8; }
@@ -715,22 +768,21 @@ int orc_encrypt_buf(const orc_transform *t, orc_record *rec)
     if (rec->data_len > ORC_OUT_CONTENT_LEN) return ORC_ERR_SSL_BAD_INPUT_DATA; /* :831-839 */
 
     if (t->tls_version == ORC_VERSION_TLS1_3) {                          /* :853-868 */
-        size_t g = t->granularity;
-        size_t pad = (g - (rec->data_len + 1) % g) % g;                  /* :431-435 */
-        size_t len = rec->data_len, remaining = post_avail;
-        if (remaining == 0) return ORC_ERR_SSL_BUFFER_TOO_SMALL;         /* :471-479 */
-        data[len++] = rec->type;
-        remaining--;
-        if (remaining < pad) return ORC_ERR_SSL_BUFFER_TOO_SMALL;
-        memset(data + len, 0, pad);
-        len += pad;
-        rec->data_len = len;
+        if (build_inner(data, &rec->data_len, post_avail, rec->type, t->granularity) != 0)
+            return ORC_ERR_SSL_BUFFER_TOO_SMALL;
         rec->type = 23;                                                  /* APPLICATION_DATA */
+    }
+    rec->cid_len = t->out_cid_len;                                       /* :874-875 */
+    memcpy(rec->cid, t->out_cid, t->out_cid_len);
+    if (rec->cid_len != 0) {                                             /* :878-897 */
+        if (build_inner(data, &rec->data_len, post_avail, rec->type, t->granularity) != 0)
+            return ORC_ERR_SSL_BUFFER_TOO_SMALL;
+        rec->type = ORC_SSL_MSG_CID;
     }
     post_avail = rec->buf_len - (rec->data_len + rec->data_offset);
 
     if (post_avail < t->taglen) return ORC_ERR_SSL_BUFFER_TOO_SMALL;    /* :995-998 */
-    uint8_t nonce[12], aad[13];
+    uint8_t nonce[12], aad[23 + ORC_CID_LEN_MAX];
     build_nonce(nonce, t->iv_enc, t->fixed_ivlen, rec->ctr);             /* :1012-1019 */
     size_t aad_len = build_aad(aad, rec, t->tls_version, t->taglen);    /* :1025-1027 */
     aead_seal(t, nonce, aad, aad_len, data, rec->data_len);             /* :1043-1049 */
@@ -751,6 +803,10 @@ int orc_decrypt_buf(const orc_transform *t, orc_record *rec)
         rec->buf_len - rec->data_offset < rec->data_len) {
         return ORC_ERR_SSL_INTERNAL_ERROR;                               /* :1301-1307 */
     }
+    if (rec->cid_len != t->in_cid_len ||                                 /* :1313-1320 */
+        memcmp(rec->cid, t->in_cid, rec->cid_len) != 0) {
+        return ORC_ERR_SSL_UNEXPECTED_CID;
+    }
     uint8_t *data = rec->buf + rec->data_offset;
     const uint8_t *dyn = rec->ctr;
     if (t->ivlen != t->fixed_ivlen) {                                   /* :1352-1365 */
@@ -762,7 +818,7 @@ int orc_decrypt_buf(const orc_transform *t, orc_record *rec)
     }
     if (rec->data_len < t->taglen) return ORC_ERR_SSL_INVALID_MAC;      /* :1371-1377 */
     rec->data_len -= t->taglen;
-    uint8_t nonce[12], aad[13];
+    uint8_t nonce[12], aad[23 + ORC_CID_LEN_MAX];
     build_nonce(nonce, t->iv_dec, t->fixed_ivlen, dyn);
     size_t aad_len = build_aad(aad, rec, t->tls_version, t->taglen);
     if (aead_open(t, nonce, aad, aad_len, data, rec->data_len) != 0) {   /* :1412-1424 */
@@ -771,13 +827,10 @@ int orc_decrypt_buf(const orc_transform *t, orc_record *rec)
         return ORC_ERR_SSL_INVALID_MAC;
     }
     if (t->tls_version == ORC_VERSION_TLS1_3) {                          /* :1809-1818 */
-        size_t remaining = rec->data_len;                                /* :496-514 */
-        do {
-            if (remaining == 0) return ORC_ERR_SSL_INVALID_RECORD;
-            remaining--;
-        } while (data[remaining] == 0);
-        rec->data_len = remaining;
-        rec->type = data[remaining];
+        if (parse_inner(data, &rec->data_len, &rec->type) != 0) return ORC_ERR_SSL_INVALID_RECORD;
+    }
+    if (rec->cid_len != 0) {                                             /* :1821-1829 */
+        if (parse_inner(data, &rec->data_len, &rec->type) != 0) return ORC_ERR_SSL_INVALID_RECORD;
     }
     return 0;
 }
@@ -799,6 +852,7 @@ static void *bench_worker(void *arg)
     bench_job *j = (bench_job *) arg;
     for (uint64_t i = j->lo; i < j->hi; i++) {
         orc_record rec;
+        rec.cid_len = 0;   /* no DTLS connection ID on this path */
         uint64_t seq = j->seq0 + i;
         for (int k = 7; k >= 0; k--) { rec.ctr[k] = (uint8_t) seq; seq >>= 8; }
         rec.type = 23;   /* application data (inner type on encrypt, outer on decrypt) */

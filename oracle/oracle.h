@@ -10,7 +10,8 @@
  *       ssl_compute_padding_length        ssl_msg.c:431-435
  *       ssl_build_inner_plaintext         ssl_msg.c:466-491
  *       ssl_parse_inner_plaintext         ssl_msg.c:496-514
- *       ssl_extract_add_data_from_record  ssl_msg.c:568-735 (non-CID branch)
+ *       ssl_extract_add_data_from_record  ssl_msg.c:568-735 (incl. the RFC 9146
+ *                                         DTLS 1.2 CID branch, :667-733)
  *       ssl_transform_aead_dynamic_iv_is_explicit ssl_msg.c:739-743
  *       ssl_build_record_nonce            ssl_msg.c:768-781
  *       mbedtls_ssl_encrypt_buf (AEAD)    ssl_msg.c:784-1078
@@ -53,6 +54,9 @@ extern "C" {
 #define ORC_ERR_SSL_INVALID_RECORD     (-0x7200)
 #define ORC_ERR_SSL_INTERNAL_ERROR     (-0x6C00)
 #define ORC_ERR_SSL_FEATURE_UNAVAILABLE (-0x7080)
+#define ORC_ERR_SSL_UNEXPECTED_CID     (-0x6000)   /* ssl.h:156 */
+#define ORC_SSL_MSG_CID                25          /* MBEDTLS_SSL_MSG_CID, ssl.h:528 */
+#define ORC_CID_LEN_MAX                32          /* MBEDTLS_SSL_CID_{IN,OUT}_LEN_MAX, ssl.h:423-429 */
 
 #define ORC_VERSION_TLS1_2 0x0303
 #define ORC_VERSION_TLS1_3 0x0304
@@ -141,9 +145,12 @@ typedef struct {
     uint8_t key_enc[32], key_dec[32];
     orc_gcm_ctx gcm_enc, gcm_dec;   /* expanded GCM state (its AES context serves CCM) */
     size_t granularity;             /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY */
+    /* DTLS 1.2 connection IDs (ssl_misc.h transform in_cid / out_cid) */
+    uint8_t in_cid_len, out_cid_len;
+    uint8_t in_cid[ORC_CID_LEN_MAX], out_cid[ORC_CID_LEN_MAX];
 } orc_transform;
 
-/* Mirror of mbedtls_record (library/ssl_misc.h:1163-1188), non-CID. */
+/* Mirror of mbedtls_record (library/ssl_misc.h:1163-1188). */
 typedef struct {
     uint8_t ctr[8];
     uint8_t type;
@@ -152,6 +159,8 @@ typedef struct {
     size_t buf_len;
     size_t data_offset;
     size_t data_len;
+    uint8_t cid_len;
+    uint8_t cid[ORC_CID_LEN_MAX];
 } orc_record;
 
 /* Populate a transform as ssl_tls13_keys.c:922-1042 / ssl_tls.c:7639-7979
@@ -160,6 +169,11 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
                         const uint8_t *key_enc, const uint8_t *key_dec,
                         const uint8_t *iv_enc, const uint8_t *iv_dec,
                         size_t granularity);
+
+/* Set the transform's DTLS 1.2 connection IDs (what ssl_tls12_populate_transform
+ * copies from ssl->own_cid / handshake->peer_cid, ssl_tls.c). */
+int orc_transform_set_cid(orc_transform *t, const uint8_t *in_cid, size_t in_len,
+                          const uint8_t *out_cid, size_t out_len);
 
 int orc_encrypt_buf(const orc_transform *t, orc_record *rec);
 int orc_decrypt_buf(const orc_transform *t, orc_record *rec);

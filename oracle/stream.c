@@ -64,6 +64,7 @@ int orc_stream_decrypt(const orc_transform *t, uint8_t *buf, size_t len, const u
         }
         if (len - pos < 5 + dlen) break;                            /* incomplete record: wait */
         orc_record rec;
+        rec.cid_len = 0;   /* no DTLS connection ID on this path */
         memcpy(rec.ctr, res->in_ctr, 8);
         rec.type = type;
         rec.ver[0] = hdr[1];
@@ -143,6 +144,7 @@ int orc_stream_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, ui
         memset(tmp, 0, sizeof(tmp));
         memcpy(tmp + head, pt + off, n);
         orc_record rec;
+        rec.cid_len = 0;   /* no DTLS connection ID on this path */
         memcpy(rec.ctr, out_ctr, 8);
         rec.type = type;
         rec.ver[0] = 3;                                             /* TLS 1.3 writes 0x0303 (:2669-2674) */
