@@ -28,7 +28,7 @@
  * is transformed in place and its data_offset / data_len / type are updated
  * exactly as the reference updates them.  Only the AEAD suites are supported
  * (AES-128/192/256-GCM, AES-128/192/256-CCM and CCM_8, ChaCha20-Poly1305;
- * TLS 1.2 and 1.3, no CID).
+ * TLS 1.2 and 1.3, and DTLS 1.2 records with an RFC 9146 connection ID).
  *
  * Every entry point that touches record data runs on the GPU; there is no CPU
  * fallback.  Without a usable HIP device they return
@@ -53,6 +53,7 @@ extern "C" {
 #define TLSREC_ERR_SSL_INVALID_RECORD        (-0x7200) /* ssl.h:44 */
 #define TLSREC_ERR_SSL_HW_ACCEL_FAILED       (-0x7F80) /* ssl.h:103 */
 #define TLSREC_ERR_SSL_INTERNAL_ERROR        (-0x6C00) /* ssl.h:117 */
+#define TLSREC_ERR_SSL_UNEXPECTED_CID        (-0x6000) /* ssl.h:156 */
 
 #define TLSREC_VERSION_TLS1_2   0x0303   /* MBEDTLS_SSL_VERSION_TLS1_2 */
 #define TLSREC_VERSION_TLS1_3   0x0304   /* MBEDTLS_SSL_VERSION_TLS1_3 */
@@ -73,6 +74,8 @@ extern "C" {
 #define TLSREC_CIPHER_MAX                10
 
 #define TLSREC_MSG_APPLICATION_DATA  23      /* ssl.h:527 */
+#define TLSREC_MSG_CID               25      /* MBEDTLS_SSL_MSG_CID, ssl.h:528 */
+#define TLSREC_CID_LEN_MAX           32      /* MBEDTLS_SSL_CID_{IN,OUT}_LEN_MAX, ssl.h:423-429 */
 #define TLSREC_OUT_CONTENT_LEN       16384   /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
 #define TLSREC_PADDING_GRANULARITY   16      /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY, ssl.h:432 */
 
@@ -96,17 +99,25 @@ typedef struct tlsrec_transform {
     int32_t slot_enc;        /* device key slots (engine key table), -1 = none */
     int32_t slot_dec;
     uint32_t granularity;    /* MBEDTLS_SSL_CID_TLS1_3_PADDING_GRANULARITY (16) */
+    /* DTLS 1.2 connection IDs (ssl_misc.h transform in_cid / out_cid); set
+     * with tlsrec_transform_set_cid, zero after tlsrec_transform_setup */
+    uint8_t in_cid_len;
+    uint8_t out_cid_len;
+    unsigned char in_cid[TLSREC_CID_LEN_MAX];
+    unsigned char out_cid[TLSREC_CID_LEN_MAX];
 } tlsrec_transform;
 
-/* mbedtls_record without the CID fields. */
+/* mbedtls_record (ssl_misc.h:1163-1188). */
 typedef struct tlsrec_record {
-    uint8_t ctr[8];          /* implicit sequence number, big endian */
+    uint8_t ctr[8];          /* implicit sequence number (DTLS: epoch + seq), big endian */
     uint8_t type;            /* record content type */
     uint8_t ver[2];          /* version as on the wire */
     unsigned char *buf;      /* host buffer enclosing the record content */
     size_t buf_len;
     size_t data_offset;
     size_t data_len;
+    uint8_t cid_len;         /* connection ID of the record (0 = none) */
+    unsigned char cid[TLSREC_CID_LEN_MAX];
 } tlsrec_record;
 
 /* Populate `t` like mbedtls_ssl_tls13_populate_transform (TLS 1.3) or the
@@ -123,6 +134,14 @@ int tlsrec_transform_setup_ex(tlsrec_transform *t, int tls_version, int cipher,
                               const unsigned char *key_enc, const unsigned char *key_dec,
                               const unsigned char *iv_enc, const unsigned char *iv_dec,
                               unsigned granularity);
+/* DTLS 1.2 connection IDs of a transform: in_cid (records it decrypts must
+ * carry it, else TLSREC_ERR_SSL_UNEXPECTED_CID) and out_cid (records it
+ * encrypts get it and become DTLSInnerPlaintext of type TLSREC_MSG_CID) --
+ * what ssl_tls12_populate_transform copies from ssl->own_cid and the peer's
+ * CID (library/ssl_tls.c).  Lengths <= TLSREC_CID_LEN_MAX, 0 = none.  Also
+ * sets the CID of the transform's device key slots. */
+int tlsrec_transform_set_cid(tlsrec_transform *t, const unsigned char *in_cid, size_t in_len,
+                             const unsigned char *out_cid, size_t out_len);
 /* Release the key slots and zeroize the transform. */
 void tlsrec_transform_free(tlsrec_transform *t);
 
@@ -158,6 +177,11 @@ int tlsrec_keytab_create(tlsrec_keytab **kt, uint32_t capacity);
 int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t count,
                        const tlsrec_key_material *keys, int keys_on_device,
                        void *stream);
+/* Connection ID of slot `slot` (a transform direction: out_cid for an
+ * encrypting slot, in_cid for a decrypting one); a (re)load resets it to
+ * none.  Enqueued on `stream` and waited for. */
+int tlsrec_keytab_set_cid(tlsrec_keytab *kt, uint32_t slot, const unsigned char *cid, size_t cid_len,
+                          void *stream);
 uint32_t tlsrec_keytab_capacity(const tlsrec_keytab *kt);
 void tlsrec_keytab_free(tlsrec_keytab *kt);
 
@@ -173,7 +197,9 @@ typedef struct tlsrec_batch_rec {
     uint8_t  ctr[8];         /* sequence number, big endian */
     uint8_t  type;
     uint8_t  ver[2];
-    uint8_t  reserved[5];
+    uint8_t  cid_len;        /* decrypt: the record's connection ID length (0 = none) */
+    uint8_t  cid_off[4];     /* decrypt: its bytes at in_arena + buf_off + cid_off
+                                (little-endian u32; the DTLS header holds them) */
 } tlsrec_batch_rec;
 
 /* The fields of the record after the call, plus its status (16 bytes). */
@@ -182,7 +208,9 @@ typedef struct tlsrec_batch_res {
     uint32_t data_offset;
     uint32_t data_len;
     uint8_t  type;
-    uint8_t  reserved[3];
+    uint8_t  cid_len;        /* encrypt: rec->cid_len as the reference leaves it
+                                (the slot's CID once ssl_msg.c:874 has run) */
+    uint8_t  reserved[2];
 } tlsrec_batch_res;
 
 /* Protect / unprotect `n` records.  `recs` and `res` are device arrays; the

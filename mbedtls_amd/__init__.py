@@ -10,7 +10,8 @@ from ._abi import (CIPHER_AES_128_GCM, CIPHER_AES_256_GCM, CIPHER_CHACHA20_POLY1
                    CIPHER_AES_128_CCM_8, CIPHER_AES_192_CCM_8, CIPHER_AES_256_CCM_8, KEYLEN, TAGLEN,
                    ERR_SSL_BAD_INPUT_DATA, ERR_SSL_BUFFER_TOO_SMALL, ERR_SSL_FEATURE_UNAVAILABLE,
                    ERR_SSL_HW_ACCEL_FAILED, ERR_SSL_INTERNAL_ERROR, ERR_SSL_INVALID_MAC,
-                   ERR_SSL_INVALID_RECORD, MSG_APPLICATION_DATA, VERSION_TLS1_2, VERSION_TLS1_3,
+                   ERR_SSL_INVALID_RECORD, ERR_SSL_UNEXPECTED_CID, MSG_APPLICATION_DATA, MSG_CID,
+                   CID_LEN_MAX, VERSION_TLS1_2, VERSION_TLS1_3,
                    BATCH_REC, BATCH_RES, KEY_MATERIAL, load)
 from .batch import (KeyTable, batch_decrypt, batch_encrypt, frame_check, key_material,  # noqa: F401
                     records, results, seq_bytes)

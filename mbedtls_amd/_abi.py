@@ -23,6 +23,7 @@ ERR_SSL_INVALID_MAC = -0x7180
 ERR_SSL_INVALID_RECORD = -0x7200
 ERR_SSL_HW_ACCEL_FAILED = -0x7F80
 ERR_SSL_INTERNAL_ERROR = -0x6C00
+ERR_SSL_UNEXPECTED_CID = -0x6000
 ERR_SSL_COUNTER_WRAPPING = -0x6B80
 ERR_SSL_SESSION_TICKET_EXPIRED = -0x6D80
 MAX_IN_RECORD = 16421
@@ -39,6 +40,8 @@ CIPHER_AES_128_CCM_8, CIPHER_AES_192_CCM_8, CIPHER_AES_256_CCM_8 = 8, 9, 10
 KEYLEN = {1: 16, 2: 32, 3: 32, 4: 24, 5: 16, 6: 24, 7: 32, 8: 16, 9: 24, 10: 32}
 TAGLEN = {c: (8 if c >= 8 else 16) for c in KEYLEN}
 MSG_APPLICATION_DATA = 23
+MSG_CID = 25
+CID_LEN_MAX = 32
 ALG_SHA_256 = 0x02000009      # PSA_ALG_SHA_256
 ALG_SHA_384 = 0x0200000a      # PSA_ALG_SHA_384
 TLS13_CONTEXT_UNHASHED = 0
@@ -50,9 +53,9 @@ KEY_MATERIAL = np.dtype([("cipher", "u1"), ("tls_minor", "u1"), ("fixed_ivlen", 
                          ("iv", "u1", 16), ("key", "u1", 32)])
 BATCH_REC = np.dtype([("buf_off", "<u8"), ("buf_len", "<u4"), ("data_offset", "<u4"),
                       ("data_len", "<u4"), ("slot", "<u4"), ("ctr", "u1", 8), ("type", "u1"),
-                      ("ver", "u1", 2), ("reserved", "u1", 5)])
+                      ("ver", "u1", 2), ("cid_len", "u1"), ("cid_off", "<u4")], align=False)
 BATCH_RES = np.dtype([("status", "<i4"), ("data_offset", "<u4"), ("data_len", "<u4"),
-                      ("type", "u1"), ("reserved", "u1", 3)])
+                      ("type", "u1"), ("cid_len", "u1"), ("reserved", "u1", 2)])
 STREAM_IN = np.dtype([("off", "<u8"), ("len", "<u4"), ("slot", "<u4"), ("in_ctr", "u1", 8),
                       ("nb_zero", "u1"), ("reserved", "u1", 7)])
 STREAM_IN_RES = np.dtype([("status", "<i4"), ("first", "<u4"), ("nrec", "<u4"), ("consumed", "<u4"),
@@ -80,7 +83,9 @@ class CTransform(ctypes.Structure):
                 ("cipher", ctypes.c_int), ("keylen", ctypes.c_size_t),
                 ("key_enc", ctypes.c_ubyte * 32), ("key_dec", ctypes.c_ubyte * 32),
                 ("slot_enc", ctypes.c_int32), ("slot_dec", ctypes.c_int32),
-                ("granularity", ctypes.c_uint32)]
+                ("granularity", ctypes.c_uint32), ("in_cid_len", ctypes.c_uint8),
+                ("out_cid_len", ctypes.c_uint8), ("in_cid", ctypes.c_ubyte * 32),
+                ("out_cid", ctypes.c_ubyte * 32)]
 
 
 class CKeySet(ctypes.Structure):
@@ -98,7 +103,8 @@ class CTicketKeys(ctypes.Structure):
 class CRecord(ctypes.Structure):
     _fields_ = [("ctr", ctypes.c_ubyte * 8), ("type", ctypes.c_ubyte), ("ver", ctypes.c_ubyte * 2),
                 ("buf", ctypes.c_void_p), ("buf_len", ctypes.c_size_t),
-                ("data_offset", ctypes.c_size_t), ("data_len", ctypes.c_size_t)]
+                ("data_offset", ctypes.c_size_t), ("data_len", ctypes.c_size_t),
+                ("cid_len", ctypes.c_ubyte), ("cid", ctypes.c_ubyte * 32)]
 
 
 # every function include/tlsrec.h declares, with its signature
@@ -107,6 +113,8 @@ SIGNATURES = {
     "tlsrec_transform_setup": (_INT, [_VP, _INT, _INT, _VP, _VP, _VP, _VP]),
     "tlsrec_transform_setup_ex": (_INT, [_VP, _INT, _INT, _VP, _VP, _VP, _VP, ctypes.c_uint]),
     "tlsrec_transform_free": (None, [_VP]),
+    "tlsrec_transform_set_cid": (_INT, [_VP, _VP, _SZ, _VP, _SZ]),
+    "tlsrec_keytab_set_cid": (_INT, [_VP, _U32, _VP, _SZ, _VP]),
     "tlsrec_encrypt_buf": (_INT, [_VP, _VP, _VP]),
     "tlsrec_decrypt_buf": (_INT, [_VP, _VP, _VP]),
     "tlsrec_keytab_create": (_INT, [ctypes.POINTER(_VP), _U32]),
@@ -152,7 +160,10 @@ def load():
         raise ImportError(f"{path} is missing: build it with `python -m mbedtls_amd.build` "
                           "(there is no CPU fallback)")
     L = ctypes.CDLL(path)
+    alt = path != LIB_PATH
     for name, (res, args) in SIGNATURES.items():
+        if alt and not hasattr(L, name):
+            continue          # an older A/B build may predate an entry point
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

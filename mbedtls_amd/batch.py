@@ -78,6 +78,12 @@ class KeyTable:
         if r != 0:
             raise RuntimeError(f"tlsrec_keytab_load failed: {r:#x}")
 
+    def set_cid(self, slot: int, cid: bytes, stream=None):
+        """DTLS 1.2 connection ID of one slot (tlsrec_keytab_set_cid)."""
+        r = self._lib.tlsrec_keytab_set_cid(self.handle, slot, bytes(cid), len(cid), _stream(stream))
+        if r != 0:
+            raise RuntimeError(f"tlsrec_keytab_set_cid failed: {r:#x}")
+
     def close(self):
         if self.handle is not None:
             self._lib.tlsrec_keytab_free(self.handle)

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
         const tlsrec_key_material km = a.slots[s].km;
         const tlsrec_batch_rec d = a.recs[my_rec];
         tlsrec_plan p;
-        make_plan<DEC>(p, d, km);
+        make_plan<DEC>(p, d, km, &a.slots[s], a.in);
         if (p.status != 0) {
             finish_early(p, d, a.out, &a.res[my_rec]);
             continue;
@@ -100,7 +100,8 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
                                      make_uint4(m0 | flags, m1, m2,
                                                 m3 | w4(0, (aead_len >> 16) & 0xff, (aead_len >> 8) & 0xff,
                                                         aead_len & 0xff)));
-        /* A1 = len16(aad) || aad || zeros (the record AAD is 5 or 13 bytes) */
+        /* A1 = len16(aad) || aad || zeros (the record AAD is 5 or 13 bytes;
+         * with a DTLS 1.2 CID 23..55, continued below) */
         {
             uint8_t ab[16];
 #pragma unroll
@@ -108,11 +109,17 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             ab[0] = 0;
             ab[1] = p.aad_len;
 #pragma unroll
-            for (int i = 0; i < 13; i++)
+            for (int i = 0; i < 14; i++)
                 if (i < (int) p.aad_len) ab[2 + i] = p.aad[i];
             const uint4 a1 = make_uint4(w4(ab[0], ab[1], ab[2], ab[3]), w4(ab[4], ab[5], ab[6], ab[7]),
                                         w4(ab[8], ab[9], ab[10], ab[11]), w4(ab[12], ab[13], ab[14], ab[15]));
             x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, a1));
+            if (p.aad_len > 14) {   /* DTLS 1.2 + CID: 23..55 AAD bytes after len16 */
+                const uint8_t *cid = a.slots[s].cid;
+                x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<1, 2>(p, d, cid)));
+                if (p.aad_len > 30) x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<2, 2>(p, d, cid)));
+                if (p.aad_len > 46) x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<3, 2>(p, d, cid)));
+            }
         }
         /* counter blocks: 2 || N || i24 */
         const uint32_t c0 = m0 | 2u;
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
                 const uint4 ks = aes_encrypt<NR, 0>(lds, lanebase, rk, cb);
                 const uint4 pt = mask_block(xor4(in, ks), pos, aead_len);
                 store_block(dst, pos, aead_len, pt, true);
-                if (p.tls13 && (pt.x | pt.y | pt.z | pt.w)) nzpos = pos + 1;
+                if (p.inner && (pt.x | pt.y | pt.z | pt.w)) nzpos = pos + 1;
                 x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, pt));
             } else {
                 /* MAC and keystream are independent: two AES chains interleave */
@@ -141,7 +148,8 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
         const uint4 s0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(c0, m1, m2, m3));
         const uint4 tag = xor4(x, s0);
         tlsrec_batch_res r;
-        r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+        r.cid_len = 0;
+        r.reserved[0] = r.reserved[1] = 0;
         if (!DEC) {
             store_block(dst, aead_len, aead_len + taglen, tag, false);
             if (p.explicit_iv && p.post_status == 0) {
@@ -152,6 +160,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             r.data_offset = p.data_offset;
             r.data_len = p.data_len;
             r.type = p.type;
+            r.cid_len = p.cid_set ? p.cid_len : 0;
         } else {
             const uint4 want = load_block(src, aead_len, aead_len + taglen, aead_len + taglen, 0, false);
             const uint4 got = mask_block(tag, 0, taglen);
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
                 /* PSA wipes the whole output buffer on a bad tag */
                 zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, 0, 1);
                 r.status = TLSREC_E_INVALID_MAC;
-            } else if (p.tls13) {                              /* ssl_msg.c:1809-1818 */
+            } else if (p.inner) {                              /* ssl_msg.c:1809-1829 */
                 const uint32_t key = nzpos ? last_nonzero_key(load_block(dst, nzpos - 1, aead_len, aead_len, 0, false),
                                                               nzpos - 1)
                                            : 0u;

@@ -78,6 +78,22 @@ extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
 
 extern "C" uint32_t tlsrec_keytab_capacity(const tlsrec_keytab *kt) { return kt ? kt->capacity : 0; }
 
+extern "C" int tlsrec_keytab_set_cid(tlsrec_keytab *kt, uint32_t slot, const unsigned char *cid, size_t cid_len,
+                                     void *stream)
+{
+    if (kt == NULL || slot >= kt->capacity || cid_len > TLSREC_CID_LEN_MAX || (cid_len && cid == NULL))
+        return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    uint8_t v[1 + TLSREC_CID_LEN_MAX];
+    memset(v, 0, sizeof(v));
+    v[0] = (uint8_t) cid_len;
+    if (cid_len) memcpy(v + 1, cid, cid_len);
+    static_assert(offsetof(SlotState, cid) == offsetof(SlotState, cid_len) + 1, "SlotState CID layout");
+    hipStream_t st = (hipStream_t) stream;
+    hipError_t e = hipMemcpyAsync(&kt->d_slots[slot].cid_len, v, sizeof(v), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+}
+
 extern "C" void tlsrec_keytab_free(tlsrec_keytab *kt)
 {
     if (!kt) return;
@@ -415,17 +431,29 @@ extern "C" void tlsrec__engine_slot_free(int slot)
     pthread_mutex_unlock(&g_mu);
 }
 
-/* Run one record through the batch kernels: host buffer -> device -> host. */
+extern "C" int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, size_t cid_len)
+{
+    if (slot < 0 || slot >= TLSREC_ENGINE_SLOTS) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    pthread_mutex_lock(&g_mu);
+    int r = g_kt && g_used[slot] ? tlsrec_keytab_set_cid(g_kt, (uint32_t) slot, cid, cid_len, g_stream)
+                                 : TLSREC_ERR_SSL_INTERNAL_ERROR;
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}
+
+/* Run one record through the batch kernels: host buffer -> device -> host.
+ * A decrypted record's CID (cid_len bytes) is staged right after the buffer
+ * (rec->cid_off = buf_len). */
 extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
-                                  tlsrec_batch_res *out)
+                                  const unsigned char *cid, tlsrec_batch_res *out)
 {
     pthread_mutex_lock(&g_mu);
     int r = engine_init_locked();
-    if (r == 0 && g_dbuf_len < buf_len + 16) {
+    if (r == 0 && g_dbuf_len < buf_len + 16 + TLSREC_CID_LEN_MAX) {
         hipFree(g_dbuf);
         g_dbuf = NULL;
         g_dbuf_len = 0;
-        size_t want = buf_len + 16 > 65536 ? buf_len + 16 : 65536;
+        size_t want = buf_len + 16 + TLSREC_CID_LEN_MAX > 65536 ? buf_len + 16 + TLSREC_CID_LEN_MAX : 65536;
         if (hipMalloc((void **) &g_dbuf, want) != hipSuccess) r = TLSREC_ERR_SSL_ALLOC_FAILED;
         else g_dbuf_len = want;
     }
@@ -436,6 +464,12 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
         tlsrec_batch_res *d_res = (tlsrec_batch_res *) ((uint8_t *) g_dmeta + 48);
         hipError_t e = hipSuccess;
         if (buf_len) e = hipMemcpyAsync(g_dbuf, buf, buf_len, hipMemcpyHostToDevice, g_stream);
+        if (e == hipSuccess && d.cid_len) {
+            e = hipMemcpyAsync(g_dbuf + buf_len, cid, d.cid_len, hipMemcpyHostToDevice, g_stream);
+            const uint32_t off = (uint32_t) buf_len;
+            d.cid_off[0] = (uint8_t) off; d.cid_off[1] = (uint8_t) (off >> 8);
+            d.cid_off[2] = (uint8_t) (off >> 16); d.cid_off[3] = (uint8_t) (off >> 24);
+        }
         if (e == hipSuccess) e = hipMemcpyAsync(d_rec, &d, sizeof(d), hipMemcpyHostToDevice, g_stream);
         if (e == hipSuccess) {
             r = batch(g_kt, d_rec, d_res, 1, g_dbuf, g_dbuf, 0, g_stream, dec);

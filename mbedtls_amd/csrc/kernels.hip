@@ -98,6 +98,7 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     if (tid == 0) {
         st->km = km;
         st->nr = 0;
+        st->cid_len = 0;          /* a (re)load leaves the slot without a CID */
         if (aes) {
             const int nk = (int) tlsrec_cipher_keylen(km.cipher) / 4;
             aes_key_expand(km.key, nk, st->rk);
@@ -166,7 +167,7 @@ struct GcmLds {
 /* Per-record state that the AEAD loop reads (kept small: it lives in
  * VGPRs across the loop). */
 struct GcmJob {
-    bool run, aligned, tls13;
+    bool run, aligned, inner;   /* inner: TLS 1.3 / DTLS 1.2 + CID inner plaintext */
     uint8_t inner_type;
     uint32_t aead_len, content_len, aad_len;
     uint32_t nw0, nw1, nw2;
@@ -186,7 +187,7 @@ struct GcmJob {
         aead_len = p.aead_len;
         content_len = DEC ? p.aead_len : p.content_len;
         inner_type = p.inner_type;
-        tls13 = p.tls13;
+        inner = p.inner;
         src = in + d.buf_off + p.aead_pos;
         dst = out + d.buf_off + p.aead_pos;
         /* 16-byte global accesses need no 16-byte alignment on gfx950: the
@@ -199,6 +200,18 @@ struct GcmJob {
         run = true;
     }
 };
+
+/* GHASH Horner over blocks 0..3 of a CID record's AAD (block 0 = a0), leaving
+ * the last block un-multiplied (the kernel's AAD fold applies that H).  Out
+ * of line: CID records are rare, the record kernel's registers are not. */
+__device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, const tlsrec_plan &p,
+                                               const tlsrec_batch_rec &d, const uint8_t *cid)
+{
+    uint4 f = xor4(gmul<0>(gp, a0), cid_aad_block<1, 0>(p, d, cid));
+    if (p.aad_len > 32) f = xor4(gmul<0>(gp, f), cid_aad_block<2, 0>(p, d, cid));
+    if (p.aad_len > 48) f = xor4(gmul<0>(gp, f), cid_aad_block<3, 0>(p, d, cid));
+    return f;
+}
 
 /* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0 */
 template <int SH>
@@ -302,7 +315,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             if (mine) {
                 const tlsrec_batch_rec d = a.recs[my_rec];
                 tlsrec_plan p;
-                make_plan<DEC>(p, d, km);
+                make_plan<DEC>(p, d, km, &a.slots[s], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
             }
             ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
@@ -329,11 +342,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             if (active) {
                 const tlsrec_batch_rec d = a.recs[ridx];
                 tlsrec_plan p;
-                make_plan<DEC>(p, d, km);
+                make_plan<DEC>(p, d, km, &a.slots[s], a.in);
                 if (p.status != 0) {
                     if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
                 } else {
                     jb.setup<DEC>(p, d, a.in, a.out);
+                    /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
+                     * into the block the AAD fold multiplies by H below */
+                    if (p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
                 }
             }
             const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
@@ -400,13 +416,13 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                             const uint4 o = xor4(blk, ks);
                             gstore16(jb.dst + pos, o);
                             X = DEC ? blk : o;
-                            if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                         } else if (valid) {
                             blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type, jb.aligned);
                             const uint4 o = mask_block(xor4(blk, ks), pos, jb.aead_len);
                             store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
                             X = DEC ? blk : o;
-                            if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                         }
                         if (live && cc == 0) X = xor4(X, *fold);
                         if (live) { Z = Zn; Xp = X; }
@@ -426,7 +442,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                             crypt(cc, xor4(Z, Xp), ks, Zn);
                             const uint4 o = xor4(blk, ks);
                             gstore16(dp + 16 * L * b, o);
-                            if (DEC && jb.tls13 && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
                             Z = Zn;
                             Xp = DEC ? blk : o;
                         }
@@ -443,7 +459,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 steps(std::integral_constant<bool, false>());
             uint4 Y = xor4(Z, Xp);
             uint32_t nzkey = 0;
-            if (DEC && jb.tls13 && nzpos) {
+            if (DEC && jb.inner && nzpos) {
                 /* the lane's last non-zero plaintext block, as written above */
                 const uint32_t pos = nzpos - 1;
                 nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
@@ -458,7 +474,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint4 tag = xor4(Y, ej0);
             const tlsrec_batch_rec d = a.recs[ridx];
             tlsrec_plan p;
-            make_plan<DEC>(p, d, km);
+            make_plan<DEC>(p, d, km, &a.slots[s], a.in);
             if (!DEC) {
                 if (q == 0) {
                     store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
@@ -471,7 +487,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                     r.data_offset = p.data_offset;
                     r.data_len = p.data_len;
                     r.type = p.type;
-                    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+                    r.cid_len = p.cid_set ? p.cid_len : 0;
+                    r.reserved[0] = r.reserved[1] = 0;
                     a.res[ridx] = r;
                 }
             } else {
@@ -483,12 +500,13 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 r.data_offset = p.data_offset;
                 r.data_len = p.data_len;
                 r.type = d.type;
-                r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+                r.cid_len = 0;
+                r.reserved[0] = r.reserved[1] = 0;
                 if (diff != 0) {
                     /* PSA wipes the whole output buffer on a bad tag */
                     zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
                     r.status = TLSREC_E_INVALID_MAC;
-                } else if (p.tls13) {                                /* ssl_msg.c:1809-1818 */
+                } else if (p.inner) {                                /* ssl_msg.c:1809-1829 */
                     if (key == 0) {
                         r.status = TLSREC_E_INVALID_RECORD;
                     } else {
@@ -697,7 +715,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
                 mine = true;
                 const tlsrec_key_material km = a.slots[d.slot].km;
                 tlsrec_plan p;
-                make_plan<DEC>(p, d, km);
+                make_plan<DEC>(p, d, km, &a.slots[d.slot], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
                 for (int i = 0; i < 8; i++) key[i] = ld_u32le(km.key + 4 * i);
             }
@@ -733,7 +751,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         if (active) {
             d = a.recs[ridx];
             const tlsrec_key_material km = a.slots[d.slot].km;
-            make_plan<DEC>(p, d, km);
+            make_plan<DEC>(p, d, km, &a.slots[d.slot], a.in);
             if (p.status != 0) {
                 if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
             } else {
@@ -747,20 +765,27 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         const uint32_t z = (L - B % L) % L;
         const uint32_t J = run ? (B + z) / L : 0;
         const uint32_t Jmax = wave_max(J);
-        uint4 aadw = make_uint4(0, 0, 0, 0);
+        P5 aadp = p_zero();   /* AAD blocks Horner-folded: A_1 r^(a-1) + ... + A_a */
         const uint8_t *src = a.in;
         uint8_t *dst = a.out;
         bool aligned = false;
         uint32_t content_len = 0;
         if (run) {
-            aadw = aad_words(p);
+            aadp = p_from_words(aad_words(p));
+            if (p.aad_len > 16) {   /* DTLS 1.2 + CID: 2..4 AAD blocks */
+                const uint8_t *cid = a.slots[d.slot].cid;
+                const P5 r1 = p_lds(cr.r1);
+                aadp = p_add(p_mul(aadp, r1), p_from_words(cid_aad_block<1, 0>(p, d, cid)));
+                if (p.aad_len > 32) aadp = p_add(p_mul(aadp, r1), p_from_words(cid_aad_block<2, 0>(p, d, cid)));
+                if (p.aad_len > 48) aadp = p_add(p_mul(aadp, r1), p_from_words(cid_aad_block<3, 0>(p, d, cid)));
+            }
             src = a.in + d.buf_off + p.aead_pos;
             dst = a.out + d.buf_off + p.aead_pos;
             aligned = true;   /* any byte offset: see GcmJob::setup */
             content_len = DEC ? aead_len : p.content_len;
         }
         const uint8_t inner_type = run ? p.inner_type : 0;
-        const bool tls13 = run && p.tls13;
+        const bool tls13 = run && p.inner;   /* TLS 1.3 or DTLS 1.2 + CID inner plaintext */
         /* a readable 16-byte address for lanes with nothing to load */
         const uint8_t *safe = run ? src : reinterpret_cast<const uint8_t *>(a.recs);
 
@@ -809,7 +834,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
             const P5 r1 = p_lds(cr.r1);
             const uint32_t vv = (valid && (uint32_t) b == B - 1) ? v : 4;
             P5 x = p_from_words(ct[0]);
-            if (b == 0) x = p_add(x, p_mul(p_from_words(aadw), r1));
+            if (b == 0) x = p_add(x, p_mul(aadp, r1));
 #pragma unroll
             for (int t = 1; t < 4; t++) {
                 P5 y = p_add(p_mul(x, r1), p_from_words(ct[t]));
@@ -894,7 +919,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         }
         for (; j < Jmax; j++) general(j);
 
-        if (run && B == 0 && q == L - 1) vf = p_from_words(aadw);
+        if (run && B == 0 && q == L - 1) vf = aadp;
         /* rotated tree: logical ql = (q+1) % L, anchored at chunk B-2;
          * level i combines with r^(4 * 2^i) */
         const P5 r1 = p_lds(cr.r1), r2 = p_lds(cr.r2);
@@ -932,7 +957,8 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
                 r.data_offset = p.data_offset;
                 r.data_len = p.data_len;
                 r.type = p.type;
-                r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+                r.cid_len = p.cid_set ? p.cid_len : 0;
+                r.reserved[0] = r.reserved[1] = 0;
                 a.res[ridx] = r;
             }
         } else {
@@ -949,11 +975,12 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
             r.data_offset = p.data_offset;
             r.data_len = p.data_len;
             r.type = d.type;
-            r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+            r.cid_len = 0;
+            r.reserved[0] = r.reserved[1] = 0;
             if (diff != 0) {
                 zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
                 r.status = TLSREC_E_INVALID_MAC;
-            } else if (p.tls13) {
+            } else if (p.inner) {
                 if (key2 == 0) {
                     r.status = TLSREC_E_INVALID_RECORD;
                 } else {

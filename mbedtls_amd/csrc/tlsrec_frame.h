@@ -10,7 +10,9 @@
  *   TLS 1.3 inner plaintext     ssl_msg.c:853-868 with :431-435, :466-491
  *   tag room                    ssl_msg.c:995-998
  *   nonce                       ssl_msg.c:768-781, :1012-1019, :1383-1388
- *   additional data             ssl_msg.c:568-735 (non-CID)
+ *   additional data             ssl_msg.c:568-735 (incl. the DTLS 1.2 CID
+ *                               branch of RFC 9146, :683-724)
+ *   DTLS 1.2 + CID              ssl_msg.c:874-897 (enc), :1313-1320 (dec)
  *   explicit IV (TLS 1.2 GCM)   ssl_msg.c:1066-1075 (enc), :1352-1365 (dec)
  *   short-record checks         ssl_msg.c:1356-1377
  *
@@ -26,8 +28,12 @@
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define TLSREC_HD __host__ __device__ static inline
+/* rare paths (DTLS connection IDs) kept out of the record kernels' register
+ * allocation */
+#define TLSREC_HD_COLD __host__ __device__ static __attribute__((noinline))
 #else
 #define TLSREC_HD static inline
+#define TLSREC_HD_COLD static
 #endif
 
 #define TLSREC_E_BAD_INPUT_DATA   (-135)
@@ -35,6 +41,8 @@
 #define TLSREC_E_INVALID_MAC      (-0x7180)
 #define TLSREC_E_INVALID_RECORD   (-0x7200)
 #define TLSREC_E_INTERNAL_ERROR   (-0x6C00)
+#define TLSREC_E_UNEXPECTED_CID   (-0x6000)
+#define TLSREC_MSG_CID_TYPE       25           /* MBEDTLS_SSL_MSG_CID, ssl.h:528 */
 
 /* Cipher properties (mbedtls_ssl_cipher_to_psa, ssl_tls.c:2168-2363; the
  * _CCM_8 ids are the short-tag suites).  Ids: include/tlsrec.h. */
@@ -62,7 +70,7 @@ typedef struct tlsrec_plan {
     uint8_t  type;            /* rec->type when the call returns (enc) */
     uint8_t  tls13;
     uint8_t  explicit_iv;     /* TLS 1.2 GCM: 8-byte nonce travels in the record */
-    uint8_t  aad_len;         /* 5 (TLS 1.3) or 13 (TLS 1.2) */
+    uint8_t  aad_len;         /* 5 (TLS 1.3), 13 (TLS 1.2) or 23 + cid_len (CID) */
     uint32_t aead_pos;        /* buffer offset of the AEAD input/output */
     uint32_t aead_len;        /* AEAD plaintext length (ciphertext w/o tag) */
     uint32_t content_len;     /* encrypt: bytes taken from the buffer; the
@@ -72,9 +80,13 @@ typedef struct tlsrec_plan {
     uint8_t  side_type;       /* early error still wrote the type byte ... */
     uint16_t side_zeros;      /* ... and this many zero pad bytes after it */
     uint32_t side_pos;        /* at this buffer offset */
-    uint8_t  aad[16];
+    uint8_t  aad[16];         /* first 16 bytes of the AAD (all of it unless CID) */
     uint8_t  nonce[12];       /* decrypt + explicit_iv: bytes 4..11 come from
                                  the record (buffer offset data_offset) */
+    uint8_t  inner;           /* AEAD plaintext is a (D)TLSInnerPlaintext:
+                                 TLS 1.3, or DTLS 1.2 with a CID */
+    uint8_t  cid_len;         /* CID in the AAD (0 = none) */
+    uint8_t  cid_set;         /* encrypt: the reference has set rec->cid (:874) */
 } tlsrec_plan;
 
 /* Key-slot parameters the plan needs (from the transform / key material). */
@@ -83,6 +95,8 @@ typedef struct tlsrec_plan_key {
     uint32_t fixed_ivlen;     /* 12 or 4 */
     uint32_t taglen;          /* 16, or 8 for the CCM_8 suites */
     const uint8_t *iv;        /* fixed IV (iv_enc for encrypt, iv_dec for decrypt) */
+    uint32_t cid_len;         /* DTLS 1.2 CID: out_cid (encrypt) / in_cid (decrypt) */
+    const uint8_t *cid;
 } tlsrec_plan_key;
 
 TLSREC_HD void tlsrec__nonce(uint8_t nonce[12], const uint8_t *fixed, uint32_t fixed_len,
@@ -93,14 +107,49 @@ TLSREC_HD void tlsrec__nonce(uint8_t nonce[12], const uint8_t *fixed, uint32_t f
     for (int i = 0; i < 8; i++) nonce[4 + i] ^= dyn[i];
 }
 
-TLSREC_HD uint8_t tlsrec__aad(uint8_t aad[16], int tls13, const uint8_t ctr[8], uint8_t type,
-                              const uint8_t ver[2], uint32_t len_field)
+/* Byte k of the RFC 9146 AAD of a DTLS 1.2 record with a CID
+ * (ssl_extract_add_data_from_record, ssl_msg.c:683-724):
+ *   0xff x 8 || type || cid_len || type || ver || epoch+seq || cid || len16 */
+TLSREC_HD uint8_t tlsrec_cid_aad_byte(uint32_t k, uint8_t type, const uint8_t ver[2], const uint8_t ctr[8],
+                                      const uint8_t *cid, uint32_t cid_len, uint32_t len_field)
 {
-    /* ssl_extract_add_data_from_record (ssl_msg.c:568-735), non-CID:
+    if (k < 8) return 0xff;                          /* seq_num_placeholder */
+    if (k == 8 || k == 10) return type;              /* tls12_cid, type */
+    if (k == 9) return (uint8_t) cid_len;
+    if (k == 11 || k == 12) return ver[k - 11];
+    if (k < 21) return ctr[k - 13];
+    if (k < 21 + cid_len) return cid[k - 21];
+    if (k == 21 + cid_len) return (uint8_t) (len_field >> 8);
+    if (k == 22 + cid_len) return (uint8_t) len_field;
+    return 0;
+}
+
+/* aad[0..15] of a CID record; returns the AAD length */
+TLSREC_HD_COLD uint8_t tlsrec__cid_aad_head(uint8_t aad[16], const uint8_t ctr[8], uint8_t type, const uint8_t ver[2],
+                                           uint32_t len_field, const uint8_t *cid, uint32_t cid_len)
+{
+    for (uint32_t i = 0; i < 16; i++) aad[i] = tlsrec_cid_aad_byte(i, type, ver, ctr, cid, cid_len, len_field);
+    return (uint8_t) (23 + cid_len);
+}
+
+/* rec->cid == transform->in_cid (ssl_msg.c:1317-1318) */
+TLSREC_HD_COLD int tlsrec__cid_equal(const uint8_t *a, const uint8_t *b, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; i++)
+        if (a[i] != b[i]) return 0;
+    return 1;
+}
+
+TLSREC_HD uint8_t tlsrec__aad(uint8_t aad[16], int tls13, const uint8_t ctr[8], uint8_t type,
+                              const uint8_t ver[2], uint32_t len_field, const uint8_t *cid, uint32_t cid_len)
+{
+    /* ssl_extract_add_data_from_record (ssl_msg.c:568-735):
      * TLS 1.3: type || ver || len(TLSCiphertext)        (:671-677, :727-731)
-     * TLS 1.2: seq  || type || ver || len(plaintext)    (:700-703, :727-731) */
+     * TLS 1.2: seq  || type || ver || len(plaintext)    (:700-703, :727-731)
+     * DTLS 1.2 + CID: tlsrec_cid_aad_byte; aad[] keeps its first 16 bytes */
     uint8_t n = 0;
     for (int i = 0; i < 16; i++) aad[i] = 0;
+    if (!tls13 && cid_len != 0) return tlsrec__cid_aad_head(aad, ctr, type, ver, len_field, cid, cid_len);
     if (!tls13) {
         for (int i = 0; i < 8; i++) aad[n++] = ctr[i];
     }
@@ -134,6 +183,9 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     p->side_type = 0;
     p->side_zeros = 0;
     p->side_pos = 0;
+    p->inner = (uint8_t) k->tls13;
+    p->cid_len = 0;
+    p->cid_set = 0;
 
     if (buf_len < data_offset || buf_len - data_offset < data_len) {    /* :814-823 */
         p->status = TLSREC_E_INTERNAL_ERROR;
@@ -145,7 +197,14 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     }
     uint64_t post_avail = buf_len - (data_len + data_offset);
     uint64_t len = data_len;
-    if (k->tls13) {                                                    /* :853-868 */
+    /* (D)TLSInnerPlaintext: TLS 1.3 (:853-868), or DTLS 1.2 with a CID
+     * (:874-897; a TLS 1.3 transform carries no CID) */
+    const int cid = !k->tls13 && k->cid_len != 0;
+    if (cid) {
+        p->cid_len = (uint8_t) k->cid_len;
+        p->cid_set = 1;                                                /* :874-875 */
+    }
+    if (k->tls13 || cid) {
         uint32_t g = granularity ? granularity : 16;
         uint64_t pad = (g - (data_len + 1) % g) % g;                   /* :431-435 */
         if (post_avail == 0) {                                         /* :473-475 */
@@ -161,7 +220,8 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
         }
         len = data_len + 1 + pad;
         p->data_len = (uint32_t) len;
-        p->type = 23;                                                  /* :867 */
+        p->type = cid ? TLSREC_MSG_CID_TYPE : 23;                      /* :867, :896 */
+        p->inner = 1;
         post_avail = buf_len - (len + data_offset);
         if (post_avail < k->taglen) {                                  /* :995-998 */
             /* inner plaintext was built in the buffer before this check */
@@ -177,7 +237,7 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     }
     tlsrec__nonce(p->nonce, k->iv, k->fixed_ivlen, ctr);               /* :1012-1019 */
     p->aad_len = tlsrec__aad(p->aad, k->tls13, ctr, p->type, ver,
-                             (uint32_t) (k->tls13 ? len + k->taglen : len));
+                             (uint32_t) (k->tls13 ? len + k->taglen : len), k->cid, p->cid_len);
     p->aead_len = (uint32_t) len;
     p->data_len = (uint32_t) (len + k->taglen);                        /* psa_aead_encrypt output */
     if (p->explicit_iv) {                                              /* :1066-1075 */
@@ -190,10 +250,12 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     }
 }
 
-/* mbedtls_ssl_decrypt_buf, AEAD mode (up to, not including, the AEAD call). */
+/* mbedtls_ssl_decrypt_buf, AEAD mode (up to, not including, the AEAD call).
+ * rec_cid / rec_cid_len: the record's connection ID (rec->cid). */
 TLSREC_HD void tlsrec_plan_decrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
                                    const uint8_t ctr[8], uint8_t type, const uint8_t ver[2],
-                                   uint64_t buf_len, uint64_t data_offset, uint64_t data_len)
+                                   uint64_t buf_len, uint64_t data_offset, uint64_t data_len,
+                                   const uint8_t *rec_cid, uint32_t rec_cid_len)
 {
     p->status = 0;
     p->post_status = 0;
@@ -210,9 +272,18 @@ TLSREC_HD void tlsrec_plan_decrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     p->side_type = 0;
     p->side_zeros = 0;
     p->side_pos = 0;
+    p->cid_set = 0;
+    p->cid_len = (uint8_t) rec_cid_len;
+    /* TLS 1.3 and DTLS 1.2 + CID end with ssl_parse_inner_plaintext (:1809-1829) */
+    p->inner = (uint8_t) (k->tls13 || rec_cid_len != 0);
 
     if (buf_len < data_offset || buf_len - data_offset < data_len) {    /* :1301-1307 */
         p->status = TLSREC_E_INTERNAL_ERROR;
+        return;
+    }
+    if (rec_cid_len != k->cid_len ||                                   /* :1313-1320 */
+        (rec_cid_len != 0 && !tlsrec__cid_equal(rec_cid, k->cid, rec_cid_len))) {
+        p->status = TLSREC_E_UNEXPECTED_CID;
         return;
     }
     uint64_t off = data_offset, len = data_len;
@@ -237,7 +308,7 @@ TLSREC_HD void tlsrec_plan_decrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     /* the dynamic part is rec->ctr, or the explicit IV read from the record */
     tlsrec__nonce(p->nonce, k->iv, k->fixed_ivlen, ctr);
     p->aad_len = tlsrec__aad(p->aad, k->tls13, ctr, type, ver,
-                             (uint32_t) (k->tls13 ? len + k->taglen : len));
+                             (uint32_t) (k->tls13 ? len + k->taglen : len), rec_cid, rec_cid_len);
 }
 
 #endif /* TLSREC_FRAME_H */

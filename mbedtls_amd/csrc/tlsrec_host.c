@@ -19,7 +19,8 @@
 int tlsrec__engine_slot_alloc(const tlsrec_key_material *km);
 void tlsrec__engine_slot_free(int slot);
 int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
-                       tlsrec_batch_res *out);
+                       const unsigned char *cid, tlsrec_batch_res *out);
+int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, size_t cid_len);
 
 static void zeroize(void *p, size_t n)
 {
@@ -96,6 +97,27 @@ int tlsrec_transform_setup_ex(tlsrec_transform *t, int tls_version, int cipher,
     return 0;
 }
 
+/* transform->in_cid / out_cid (ssl_tls12_populate_transform, library/ssl_tls.c);
+ * the encrypt slot gets out_cid, the decrypt slot in_cid */
+int tlsrec_transform_set_cid(tlsrec_transform *t, const unsigned char *in_cid, size_t in_len,
+                             const unsigned char *out_cid, size_t out_len)
+{
+    if (t == NULL || in_len > TLSREC_CID_LEN_MAX || out_len > TLSREC_CID_LEN_MAX ||
+        (in_len && in_cid == NULL) || (out_len && out_cid == NULL))
+        return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (t->slot_enc < 0 || t->slot_dec < 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    int r = tlsrec__engine_slot_set_cid(t->slot_enc, out_cid, out_len);
+    if (r == 0) r = tlsrec__engine_slot_set_cid(t->slot_dec, in_cid, in_len);
+    if (r != 0) return r;
+    memset(t->in_cid, 0, sizeof(t->in_cid));
+    memset(t->out_cid, 0, sizeof(t->out_cid));
+    if (in_len) memcpy(t->in_cid, in_cid, in_len);
+    if (out_len) memcpy(t->out_cid, out_cid, out_len);
+    t->in_cid_len = (uint8_t) in_len;
+    t->out_cid_len = (uint8_t) out_len;
+    return 0;
+}
+
 void tlsrec_transform_free(tlsrec_transform *t)
 {
     if (t == NULL) return;
@@ -112,6 +134,8 @@ static tlsrec_plan_key pkey(const tlsrec_transform *t, int dec)
     k.fixed_ivlen = (uint32_t) t->fixed_ivlen;
     k.taglen = (uint32_t) t->taglen;
     k.iv = dec ? t->iv_dec : t->iv_enc;
+    k.cid_len = dec ? t->in_cid_len : t->out_cid_len;
+    k.cid = dec ? t->in_cid : t->out_cid;
     return k;
 }
 
@@ -129,11 +153,16 @@ static int run(int dec, tlsrec_transform *t, tlsrec_record *rec)
     d.type = rec->type;
     d.ver[0] = rec->ver[0];
     d.ver[1] = rec->ver[1];
-    int r = tlsrec__engine_run(dec, &d, rec->buf, rec->buf_len, &res);
+    d.cid_len = dec ? rec->cid_len : 0;
+    int r = tlsrec__engine_run(dec, &d, rec->buf, rec->buf_len, rec->cid, &res);
     if (r != 0) return r;
     rec->data_offset = res.data_offset;
     rec->data_len = res.data_len;
     rec->type = res.type;
+    if (!dec && res.cid_len) {                       /* ssl_msg.c:874-875 */
+        rec->cid_len = res.cid_len;
+        memcpy(rec->cid, t->out_cid, res.cid_len);
+    }
     return res.status;
 }
 
@@ -148,6 +177,10 @@ int tlsrec_encrypt_buf(void *ssl, tlsrec_transform *t, tlsrec_record *rec)
     tlsrec_plan p;
     tlsrec_plan_encrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset,
                         rec->data_len, t->granularity);
+    if (p.cid_set) {                                 /* ssl_msg.c:874-875 */
+        rec->cid_len = p.cid_len;
+        memcpy(rec->cid, t->out_cid, p.cid_len);
+    }
     if (p.status != 0) {
         if (p.side_type) {
             rec->buf[p.side_pos] = rec->type;
@@ -171,7 +204,9 @@ int tlsrec_decrypt_buf(const void *ssl, tlsrec_transform *t, tlsrec_record *rec)
     if (rec->buf_len > 0xffffffffu) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     tlsrec_plan_key k = pkey(t, 1);
     tlsrec_plan p;
-    tlsrec_plan_decrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset, rec->data_len);
+    if (rec->cid_len > TLSREC_CID_LEN_MAX) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    tlsrec_plan_decrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset, rec->data_len,
+                        rec->cid, rec->cid_len);
     if (p.status != 0) {
         rec->data_offset = p.data_offset;
         rec->data_len = p.data_len;
@@ -190,9 +225,11 @@ int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_
     k.fixed_ivlen = km->fixed_ivlen;
     k.taglen = km->taglen;
     k.iv = km->iv;
+    k.cid_len = 0;      /* framing of records without a connection ID */
+    k.cid = NULL;
     if (decrypt)
         tlsrec_plan_decrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset,
-                            rec->data_len);
+                            rec->data_len, NULL, 0);
     else
         tlsrec_plan_encrypt(&p, &k, rec->ctr, rec->type, rec->ver, rec->buf_len, rec->data_offset,
                             rec->data_len, km->granularity ? km->granularity : TLSREC_PADDING_GRANULARITY);
@@ -201,7 +238,8 @@ int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_
         early->data_offset = p.data_offset;
         early->data_len = p.data_len;
         early->type = p.type;
-        early->reserved[0] = early->reserved[1] = early->reserved[2] = 0;
+        early->cid_len = p.cid_set ? p.cid_len : 0;
+        early->reserved[0] = early->reserved[1] = 0;
     }
     if (aead_pos) *aead_pos = p.aead_pos;
     if (aead_len) *aead_len = p.aead_len;

@@ -25,7 +25,9 @@ struct SlotState {
     uint32_t rkr[60];         /* same, middle rounds 1..NR-1 stored rotr16 (aes_encrypt) */
     uint32_t nr;              /* 10 / 14, 0 for ChaCha20-Poly1305 */
     uint8_t h[16];            /* H = E_K(0^128) */
-    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16];
+    uint8_t cid_len;          /* DTLS 1.2 connection ID of this transform direction */
+    uint8_t cid[32];          /* (out_cid encrypting, in_cid decrypting), tlsrec_keytab_set_cid */
+    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16 - 33];
 };
 static_assert(sizeof(SlotState) == 1024, "SlotState layout");
 static_assert(sizeof(tlsrec_key_material) == 64, "key material layout");

@@ -135,25 +135,50 @@ __device__ __forceinline__ void zero_range(uint8_t *dst, uint32_t from, uint32_t
     for (uint32_t i = from + (uint32_t) q; i < to; i += (uint32_t) L) dst[i] = 0;
 }
 
-__device__ __forceinline__ tlsrec_plan_key plan_key(const tlsrec_key_material &km)
+__device__ __forceinline__ tlsrec_plan_key plan_key(const tlsrec_key_material &km, const SlotState *st)
 {
     tlsrec_plan_key k;
     k.tls13 = km.tls_minor == 4;
     k.fixed_ivlen = km.fixed_ivlen;
     k.taglen = km.taglen;
     k.iv = km.iv;
+    k.cid_len = st->cid_len;
+    k.cid = st->cid;
     return k;
 }
 
+/* The plan of batch record d under slot st (km = st->km, already loaded);
+ * `in` is the input arena (decrypt reads the record's CID bytes there). */
 template <bool DEC>
-__device__ __forceinline__ void make_plan(tlsrec_plan &p, const tlsrec_batch_rec &d, const tlsrec_key_material &km)
+__device__ __forceinline__ void make_plan(tlsrec_plan &p, const tlsrec_batch_rec &d, const tlsrec_key_material &km,
+                                          const SlotState *st, const uint8_t *in)
 {
-    tlsrec_plan_key k = plan_key(km);
-    if (DEC)
-        tlsrec_plan_decrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len);
-    else
+    tlsrec_plan_key k = plan_key(km, st);
+    if (DEC) {
+        const uint32_t off = (uint32_t) d.cid_off[0] | ((uint32_t) d.cid_off[1] << 8) |
+                             ((uint32_t) d.cid_off[2] << 16) | ((uint32_t) d.cid_off[3] << 24);
+        tlsrec_plan_decrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len,
+                            in + d.buf_off + off, d.cid_len);
+    } else {
         tlsrec_plan_encrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len,
                             km.granularity ? km.granularity : TLSREC_PADDING_GRANULARITY);
+    }
+}
+
+/* Block I >= 1 of the RFC 9146 AAD of a CID record (block 0 is p.aad), the
+ * byte stream shifted right by SHIFT bytes (CCM's len16 prefix, SHIFT = 2).
+ * cid = the slot's CID (for decrypt the plan checked it equals the record's). */
+template <int I, int SHIFT>
+__device__ __forceinline__ uint4 cid_aad_block(const tlsrec_plan &p, const tlsrec_batch_rec &d, const uint8_t *cid)
+{
+    uint32_t w[4] = { 0, 0, 0, 0 };
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int k = 16 * I + j - SHIFT;
+        const uint32_t b = k < 0 ? 0u : tlsrec_cid_aad_byte((uint32_t) k, p.type, d.ver, d.ctr, cid, p.cid_len, p.aead_len);
+        w[j >> 2] |= b << (8 * (j & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 /* Record naming no usable key slot (out of range or never loaded). */
@@ -164,7 +189,8 @@ __device__ inline void bad_slot_result(const tlsrec_batch_rec &d, tlsrec_batch_r
     r.data_offset = d.data_offset;
     r.data_len = d.data_len;
     r.type = d.type;
-    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+    r.cid_len = 0;
+        r.reserved[0] = r.reserved[1] = 0;
     *res = r;
 }
 
@@ -182,7 +208,8 @@ __device__ inline void finish_early(const tlsrec_plan &p, const tlsrec_batch_rec
     r.data_offset = p.data_offset;
     r.data_len = p.data_len;
     r.type = p.type;
-    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+    r.cid_len = p.cid_set ? p.cid_len : 0;
+        r.reserved[0] = r.reserved[1] = 0;
     *res = r;
 }
 

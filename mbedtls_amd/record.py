@@ -4,7 +4,8 @@
                  mbedtls_ssl_tls13_populate_transform (ssl_tls13_keys.c:922)
                  / the AEAD branch of ssl_tls12_populate_transform
                  (ssl_tls.c:7768-7797)
-    Record     ~ mbedtls_record (ssl_misc.h:1163-1188), non-CID
+    Record     ~ mbedtls_record (ssl_misc.h:1163-1188), incl. the DTLS 1.2
+                 connection ID (cid)
     encrypt_buf(transform, rec)  ~ mbedtls_ssl_encrypt_buf (ssl_msg.c:784)
     decrypt_buf(transform, rec)  ~ mbedtls_ssl_decrypt_buf (ssl_msg.c:1270)
 
@@ -29,6 +30,7 @@ class Record:
     data_offset: int
     data_len: int
     buf_len: int = field(default=-1)
+    cid: bytes = b""            # rec->cid / cid_len (DTLS 1.2 connection ID)
 
     def __post_init__(self):
         if self.buf_len < 0:
@@ -51,6 +53,13 @@ class Transform:
         if r != 0:
             raise RuntimeError(f"tlsrec_transform_setup failed: {r:#x}")
         self.tls_version, self.cipher = tls_version, cipher
+
+    def set_cid(self, in_cid: bytes, out_cid: bytes) -> None:
+        """transform->in_cid / out_cid (DTLS 1.2 connection IDs)."""
+        r = self._lib.tlsrec_transform_set_cid(ctypes.byref(self._t), bytes(in_cid), len(in_cid),
+                                               bytes(out_cid), len(out_cid))
+        if r != 0:
+            raise RuntimeError(f"tlsrec_transform_set_cid failed: {r:#x}")
 
     @property
     def slots(self):
@@ -84,10 +93,13 @@ class Transform:
         c.buf_len = rec.buf_len
         c.data_offset = rec.data_offset
         c.data_len = rec.data_len
+        c.cid_len = len(rec.cid)
+        c.cid[:len(rec.cid)] = list(rec.cid)
         r = fn(None, ctypes.byref(self._t), ctypes.byref(c))
         del cbuf
         rec.type, rec.ver = c.type, bytes(c.ver)
         rec.data_offset, rec.data_len = c.data_offset, c.data_len
+        rec.cid = bytes(c.cid[:c.cid_len])
         return r
 
     def encrypt_buf(self, rec: Record) -> int:

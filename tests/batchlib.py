@@ -35,21 +35,27 @@ class Rec:
     ctr: bytes
     type: int
     ver: bytes = b"\x03\x03"
+    cid: bytes = b""        # decrypt: the record's DTLS connection ID
 
 
 class Batch:
-    def __init__(self, slots, recs, align=16):
-        """slots: list of (cipher, version, key, iv, granularity)"""
+    def __init__(self, slots, recs, align=16, cids=None):
+        """slots: list of (cipher, version, key, iv, granularity); cids: optional
+        {slot: connection ID} (the slot's out_cid / in_cid)"""
         self.slots = slots
         self.recs = recs
+        self.cids = cids or {}
         offs, pos = [], 0
         for r in recs:
             offs.append(pos)
-            pos += (len(r.buf) + align - 1) // align * align + align
+            # the record's CID bytes (decrypt) sit after its buffer
+            pos += (len(r.buf) + len(r.cid) + align - 1) // align * align + align
         self.offs = offs
         self.arena = np.zeros(max(pos, 16), dtype=np.uint8)
         for r, o in zip(recs, offs):
             self.arena[o:o + len(r.buf)] = np.frombuffer(bytes(r.buf), dtype=np.uint8)
+            if r.cid:
+                self.arena[o + len(r.buf):o + len(r.buf) + len(r.cid)] = np.frombuffer(r.cid, dtype=np.uint8)
         d = M.records(len(recs))
         for i, (r, o) in enumerate(zip(recs, offs)):
             d[i]["buf_off"] = o
@@ -60,6 +66,8 @@ class Batch:
             d[i]["ctr"] = np.frombuffer(r.ctr, dtype=np.uint8)
             d[i]["type"] = r.type
             d[i]["ver"] = np.frombuffer(r.ver, dtype=np.uint8)
+            d[i]["cid_len"] = len(r.cid)
+            d[i]["cid_off"] = len(r.buf)
         self.desc = d
 
     def key_materials(self):
@@ -74,6 +82,8 @@ class Batch:
         if own:
             kt = M.KeyTable(max(1, len(self.slots)))
             kt.load(self.key_materials())
+            for slot, cid in self.cids.items():
+                kt.set_cid(slot, cid)
         arena = torch.from_numpy(self.arena.copy()).to(dev)
         out = arena if inplace else torch.zeros_like(arena)
         recs = torch.from_numpy(self.desc.view(np.uint8).copy()).to(dev)
@@ -94,9 +104,11 @@ class Batch:
             c, v, k, iv, g = self.slots[r.slot]
             if r.slot not in ts:
                 ts[r.slot] = O.Transform(v, c, k, k, iv, iv, granularity=g or 16)
+                if r.slot in self.cids:
+                    ts[r.slot].set_cid(self.cids[r.slot], self.cids[r.slot])
             t = ts[r.slot]
             rec = O.Record(ctr=r.ctr, type=r.type, ver=r.ver, buf=bytearray(r.buf),
-                           data_offset=r.data_offset, data_len=r.data_len)
+                           data_offset=r.data_offset, data_len=r.data_len, cid=r.cid if decrypt else b"")
             st = t.decrypt_buf(rec) if decrypt else t.encrypt_buf(rec)
             outs.append(rec)
             stats.append(st)
@@ -108,8 +120,9 @@ class Batch:
         bad = []
         for i, (r, orec, ost) in enumerate(zip(self.recs, o_recs, o_stats)):
             g = gpu_res[i]
-            fields = (int(g["status"]), int(g["data_offset"]), int(g["data_len"]), int(g["type"]))
-            want = (ost, orec.data_offset, orec.data_len, orec.type)
+            fields = (int(g["status"]), int(g["data_offset"]), int(g["data_len"]), int(g["type"]),
+                      int(g["cid_len"]) if not decrypt else 0)
+            want = (ost, orec.data_offset, orec.data_len, orec.type, len(orec.cid) if not decrypt else 0)
             if fields != want:
                 bad.append(f"rec {i}: fields {fields} != oracle {want}")
                 continue

@@ -33,8 +33,8 @@ def test_library_loads_and_exports_every_symbol():
 
 
 def test_struct_layouts():
-    assert ctypes.sizeof(_abi.CRecord) == 48
-    assert ctypes.sizeof(_abi.CTransform) == 168
+    assert ctypes.sizeof(_abi.CRecord) == 88       # + cid_len, cid[32]
+    assert ctypes.sizeof(_abi.CTransform) == 232   # + in/out_cid_len, in/out_cid[32]
     assert M.BATCH_REC.itemsize == 40 and M.BATCH_RES.itemsize == 16 and M.KEY_MATERIAL.itemsize == 64
 
 
