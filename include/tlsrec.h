@@ -161,7 +161,7 @@ typedef struct tlsrec_key_material {
     uint8_t fixed_ivlen;     /* 12, or 4 for TLS 1.2 GCM */
     uint8_t taglen;          /* 16, or 8 for TLSREC_CIPHER_AES_*_CCM_8 */
     uint8_t granularity;     /* TLS 1.3 padding granularity, 0 = 16 (ssl.h:432) */
-    uint8_t reserved[11];
+    uint8_t reserved[11];    /* zero (the device copy keeps the slot's CID length in [0]) */
     uint8_t iv[16];          /* static IV, first fixed_ivlen bytes used */
     uint8_t key[32];         /* 16, 24 or 32 bytes used */
 } tlsrec_key_material;

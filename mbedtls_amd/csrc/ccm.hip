@@ -40,7 +40,7 @@ __device__ __forceinline__ uint32_t w4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
 
-template <int NR, bool DEC>
+template <int NR, bool DEC, bool CID = false>
 __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[65536];   /* T0/T1 x 32 copies at offset 0 */
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
         const tlsrec_key_material km = a.slots[s].km;
         const tlsrec_batch_rec d = a.recs[my_rec];
         tlsrec_plan p;
-        make_plan<DEC>(p, d, km, &a.slots[s], a.in);
+        make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
         if (p.status != 0) {
             finish_early(p, d, a.out, &a.res[my_rec]);
             continue;
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             const uint4 a1 = make_uint4(w4(ab[0], ab[1], ab[2], ab[3]), w4(ab[4], ab[5], ab[6], ab[7]),
                                         w4(ab[8], ab[9], ab[10], ab[11]), w4(ab[12], ab[13], ab[14], ab[15]));
             x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, a1));
-            if (p.aad_len > 14) {   /* DTLS 1.2 + CID: 23..55 AAD bytes after len16 */
+            if (CID && p.aad_len > 14) {   /* DTLS 1.2 + CID: 23..55 AAD bytes after len16 */
                 const uint8_t *cid = a.slots[s].cid;
                 x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<1, 2>(p, d, cid)));
                 if (p.aad_len > 30) x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<2, 2>(p, d, cid)));
@@ -207,7 +207,10 @@ extern "C" hipError_t tlsrec__launch_ccm(const CcmArgs *a, int dec, uint32_t nr_
     hipError_t e = hipSuccess;
 #define TLSREC_CCM_LAUNCH(NR)                                                                                  \
     if (e == hipSuccess && (nr_mask & (1u << NR))) {                                                          \
-        if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true>), dim3(g), dim3(CCM_THREADS), 0, st, b);     \
+        if (b.cid) {                                                                                          \
+            if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true, true>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
+            else hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, false, true>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
+        } else if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
         else hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, false>), dim3(g), dim3(CCM_THREADS), 0, st, b);        \
         e = hipGetLastError();                                                                                \
     }

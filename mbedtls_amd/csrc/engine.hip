@@ -28,6 +28,7 @@ struct tlsrec_keytab {
     uint8_t *h_cipher;        /* host mirror of each slot's cipher */
     uint32_t cipher_mask;     /* 1 << TLSREC_CIPHER_* of every loaded slot */
     uint32_t nloaded;         /* slots holding a key */
+    uint32_t has_cid;         /* some slot was given a DTLS connection ID: launch the CID kernels */
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED; }
@@ -87,9 +88,12 @@ extern "C" int tlsrec_keytab_set_cid(tlsrec_keytab *kt, uint32_t slot, const uns
     memset(v, 0, sizeof(v));
     v[0] = (uint8_t) cid_len;
     if (cid_len) memcpy(v + 1, cid, cid_len);
+    if (cid_len) kt->has_cid = 1;
     static_assert(offsetof(SlotState, cid) == offsetof(SlotState, cid_len) + 1, "SlotState CID layout");
     hipStream_t st = (hipStream_t) stream;
     hipError_t e = hipMemcpyAsync(&kt->d_slots[slot].cid_len, v, sizeof(v), hipMemcpyHostToDevice, st);
+    /* and its mirror in the slot's key material, which the kernels hold */
+    if (e == hipSuccess) e = hipMemcpyAsync(&kt->d_slots[slot].km.reserved[0], v, 1, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
 }
@@ -294,6 +298,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         const uint32_t rpk = kt->nloaded > 1 ? n / kt->nloaded : n;
         int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
                 : (kt->nloaded <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
+        if (kt->has_cid) L = 8;     /* the CID variant: one configuration */
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;
@@ -307,14 +312,15 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.out = out;
         int nr = (int) tlsrec_cipher_nr(cipher);
         const int wpe = gcm_wp_env();
-        const bool wp = !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && rpk < 8));
-        const int waves = wp ? 8 : gcm_waves();
+        const bool wp = !kt->has_cid && !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && rpk < 8));
+        const int waves = wp ? 8 : (kt->has_cid ? 16 : gcm_waves());
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
-        if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : waves, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
+            rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     uint32_t ccm_nr = 0;
     for (int c = TLSREC_CIPHER_AES_128_CCM; c <= TLSREC_CIPHER_AES_256_CCM_8; c++)
@@ -332,10 +338,12 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.out = out;
         a.capacity = cap;
         a.flag_nr = 0;
+        a.cid = kt->has_cid;
         if (tlsrec__launch_ccm(&a, dec, ccm_nr, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (!rc && (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
         int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;
+        if (kt->has_cid) L = 2;     /* the CID variant: one configuration */
         CpArgs a;
         a.slots = kt->d_slots;
         a.recs = recs;
@@ -348,6 +356,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.out = out;
         a.rpw = pick_rpw(n, CP_WAVES, 64 / L, (uint32_t) cu * 4);
         a.capacity = cap;
+        a.cid = kt->has_cid;
         uint64_t per_wg = (uint64_t) CP_WAVES * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;

@@ -97,6 +97,7 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     const bool gcm = tlsrec_cipher_is_gcm(km.cipher);
     if (tid == 0) {
         st->km = km;
+        st->km.reserved[0] = 0;   /* CID length mirror (tlsrec_recdev.h plan_key) */
         st->nr = 0;
         st->cid_len = 0;          /* a (re)load leaves the slot without a CID */
         if (aes) {
@@ -226,7 +227,7 @@ __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
     }
 }
 
-template <int L, int NR, bool DEC, int W, int B, bool WP = false>
+template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false>
 __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 {
     using LY = GcmLds<L, W, WP>;
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             if (mine) {
                 const tlsrec_batch_rec d = a.recs[my_rec];
                 tlsrec_plan p;
-                make_plan<DEC>(p, d, km, &a.slots[s], a.in);
+                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
             }
             ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
@@ -342,14 +343,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             if (active) {
                 const tlsrec_batch_rec d = a.recs[ridx];
                 tlsrec_plan p;
-                make_plan<DEC>(p, d, km, &a.slots[s], a.in);
+                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
                 if (p.status != 0) {
                     if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
                 } else {
                     jb.setup<DEC>(p, d, a.in, a.out);
                     /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
                      * into the block the AAD fold multiplies by H below */
-                    if (p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
+                    if (CID && p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
                 }
             }
             const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint4 tag = xor4(Y, ej0);
             const tlsrec_batch_rec d = a.recs[ridx];
             tlsrec_plan p;
-            make_plan<DEC>(p, d, km, &a.slots[s], a.in);
+            make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
             if (!DEC) {
                 if (q == 0) {
                     store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
@@ -612,6 +613,20 @@ __device__ __forceinline__ P5 p_from_words(uint4 w)
     return r;
 }
 
+/* Poly1305 Horner over blocks 0..3 of a CID record's AAD (block 0 = a0, in
+ * limb form): A_1 r^(a-1) + ... + A_a.  Out of line, as gcm_cid_aad_fold. */
+__device__ __noinline__ P5 cp_cid_aad_fold(P5 a0, const uint32_t *r1w, const tlsrec_plan &p,
+                                           const tlsrec_batch_rec &d, const uint8_t *cid)
+{
+    P5 r1;
+#pragma unroll
+    for (int i = 0; i < 5; i++) r1.v[i] = r1w[i];
+    P5 f = p_add(p_mul(a0, r1), p_from_words(cid_aad_block<1, 0>(p, d, cid)));
+    if (p.aad_len > 32) f = p_add(p_mul(f, r1), p_from_words(cid_aad_block<2, 0>(p, d, cid)));
+    if (p.aad_len > 48) f = p_add(p_mul(f, r1), p_from_words(cid_aad_block<3, 0>(p, d, cid)));
+    return f;
+}
+
 template <int L>
 __device__ __forceinline__ P5 shfl_p5(P5 v, int src)
 {
@@ -630,8 +645,9 @@ struct CpRec {
     uint32_t pad0;
     uint32_t s[4];           /* Poly1305 s */
     uint32_t r1[5], r2[5], r3[5], rl[5];   /* r, r^2, r^3, r^(4L) (26-bit limbs) */
+    uint32_t aadf[5];        /* DTLS 1.2 + CID: the 2..4 AAD blocks Horner-folded */
 };
-static_assert(sizeof(CpRec) == 144, "CpRec layout");
+static_assert(sizeof(CpRec) == 164, "CpRec layout");
 
 __device__ __forceinline__ P5 p_lds(const uint32_t *v)
 {
@@ -686,7 +702,7 @@ __device__ __forceinline__ void chacha_block_kn(const uint32_t *kn, uint32_t cou
     chacha_block(key, counter, nw, out);
 }
 
-template <int L, bool DEC>
+template <int L, bool DEC, bool CID = false>
 __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void tlsrec_chachapoly_kernel(CpArgs a)
 {
     constexpr int R = 64 / L;
@@ -715,7 +731,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
                 mine = true;
                 const tlsrec_key_material km = a.slots[d.slot].km;
                 tlsrec_plan p;
-                make_plan<DEC>(p, d, km, &a.slots[d.slot], a.in);
+                make_plan<DEC, CID>(p, d, km, &a.slots[d.slot], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
                 for (int i = 0; i < 8; i++) key[i] = ld_u32le(km.key + 4 * i);
             }
@@ -751,7 +767,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         if (active) {
             d = a.recs[ridx];
             const tlsrec_key_material km = a.slots[d.slot].km;
-            make_plan<DEC>(p, d, km, &a.slots[d.slot], a.in);
+            make_plan<DEC, CID>(p, d, km, &a.slots[d.slot], a.in);
             if (p.status != 0) {
                 if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
             } else {
@@ -765,19 +781,20 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         const uint32_t z = (L - B % L) % L;
         const uint32_t J = run ? (B + z) / L : 0;
         const uint32_t Jmax = wave_max(J);
-        P5 aadp = p_zero();   /* AAD blocks Horner-folded: A_1 r^(a-1) + ... + A_a */
+        uint4 aadw = make_uint4(0, 0, 0, 0);
+        bool cidaad = false;  /* AAD of 2..4 blocks, folded into cr.aadf */
         const uint8_t *src = a.in;
         uint8_t *dst = a.out;
         bool aligned = false;
         uint32_t content_len = 0;
         if (run) {
-            aadp = p_from_words(aad_words(p));
-            if (p.aad_len > 16) {   /* DTLS 1.2 + CID: 2..4 AAD blocks */
-                const uint8_t *cid = a.slots[d.slot].cid;
-                const P5 r1 = p_lds(cr.r1);
-                aadp = p_add(p_mul(aadp, r1), p_from_words(cid_aad_block<1, 0>(p, d, cid)));
-                if (p.aad_len > 32) aadp = p_add(p_mul(aadp, r1), p_from_words(cid_aad_block<2, 0>(p, d, cid)));
-                if (p.aad_len > 48) aadp = p_add(p_mul(aadp, r1), p_from_words(cid_aad_block<3, 0>(p, d, cid)));
+            aadw = aad_words(p);
+            cidaad = CID && p.aad_len > 16;
+            if (cidaad && q == 0) {   /* DTLS 1.2 + CID: one lane folds, all read */
+                const P5 f = cp_cid_aad_fold(p_from_words(aadw), cr.r1, p, d, a.slots[d.slot].cid);
+                uint32_t *w = const_cast<uint32_t *>(cr.aadf);
+#pragma unroll
+                for (int i = 0; i < 5; i++) w[i] = f.v[i];
             }
             src = a.in + d.buf_off + p.aead_pos;
             dst = a.out + d.buf_off + p.aead_pos;
@@ -834,7 +851,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
             const P5 r1 = p_lds(cr.r1);
             const uint32_t vv = (valid && (uint32_t) b == B - 1) ? v : 4;
             P5 x = p_from_words(ct[0]);
-            if (b == 0) x = p_add(x, p_mul(aadp, r1));
+            if (b == 0) x = p_add(x, p_mul(cidaad ? p_lds(cr.aadf) : p_from_words(aadw), r1));
 #pragma unroll
             for (int t = 1; t < 4; t++) {
                 P5 y = p_add(p_mul(x, r1), p_from_words(ct[t]));
@@ -919,7 +936,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         }
         for (; j < Jmax; j++) general(j);
 
-        if (run && B == 0 && q == L - 1) vf = aadp;
+        if (run && B == 0 && q == L - 1) vf = cidaad ? p_lds(cr.aadf) : p_from_words(aadw);
         /* rotated tree: logical ql = (q+1) % L, anchored at chunk B-2;
          * level i combines with r^(4 * 2^i) */
         const P5 r1 = p_lds(cr.r1), r2 = p_lds(cr.r2);
@@ -1007,6 +1024,14 @@ static hipError_t launch_gcm_wp(const GcmArgs &a, uint32_t grid, hipStream_t st)
     return hipGetLastError();
 }
 
+/* key tables with DTLS connection IDs: one configuration (8 lanes, 16 waves) */
+template <int NR, bool DEC>
+static hipError_t launch_gcm_cid(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, true>), dim3(grid), dim3(16 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
 template <int L, int NR, bool DEC, int W>
 static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
 {
@@ -1021,6 +1046,14 @@ static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
 template <int L, bool DEC>
 static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t grid, hipStream_t st)
 {
+    if (waves == -16) {  /* CID variant (engine: the key table holds connection IDs; L = 8) */
+        if constexpr (L == 8) {
+            if (nr == 10) return launch_gcm_cid<10, DEC>(a, grid, st);
+            if (nr == 12) return launch_gcm_cid<12, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_cid<14, DEC>(a, grid, st);
+        }
+        return hipErrorInvalidValue;
+    }
     if (waves == -8) {   /* wave-pass variant (engine: many keys, few records each) */
         if constexpr (L == 16 || L == 64) {
             if (nr == 10) return launch_gcm_wp<L, 10, DEC>(a, grid, st);
@@ -1037,7 +1070,14 @@ static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t gr
 template <int L, bool DEC>
 static hipError_t launch_cp_t(const CpArgs &a, uint32_t grid, hipStream_t st)
 {
-    hipLaunchKernelGGL((tlsrec_chachapoly_kernel<L, DEC>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+    if (a.cid) {   /* key table with DTLS connection IDs: L = 2 */
+        if constexpr (L == 2)
+            hipLaunchKernelGGL((tlsrec_chachapoly_kernel<2, DEC, true>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+        else
+            return hipErrorInvalidValue;
+    } else {
+        hipLaunchKernelGGL((tlsrec_chachapoly_kernel<L, DEC>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+    }
     return hipGetLastError();
 }
 

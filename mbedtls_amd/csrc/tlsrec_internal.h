@@ -65,6 +65,7 @@ struct CpArgs {
     uint8_t *out;
     uint32_t rpw;
     uint32_t capacity;
+    uint32_t cid;             /* the key table holds DTLS connection IDs: CID kernel variant */
 };
 
 /* Bucket pass: key index of a record = AES-128-GCM slot, AES-256-GCM slot,
@@ -94,6 +95,7 @@ struct CcmArgs {
     uint8_t *out;
     uint32_t capacity;
     uint32_t flag_nr;         /* identity order: the launch (AES rounds) that flags unusable slots */
+    uint32_t cid;             /* the key table holds DTLS connection IDs: CID kernel variant */
 };
 
 } /* namespace tlsrec */

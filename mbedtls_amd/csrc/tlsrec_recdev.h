@@ -142,23 +142,42 @@ __device__ __forceinline__ tlsrec_plan_key plan_key(const tlsrec_key_material &k
     k.fixed_ivlen = km.fixed_ivlen;
     k.taglen = km.taglen;
     k.iv = km.iv;
-    k.cid_len = st->cid_len;
+    /* km.reserved[0] mirrors st->cid_len (tlsrec_keytab_set_cid): the plan
+     * needs no load beyond the key material the kernel already holds */
+    k.cid_len = km.reserved[0];
     k.cid = st->cid;
     return k;
 }
 
 /* The plan of batch record d under slot st (km = st->km, already loaded);
- * `in` is the input arena (decrypt reads the record's CID bytes there). */
-template <bool DEC>
+ * `in` is the input arena (decrypt reads the record's CID bytes there).
+ * CID = false: the kernel instantiation for key tables without connection IDs
+ * (every slot's CID is empty), in which all CID code folds away; a record
+ * that carries a CID there gets UNEXPECTED_CID (ssl_msg.c:1313-1320). */
+template <bool DEC, bool CID = false>
 __device__ __forceinline__ void make_plan(tlsrec_plan &p, const tlsrec_batch_rec &d, const tlsrec_key_material &km,
                                           const SlotState *st, const uint8_t *in)
 {
     tlsrec_plan_key k = plan_key(km, st);
+    if (!CID) {
+        k.cid_len = 0;
+        k.cid = nullptr;
+    }
     if (DEC) {
-        const uint32_t off = (uint32_t) d.cid_off[0] | ((uint32_t) d.cid_off[1] << 8) |
-                             ((uint32_t) d.cid_off[2] << 16) | ((uint32_t) d.cid_off[3] << 24);
-        tlsrec_plan_decrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len,
-                            in + d.buf_off + off, d.cid_len);
+        if (CID) {
+            const uint32_t off = (uint32_t) d.cid_off[0] | ((uint32_t) d.cid_off[1] << 8) |
+                                 ((uint32_t) d.cid_off[2] << 16) | ((uint32_t) d.cid_off[3] << 24);
+            tlsrec_plan_decrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len,
+                                in + d.buf_off + off, d.cid_len);
+        } else {
+            tlsrec_plan_decrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len, nullptr, 0);
+            if (d.cid_len != 0 && p.status != TLSREC_E_INTERNAL_ERROR) {   /* after :1301-1307 */
+                p.status = TLSREC_E_UNEXPECTED_CID;
+                p.data_offset = d.data_offset;
+                p.data_len = d.data_len;
+                p.type = d.type;
+            }
+        }
     } else {
         tlsrec_plan_encrypt(&p, &k, d.ctr, d.type, d.ver, d.buf_len, d.data_offset, d.data_len,
                             km.granularity ? km.granularity : TLSREC_PADDING_GRANULARITY);
