@@ -294,27 +294,39 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
                     bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
     threads = min(16, os.cpu_count() or 1)
     from tests.prng import prng_array
+    # grow the sample up to a 512 MiB arena, then repeat the timed pass over it
+    # (resealed untimed for decrypt) until about target_s of wall time
+    cap = 512 << 20
     n = 1024
     while True:
         arena = np.zeros(n * stride, dtype=np.uint8)
         payload = prng_array(SEED ^ 0xC0FFEE, n * content).reshape(n, content)
         arena.reshape(n, stride)[:, :content] = payload
+        st = np.zeros(n, dtype=np.int32)
         if direction == "decrypt":
-            st = np.zeros(n, dtype=np.int32)
             t.bench(1, arena, stride, content, n, 0, threads, st)     # seal (untimed)
             assert (st == 0).all()
             el = t.bench(0, arena, stride, wire, n, 0, threads, st)
-            assert (st == 0).all()
         else:
-            st = np.zeros(n, dtype=np.int32)
             el = t.bench(1, arena, stride, content, n, 0, threads, st)
-            assert (st == 0).all()
-        if el >= target_s or n * stride >= (4 << 30):
+        assert (st == 0).all()
+        if el >= target_s or n * stride * 2 > cap:
             break
-        n = min(int(n * max(2.0, min(8.0, target_s / max(el, 1e-3)))), (4 << 30) // stride)
+        n = min(int(n * max(2.0, min(8.0, target_s / max(el, 1e-3)))), cap // stride)
+    reps = 1
+    while el < target_s:
+        if direction == "decrypt":
+            arena.reshape(n, stride)[:, :content] = payload
+            t.bench(1, arena, stride, content, n, 0, threads, st)     # reseal (untimed)
+            el += t.bench(0, arena, stride, wire, n, 0, threads, st)
+        else:
+            el += t.bench(1, arena, stride, content, n, 0, threads, st)
+        assert (st == 0).all()
+        reps += 1
+    n *= reps
     gib = n * inner / el / 2**30
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} records x {inner} B inner plaintext, {direction}, oracle/liboracle.so "
+            "sample": f"{n} records ({reps} passes) x {inner} B inner plaintext, {direction}, oracle/liboracle.so "
                       f"(table AES + 4-bit Shoup GHASH / ChaCha20 + 44-bit-limb Poly1305), {el:.2f} s wall on {threads} threads"}
 
 

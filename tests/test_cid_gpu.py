@@ -127,3 +127,28 @@ def test_cid_batch_negative(cipher):
     for i in (0, 1):
         o = b.offs[i]
         assert bytes(out[o:o + len(sealed[i].buf)]) == bytes(sealed[i].buf)
+
+
+@pytest.mark.parametrize("cipher", [M.CIPHER_AES_128_GCM, M.CIPHER_CHACHA20_POLY1305, M.CIPHER_AES_256_CCM])
+def test_cid_record_in_table_without_cids(cipher):
+    """A key table without connection IDs runs the default (CID-free) kernel
+    instantiation: a record that carries a CID does not match the slot's empty
+    in_cid -> UNEXPECTED_CID, untouched; its neighbours decrypt normally."""
+    slots = [(cipher, M.VERSION_TLS1_2, prng_bytes(0xE0 + cipher, 32)[:M.KEYLEN[cipher]], prng_bytes(0xE1, 16), 0)]
+    head = 0 if cipher == M.CIPHER_CHACHA20_POLY1305 else 8
+    recs = B.plaintext_records(slots, [40, 300, 17], 0xE2 + cipher, head=head, tail=48)
+    o_recs, _ = B.Batch(slots, recs).run_oracle(False)
+    sealed = [B.Rec(slot=r.slot, buf=bytearray(o.buf), data_offset=o.data_offset, data_len=o.data_len, ctr=r.ctr,
+                    type=o.type, ver=r.ver, cid=(b"\x01\x02\x03" if i == 1 else b"")) for i, (r, o) in enumerate(zip(recs, o_recs))]
+    b = B.Batch(slots, sealed)
+    out, res = b.run_gpu(True)
+    assert not b.compare(True, out, res)
+    assert [int(x) for x in res["status"]] == [0, M.ERR_SSL_UNEXPECTED_CID, 0]
+    o = b.offs[1]
+    assert bytes(out[o:o + len(sealed[1].buf)]) == bytes(sealed[1].buf)
+    # the single-record API decides the same on the host
+    t = M.Transform(M.VERSION_TLS1_2, cipher, slots[0][2], slots[0][2], slots[0][3], slots[0][3])
+    r = sealed[1]
+    rec = M.Record(ctr=r.ctr, type=r.type, ver=r.ver, buf=bytearray(r.buf), data_offset=r.data_offset,
+                   data_len=r.data_len, cid=r.cid)
+    assert t.decrypt_buf(rec) == M.ERR_SSL_UNEXPECTED_CID
