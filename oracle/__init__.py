@@ -30,9 +30,11 @@ CHACHA20_POLY1305 = 3
 AES_192_GCM = 4
 AES_128_CCM, AES_192_CCM, AES_256_CCM = 5, 6, 7
 AES_128_CCM_8, AES_192_CCM_8, AES_256_CCM_8 = 8, 9, 10
+ARIA_128_GCM, ARIA_192_GCM, ARIA_256_GCM = 11, 12, 13
 KEYLEN = {AES_128_GCM: 16, AES_256_GCM: 32, CHACHA20_POLY1305: 32, AES_192_GCM: 24, AES_128_CCM: 16,
-          AES_192_CCM: 24, AES_256_CCM: 32, AES_128_CCM_8: 16, AES_192_CCM_8: 24, AES_256_CCM_8: 32}
-TAGLEN = {c: (8 if c >= AES_128_CCM_8 else 16) for c in KEYLEN}
+          AES_192_CCM: 24, AES_256_CCM: 32, AES_128_CCM_8: 16, AES_192_CCM_8: 24, AES_256_CCM_8: 32,
+          ARIA_128_GCM: 16, ARIA_192_GCM: 24, ARIA_256_GCM: 32}
+TAGLEN = {c: (8 if AES_128_CCM_8 <= c <= AES_256_CCM_8 else 16) for c in KEYLEN}
 
 _lib = None
 
@@ -89,8 +91,31 @@ def _buf(n):
     return ctypes.create_string_buffer(n)
 
 
+def aria_encrypt_block(key: bytes, block: bytes) -> bytes:
+    """ARIA (RFC 5794), oracle/aria.c."""
+    f = lib().orc_aria_setkey_enc
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint]
+    ctx = _buf(1024)
+    assert f(ctx, key, len(key) * 8) == 0
+    out = _buf(16)
+    g = lib().orc_aria_encrypt_block
+    g.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    g(ctx, block, out)
+    return out.raw
+
+
+def aria_gcm_encrypt(key: bytes, iv: bytes, aad: bytes, pt: bytes):
+    f = lib().orc_gcm_setkey_ex
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint, ctypes.c_int]
+    ctx = _buf(_GCM_CTX)
+    assert f(ctx, key, len(key) * 8, 1) == 0
+    out, tag = _buf(max(1, len(pt))), _buf(16)
+    lib().orc_gcm_encrypt(ctx, iv, aad, len(aad), pt, len(pt), out, tag, 16)
+    return out.raw[:len(pt)], tag.raw
+
+
 def aes_encrypt_block(key: bytes, block: bytes) -> bytes:
-    ctx = _buf(512)
+    ctx = _buf(1024)
     assert lib().orc_aes_setkey_enc(ctx, key, len(key) * 8) == 0
     out = _buf(16)
     lib().orc_aes_encrypt_block(ctx, block, out)

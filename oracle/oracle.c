@@ -106,6 +106,7 @@ int orc_aes_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits)
         case 256: nk = 8; ctx->nr = 14; break;
         default: return -1;
     }
+    ctx->kind = 0;
     int total = 4 * (ctx->nr + 1);
     for (int i = 0; i < nk; i++) ctx->rk[i] = ld32le(key + 4 * i);
     uint8_t rcon = 1;
@@ -124,6 +125,10 @@ int orc_aes_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits)
 
 void orc_aes_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t out[16])
 {
+    if (ctx->kind == 1) {               /* ARIA (aria.c) under the same GCM / CCM code */
+        orc_aria_encrypt_block(ctx, in, out);
+        return;
+    }
     const uint32_t *rk = ctx->rk;
     uint32_t s[4], t[4];
     for (int c = 0; c < 4; c++) s[c] = ld32le(in + 4 * c) ^ rk[c];
@@ -185,9 +190,15 @@ static void last4_init(void)
 
 int orc_gcm_setkey(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits)
 {
+    return orc_gcm_setkey_ex(ctx, key, keybits, 0);
+}
+
+int orc_gcm_setkey_ex(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits, int aria)
+{
     static const uint8_t zero[16] = { 0 };
     pthread_once(&g_once4, last4_init);
-    if (orc_aes_setkey_enc(&ctx->aes, key, keybits) != 0) return -1;
+    if ((aria ? orc_aria_setkey_enc(&ctx->aes, key, keybits) : orc_aes_setkey_enc(&ctx->aes, key, keybits)) != 0)
+        return -1;
     orc_aes_encrypt_block(&ctx->aes, zero, ctx->h);
     uint64_t hi = ld64be(ctx->h), lo = ld64be(ctx->h + 8);
     /* table index n = raw nibble; its bit 3 is the lowest power in the window */
@@ -624,11 +635,15 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
             t->keylen = 24; break;
         case ORC_CIPHER_AES_256_GCM: case ORC_CIPHER_AES_256_CCM: case ORC_CIPHER_AES_256_CCM_8:
         case ORC_CIPHER_CHACHA20_POLY1305: t->keylen = 32; break;
+        /* ARIA-GCM (PSA_KEY_TYPE_ARIA + PSA_ALG_GCM, ssl_tls.c:2248-2289) */
+        case ORC_CIPHER_ARIA_128_GCM: t->keylen = 16; break;
+        case ORC_CIPHER_ARIA_192_GCM: t->keylen = 24; break;
+        case ORC_CIPHER_ARIA_256_GCM: t->keylen = 32; break;
         default: return ORC_ERR_SSL_FEATURE_UNAVAILABLE;
     }
     t->ivlen = 12;
     /* MBEDTLS_CIPHERSUITE_SHORT_TAG: ssl_tls.c:7707-7708, ssl_tls13_keys.c:981-985 */
-    t->taglen = (cipher >= ORC_CIPHER_AES_128_CCM_8) ? 8 : 16;
+    t->taglen = (cipher >= ORC_CIPHER_AES_128_CCM_8 && cipher <= ORC_CIPHER_AES_256_CCM_8) ? 8 : 16;
     t->maclen = 0;
     if (tls_version == ORC_VERSION_TLS1_3) {
         t->fixed_ivlen = t->ivlen;
@@ -644,8 +659,9 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
     memcpy(t->iv_enc, iv_enc, 16);
     memcpy(t->iv_dec, iv_dec, 16);
     if (cipher != ORC_CIPHER_CHACHA20_POLY1305) {
-        orc_gcm_setkey(&t->gcm_enc, key_enc, (unsigned) t->keylen * 8);
-        orc_gcm_setkey(&t->gcm_dec, key_dec, (unsigned) t->keylen * 8);
+        const int aria = cipher >= ORC_CIPHER_ARIA_128_GCM;
+        orc_gcm_setkey_ex(&t->gcm_enc, key_enc, (unsigned) t->keylen * 8, aria);
+        orc_gcm_setkey_ex(&t->gcm_dec, key_dec, (unsigned) t->keylen * 8, aria);
     }
     return 0;
 }

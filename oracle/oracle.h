@@ -74,17 +74,29 @@ extern "C" {
 #define ORC_CIPHER_AES_128_CCM_8      8
 #define ORC_CIPHER_AES_192_CCM_8      9
 #define ORC_CIPHER_AES_256_CCM_8      10
+/* ARIA-GCM (PSA_KEY_TYPE_ARIA, ssl_tls.c:2248-2289; RFC 6209 suites) */
+#define ORC_CIPHER_ARIA_128_GCM       11
+#define ORC_CIPHER_ARIA_192_GCM       12
+#define ORC_CIPHER_ARIA_256_GCM       13
 
 #define ORC_OUT_CONTENT_LEN 16384     /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
 
 /* ---- primitives ------------------------------------------------------- */
+/* Block-cipher context of the GCM / CCM code: AES (kind 0) or ARIA (kind 1,
+ * oracle/aria.c; nr = 12/14/16 rounds, ark = the nr + 1 round keys). */
 typedef struct {
     uint32_t rk[60];
     int nr;
+    int kind;
+    uint8_t ark[17][16];
 } orc_aes_ctx;
 
 int  orc_aes_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits);
 void orc_aes_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t out[16]);
+/* ARIA (RFC 5794) in the same context type; orc_aes_encrypt_block dispatches */
+int  orc_aria_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits);
+void orc_aria_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t out[16]);
+const uint8_t *orc_aria_sbox(int i);   /* SB1..SB4 as i = 0..3 */
 const uint8_t *orc_aes_sbox(void);
 
 typedef struct {
@@ -94,6 +106,8 @@ typedef struct {
 } orc_gcm_ctx;
 
 int  orc_gcm_setkey(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits);
+/* GCM over ARIA (aria != 0) or AES */
+int  orc_gcm_setkey_ex(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits, int aria);
 void orc_ghash_mult(const orc_gcm_ctx *ctx, const uint8_t x[16], uint8_t out[16]);
 /* one-shot GCM with a 12-byte IV; tag_len <= 16 */
 void orc_gcm_encrypt(const orc_gcm_ctx *ctx, const uint8_t iv[12],

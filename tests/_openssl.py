@@ -29,7 +29,8 @@ def lib():
         L = _lib
         L.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
         L.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
-        for f in ("EVP_aes_128_gcm", "EVP_aes_192_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305",
+        for f in ("EVP_aria_128_gcm", "EVP_aria_192_gcm", "EVP_aria_256_gcm", "EVP_aria_128_ecb",
+                  "EVP_aes_128_gcm", "EVP_aes_192_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305",
                   "EVP_aes_128_ccm", "EVP_aes_192_ccm", "EVP_aes_256_ccm"):
             getattr(L, f).restype = ctypes.c_void_p
         L.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -54,6 +55,8 @@ def _cipher(name: str, keylen: int):
     L = lib()
     if name == "gcm":
         return {16: L.EVP_aes_128_gcm, 24: L.EVP_aes_192_gcm, 32: L.EVP_aes_256_gcm}[keylen]()
+    if name == "aria-gcm":
+        return {16: L.EVP_aria_128_gcm, 24: L.EVP_aria_192_gcm, 32: L.EVP_aria_256_gcm}[keylen]()
     if name == "ccm":
         return {16: L.EVP_aes_128_ccm, 24: L.EVP_aes_192_ccm, 32: L.EVP_aes_256_ccm}[keylen]()
     return L.EVP_chacha20_poly1305()
