@@ -27,7 +27,8 @@
  * negative MBEDTLS_ERR_SSL_* value (include/mbedtls/ssl.h:40-125); the record
  * is transformed in place and its data_offset / data_len / type are updated
  * exactly as the reference updates them.  Only the AEAD suites are supported
- * (AES-128/192/256-GCM, AES-128/192/256-CCM and CCM_8, ChaCha20-Poly1305;
+ * (AES-128/192/256-GCM, AES-128/192/256-CCM and CCM_8, ChaCha20-Poly1305,
+ * ARIA-128/192/256-GCM;
  * TLS 1.2 and 1.3, and DTLS 1.2 records with an RFC 9146 connection ID).
  *
  * Every entry point that touches record data runs on the GPU; there is no CPU
@@ -71,7 +72,12 @@ extern "C" {
 #define TLSREC_CIPHER_AES_128_CCM_8      8
 #define TLSREC_CIPHER_AES_192_CCM_8      9
 #define TLSREC_CIPHER_AES_256_CCM_8      10
-#define TLSREC_CIPHER_MAX                10
+/* ARIA-GCM (RFC 5794 block cipher; PSA_KEY_TYPE_ARIA + PSA_ALG_GCM in
+ * mbedtls_ssl_cipher_to_psa, ssl_tls.c:2248-2289; the RFC 6209 TLS 1.2 suites) */
+#define TLSREC_CIPHER_ARIA_128_GCM       11
+#define TLSREC_CIPHER_ARIA_192_GCM       12
+#define TLSREC_CIPHER_ARIA_256_GCM       13
+#define TLSREC_CIPHER_MAX                13
 
 #define TLSREC_MSG_APPLICATION_DATA  23      /* ssl.h:527 */
 #define TLSREC_MSG_CID               25      /* MBEDTLS_SSL_MSG_CID, ssl.h:528 */

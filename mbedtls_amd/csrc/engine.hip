@@ -225,8 +225,8 @@ struct BucketScratch {
 static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
                   hipStream_t st, BucketScratch &b)
 {
-    /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, end */
-    const size_t nk = 4 * (size_t) kt->capacity + 2;
+    /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, ARIA-128/192/256-GCM slots, end */
+    const size_t nk = 7 * (size_t) kt->capacity + 2;
     b.scan_bytes = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, b.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
                                          (int) nk, st) != hipSuccess)
@@ -290,6 +290,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     for (int ci = 0; ci < 3 && !rc; ci++) {
         const int cipher = gcm_ciphers[ci];     /* bucket class ci: keys [ci * cap, (ci + 1) * cap) */
         if (!(kt->cipher_mask & (1u << cipher))) continue;
+        /* (ARIA-GCM below: one configuration) */
         /* lanes per record: a key pass should still fill the 16 waves of a
          * workgroup.  8 for a single key or >= 128 records per key; 16
          * (4 records per wave) down to 48 records per key; 64 (one record per
@@ -320,6 +321,30 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
+            rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    /* ARIA-GCM: the GCM kernel around ARIA (8 lanes, 16 waves); bucket classes
+     * (4, 5, 6) cap + 1 */
+    for (int c = TLSREC_CIPHER_ARIA_128_GCM; c <= TLSREC_CIPHER_ARIA_256_GCM && !rc; c++) {
+        if (!(kt->cipher_mask & (1u << c))) continue;
+        const size_t base = (size_t) (4 + (c - TLSREC_CIPHER_ARIA_128_GCM)) * cap + 1;
+        GcmArgs a;
+        a.slots = kt->d_slots;
+        a.ghtab = kt->d_ghtab;
+        a.recs = recs;
+        a.res = res;
+        a.n = n;
+        a.perm = identity ? nullptr : bs.perm;
+        a.lo = identity ? nullptr : bs.offs + base;
+        a.hi = identity ? nullptr : bs.offs + base + cap;
+        a.in = in;
+        a.out = out;
+        a.rpw = pick_rpw(n, 16u, 8u, (uint32_t) cu);
+        a.capacity = cap;
+        a.cipher = (uint32_t) c;
+        const uint64_t per_wg = (uint64_t) 16 * a.rpw;
+        const uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
+        if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_aria_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)
             rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     uint32_t ccm_nr = 0;

@@ -79,6 +79,62 @@ __device__ inline void aes_encrypt_bytes(const uint32_t *rk, int nr, uint8_t st[
     }
 }
 
+/* ARIA key schedule and byte-wise block (RFC 5794 2.2, 2.3), one lane:
+ * only for the round keys and H = E_K(0^128) of a slot. */
+__device__ inline void aria_round_bytes(uint8_t d[16], const uint8_t rk[16], bool odd, bool diffuse)
+{
+    uint32_t x[16], y[16];
+    for (int i = 0; i < 16; i++) {
+        const int t = odd ? (i & 3) : ((i & 3) ^ 2);
+        x[i] = kAriaSbox.v[t][d[i] ^ rk[i]];
+    }
+    if (diffuse) {
+        TLSREC_ARIA_A(y, x);
+        for (int i = 0; i < 16; i++) d[i] = (uint8_t) y[i];
+    } else {
+        for (int i = 0; i < 16; i++) d[i] = (uint8_t) x[i];
+    }
+}
+
+__device__ inline int aria_key_expand(const uint8_t *key, int keylen, uint8_t ek[17][16])
+{
+    const uint8_t C[3][16] = {
+        { 0x51, 0x7c, 0xc1, 0xb7, 0x27, 0x22, 0x0a, 0x94, 0xfe, 0x13, 0xab, 0xe8, 0xfa, 0x9a, 0x6e, 0xe0 },
+        { 0x6d, 0xb1, 0x4a, 0xcc, 0x9e, 0x21, 0xc8, 0x20, 0xff, 0x28, 0xb1, 0xd5, 0xef, 0x5d, 0xe2, 0xb0 },
+        { 0xdb, 0x92, 0x37, 0x1d, 0x21, 0x26, 0xe9, 0x70, 0x03, 0x24, 0x97, 0x75, 0x04, 0xe8, 0xc9, 0x0e },
+    };
+    const int first = keylen == 16 ? 0 : keylen == 24 ? 1 : 2, nr = keylen / 4 + 8;
+    uint8_t w[4][16], t[16], kr[16];
+    for (int i = 0; i < 16; i++) { w[0][i] = key[i]; kr[i] = 16 + i < keylen ? key[16 + i] : 0; }
+    for (int i = 0; i < 16; i++) t[i] = w[0][i];
+    aria_round_bytes(t, C[first], true, true);
+    for (int i = 0; i < 16; i++) w[1][i] = t[i] ^ kr[i];
+    for (int i = 0; i < 16; i++) t[i] = w[1][i];
+    aria_round_bytes(t, C[(first + 1) % 3], false, true);
+    for (int i = 0; i < 16; i++) w[2][i] = t[i] ^ w[0][i];
+    for (int i = 0; i < 16; i++) t[i] = w[2][i];
+    aria_round_bytes(t, C[(first + 2) % 3], true, true);
+    for (int i = 0; i < 16; i++) w[3][i] = t[i] ^ w[1][i];
+    const int rot[5] = { 19, 31, 128 - 61, 128 - 31, 128 - 19 };   /* right rotations */
+    for (int e = 0; e < nr + 1; e++) {
+        const uint8_t *a = w[e % 4], *b = w[(e % 4 + 1) % 4];
+        const int n = rot[e / 4], by = n / 8, bi = n % 8;
+        for (int i = 0; i < 16; i++) {
+            const uint8_t hi = b[(i - by + 16) % 16], lo = b[(i - by - 1 + 32) % 16];
+            const uint8_t r = (uint8_t) (bi ? ((hi >> bi) | (lo << (8 - bi))) : hi);
+            ek[e][i] = a[i] ^ r;
+        }
+    }
+    return nr;
+}
+
+__device__ inline void aria_encrypt_bytes(const uint8_t ek[17][16], int nr, uint8_t st[16])
+{
+    for (int r = 1; r < nr; r++) aria_round_bytes(st, ek[r - 1], (r & 1) != 0, true);
+    aria_round_bytes(st, ek[nr - 1], false, false);
+    for (int i = 0; i < 16; i++) st[i] ^= ek[nr][i];
+}
+
 /* One 256-thread workgroup per slot. */
 __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab,
                                                              const tlsrec_key_material *keys,
@@ -94,7 +150,8 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     /* every AES cipher gets its key schedule (GCM and CCM), GCM also H and
      * the GHASH tables */
     const bool aes = tlsrec_cipher_nr(km.cipher) != 0;
-    const bool gcm = tlsrec_cipher_is_gcm(km.cipher);
+    const bool aria = tlsrec_cipher_is_aria(km.cipher);
+    const bool gcm = tlsrec_cipher_is_gcm(km.cipher) || aria;
     if (tid == 0) {
         st->km = km;
         st->km.reserved[0] = 0;   /* CID length mirror (tlsrec_recdev.h plan_key) */
@@ -110,6 +167,22 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
             }
             uint8_t h[16] = { 0 };
             aes_encrypt_bytes(st->rk, nk + 6, h);
+            G128 H;
+            H.hi = 0; H.lo = 0;
+            for (int i = 0; i < 8; i++) { H.hi = (H.hi << 8) | h[i]; H.lo = (H.lo << 8) | h[8 + i]; }
+            for (int i = 0; i < 16; i++) st->h[i] = h[i];
+            pw[0] = H;
+            for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);
+        } else if (aria) {
+            uint8_t ek[17][16];
+            const int nr = aria_key_expand(km.key, (int) tlsrec_cipher_keylen(km.cipher), ek);
+            for (int e = 0; e < 17; e++)
+                for (int c = 0; c < 4; c++)
+                    st->ark[4 * e + c] = e <= nr ? ((uint32_t) ek[e][4 * c] | ((uint32_t) ek[e][4 * c + 1] << 8) |
+                                                    ((uint32_t) ek[e][4 * c + 2] << 16) | ((uint32_t) ek[e][4 * c + 3] << 24))
+                                                 : 0u;
+            uint8_t h[16] = { 0 };
+            aria_encrypt_bytes(ek, nr, h);
             G128 H;
             H.hi = 0; H.lo = 0;
             for (int i = 0; i < 8; i++) { H.hi = (H.hi << 8) | h[i]; H.lo = (H.lo << 8) | h[8 + i]; }
@@ -227,7 +300,9 @@ __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
     }
 }
 
-template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false>
+/* ARIA: the block cipher is ARIA (NR = 12/14/16 rounds, S-box tables in the
+ * T-table LDS region, round keys SlotState::ark) -- GCM around it unchanged */
+template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false, bool ARIA = false>
 __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 {
     using LY = GcmLds<L, W, WP>;
@@ -239,7 +314,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     __shared__ __attribute__((aligned(16))) uint8_t lds[LY::BYTES];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane / L, q = lane % L;
-    const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
+    const uint32_t lanebase = ARIA ? (uint32_t) (lane & 15) << 2 : (uint32_t) (lane & 31) << 2;
     uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + LY::CTL);
 
     /* This workgroup's positions: wave w owns positions base + k*W + w,
@@ -250,7 +325,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     const uint64_t wg_base = (uint64_t) blockIdx.x * W * a.rpw;
     if (wg_base >= count) return;                      /* uniform: before any barrier */
 
-    aes_fill_tables(lds + LY::AES, tid, NTHR);
+    if constexpr (ARIA)
+        aria_fill_tables(lds + LY::AES, tid, NTHR);
+    else
+        aes_fill_tables(lds + LY::AES, tid, NTHR);
 
     /* pass membership: lane l tracks the record at chunk position k = l */
     uint32_t my_slot = 0xffffffffu, my_rec = 0;
@@ -305,7 +383,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
         /* Round keys through the constant address space: scalar loads.  (Read
          * through a.slots they compile to vector loads + vmcnt(0) waits in
          * every round, since the kernel's own stores might alias the table.) */
-        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) a.slots[s].rkr;
+        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) (ARIA ? a.slots[s].ark : a.slots[s].rkr);
         const tlsrec_key_material km = a.slots[s].km;
 
         /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
@@ -319,7 +397,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
             }
-            ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+            if constexpr (ARIA)
+                ej0 = aria_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+            else
+                ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
             reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
         }
         /* lanes of this wave read other lanes' E(J0): the wave's own LDS
@@ -396,7 +477,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                     if constexpr (CACHED) {
                         aes_ghash<NR, LY::AES, HPI>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
                     } else {
-                        ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                        if constexpr (ARIA)
+                            ks = aria_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                        else
+                            ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
                         Zn = gmul<HPI>(hor, y);
                     }
                 };
@@ -454,10 +538,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 for (; j < Jmax; j++) general(j);
             };
             /* counters stay below 2^16 (any TLS record): cached rounds 1-2 */
-            if (wave_max(m) + 2 < 65536u)
-                steps(std::integral_constant<bool, true>());
-            else
-                steps(std::integral_constant<bool, false>());
+            if constexpr (ARIA) {
+                steps(std::integral_constant<bool, false>());   /* no cached rounds for ARIA */
+            } else {
+                if (wave_max(m) + 2 < 65536u)
+                    steps(std::integral_constant<bool, true>());
+                else
+                    steps(std::integral_constant<bool, false>());
+            }
             uint4 Y = xor4(Z, Xp);
             uint32_t nzkey = 0;
             if (DEC && jb.inner && nzpos) {
@@ -531,7 +619,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
  * after them; records without a usable slot get BAD_INPUT_DATA here.
  *   key index: AES-128-GCM -> slot, AES-256-GCM -> cap + slot, AES-192-GCM
  *   -> 2 cap + slot, AES-CCM (any size/tag) -> 3 cap + slot, ChaCha -> 4 cap,
- *   none -> no index.
+ *   ARIA-128/192/256-GCM -> (4, 5, 6) cap + 1 + slot, none -> no index.
  * Atomics are wave-aggregated when the wave's records share one key (a
  * batch already grouped by key costs one atomic per wave).
  * ==================================================================== */
@@ -544,6 +632,10 @@ __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec
         case TLSREC_CIPHER_AES_256_GCM: return a.capacity + d.slot;
         case TLSREC_CIPHER_AES_192_GCM: return 2 * a.capacity + d.slot;
         case TLSREC_CIPHER_CHACHA20_POLY1305: return 4 * a.capacity;
+        /* ARIA-GCM classes after the ChaCha counter: 4 cap + 1 + (0..2) cap + slot */
+        case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + 1 + d.slot;
+        case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + 1 + d.slot;
+        case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + 1 + d.slot;
         default: return tlsrec_cipher_is_ccm(c) ? 3 * a.capacity + d.slot : 0xffffffffu;
     }
 }
@@ -1024,6 +1116,17 @@ static hipError_t launch_gcm_wp(const GcmArgs &a, uint32_t grid, hipStream_t st)
     return hipGetLastError();
 }
 
+/* ARIA-GCM: one configuration (8 lanes, 16 waves), with or without CIDs */
+template <int NR, bool DEC>
+static hipError_t launch_gcm_aria(const GcmArgs &a, uint32_t grid, hipStream_t st, bool cid)
+{
+    if (cid)
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, true, true>), dim3(grid), dim3(16 * 64), 0, st, a);
+    else
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, false, true>), dim3(grid), dim3(16 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
 /* key tables with DTLS connection IDs: one configuration (8 lanes, 16 waves) */
 template <int NR, bool DEC>
 static hipError_t launch_gcm_cid(const GcmArgs &a, uint32_t grid, hipStream_t st)
@@ -1091,6 +1194,16 @@ extern "C" hipError_t tlsrec__launch_keysetup(SlotState *slots, uint4 *ghtab, co
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(tlsrec_keysetup_kernel, dim3(count), dim3(256), 0, st, slots, ghtab, keys, first, count);
     return hipGetLastError();
+}
+
+extern "C" hipError_t tlsrec__launch_gcm_aria(const GcmArgs *a, int dec, int nr, int cid, uint32_t grid, hipStream_t st)
+{
+    switch (nr) {
+        case 12: return dec ? launch_gcm_aria<12, true>(*a, grid, st, cid) : launch_gcm_aria<12, false>(*a, grid, st, cid);
+        case 14: return dec ? launch_gcm_aria<14, true>(*a, grid, st, cid) : launch_gcm_aria<14, false>(*a, grid, st, cid);
+        case 16: return dec ? launch_gcm_aria<16, true>(*a, grid, st, cid) : launch_gcm_aria<16, false>(*a, grid, st, cid);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 extern "C" hipError_t tlsrec__launch_gcm(const GcmArgs *a, int dec, int lanes, int nr, int waves, uint32_t grid,

@@ -152,6 +152,115 @@ __device__ __forceinline__ uint4 aes_encrypt(const uint8_t *lds, uint32_t lb, RK
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+/* ---------------- ARIA (RFC 5794) --------------------------------------- */
+/* SB1 = AES S-box, SB2(x) = B x^247 ^ 0xE2 (B by the images of the 8 basis
+ * bits), SB3 = SB1^-1, SB4 = SB2^-1; generated at compile time. */
+struct AriaSboxGen {
+    uint8_t v[4][256];
+    static constexpr uint8_t mul(uint8_t a, uint8_t b)
+    {
+        uint8_t r = 0;
+        for (int i = 0; i < 8; i++) {
+            if ((b >> i) & 1) r = (uint8_t) (r ^ a);
+            a = (uint8_t) ((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+        }
+        return r;
+    }
+    constexpr AriaSboxGen() : v()
+    {
+        const SboxGen aes{};
+        const uint8_t bcol[8] = { 0xac, 0xc5, 0x12, 0xcf, 0x5b, 0x5f, 0x85, 0xee };
+        for (int x = 0; x < 256; x++) {
+            uint8_t y = 1, base = (uint8_t) x;
+            for (int e = 247; e; e >>= 1) {
+                if (e & 1) y = mul(y, base);
+                base = mul(base, base);
+            }
+            if (x == 0) y = 0;
+            uint8_t t = 0xe2;
+            for (int k = 0; k < 8; k++)
+                if ((y >> k) & 1) t = (uint8_t) (t ^ bcol[k]);
+            v[0][x] = aes.v[x];
+            v[1][x] = t;
+        }
+        for (int x = 0; x < 256; x++) {
+            v[2][v[0][x]] = (uint8_t) x;
+            v[3][v[1][x]] = (uint8_t) x;
+        }
+    }
+};
+
+__constant__ const AriaSboxGen kAriaSbox{};
+
+/* Diffusion layer A (RFC 5794 2.4.3), on 16 bytes held in the low bits of
+ * 16 registers: y_i = x_a ^ x_b ^ ... (7 terms, two xor3 + one xor). */
+#define TLSREC_ARIA_A(y, x)                                                                  \
+    do {                                                                                     \
+        y[0] = xor3(xor3(x[3], x[4], x[6]), xor3(x[8], x[9], x[13]), x[14]);                 \
+        y[1] = xor3(xor3(x[2], x[5], x[7]), xor3(x[8], x[9], x[12]), x[15]);                 \
+        y[2] = xor3(xor3(x[1], x[4], x[6]), xor3(x[10], x[11], x[12]), x[15]);               \
+        y[3] = xor3(xor3(x[0], x[5], x[7]), xor3(x[10], x[11], x[13]), x[14]);               \
+        y[4] = xor3(xor3(x[0], x[2], x[5]), xor3(x[8], x[11], x[14]), x[15]);                \
+        y[5] = xor3(xor3(x[1], x[3], x[4]), xor3(x[9], x[10], x[14]), x[15]);                \
+        y[6] = xor3(xor3(x[0], x[2], x[7]), xor3(x[9], x[10], x[12]), x[13]);                \
+        y[7] = xor3(xor3(x[1], x[3], x[6]), xor3(x[8], x[11], x[12]), x[13]);                \
+        y[8] = xor3(xor3(x[0], x[1], x[4]), xor3(x[7], x[10], x[13]), x[15]);                \
+        y[9] = xor3(xor3(x[0], x[1], x[5]), xor3(x[6], x[11], x[12]), x[14]);                \
+        y[10] = xor3(xor3(x[2], x[3], x[5]), xor3(x[6], x[8], x[13]), x[15]);                \
+        y[11] = xor3(xor3(x[2], x[3], x[4]), xor3(x[7], x[9], x[12]), x[14]);                \
+        y[12] = xor3(xor3(x[1], x[2], x[6]), xor3(x[7], x[9], x[11]), x[12]);                \
+        y[13] = xor3(xor3(x[0], x[3], x[6]), xor3(x[7], x[8], x[10]), x[13]);                \
+        y[14] = xor3(xor3(x[0], x[3], x[4]), xor3(x[5], x[9], x[11]), x[14]);                \
+        y[15] = xor3(xor3(x[1], x[2], x[4]), xor3(x[5], x[8], x[10]), x[15]);                \
+    } while (0)
+
+/* LDS S-box tables: SB_t[x] as a dword (value in the low byte), 16 copies
+ * (copy = lane & 15) at ARIA_OFF + t*16384 + x*64 + copy*4 -- 64 KiB, the
+ * region the AES T-tables use. */
+__device__ __forceinline__ void aria_fill_tables(uint8_t *lds, int tid, int nthreads)
+{
+    for (int i = tid; i < 4 * 256 * 4; i += nthreads) {
+        const int t = i >> 10, x = (i >> 2) & 255, part = i & 3;   /* part: copies 4*part .. 4*part+3 */
+        const uint32_t v = kAriaSbox.v[t][x];
+        *reinterpret_cast<uint4 *>(lds + t * 16384 + x * 64 + part * 16) = make_uint4(v, v, v, v);
+    }
+}
+
+/* ARIA forward cipher (NR = 12/14/16 rounds) of one block per lane.  Words
+ * are little-endian (byte i of the block = byte i%4 of word i/4); rk = the
+ * NR + 1 round keys as 4 words each.  lb = (lane & 15) * 4. */
+template <int NR, int ARIA_OFF, typename RK>
+__device__ __forceinline__ uint4 aria_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
+{
+    const uint32_t w[4] = { in.x, in.y, in.z, in.w };
+    uint32_t x[16], y[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
+#pragma unroll
+    for (int r = 1; r <= NR; r++) {
+        /* AddRoundKey, then SL1 (odd rounds: SB1 SB2 SB3 SB4) or SL2 (even and
+         * the last round: SB3 SB4 SB1 SB2) */
+        const bool odd = (r & 1) && r != NR;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t kb = (rk[4 * (r - 1) + (i >> 2)] >> (8 * (i & 3))) & 0xffu;
+            const int t = odd ? (i & 3) : ((i & 3) ^ 2);
+            const uint32_t a = ((x[i] ^ kb) << 6) + lb;
+            x[i] = *reinterpret_cast<const uint32_t *>(lds + ARIA_OFF + t * 16384 + a);
+        }
+        if (r != NR) {
+            TLSREC_ARIA_A(y, x);
+#pragma unroll
+            for (int i = 0; i < 16; i++) x[i] = y[i];
+        }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        o[c] = (x[4 * c] | (x[4 * c + 1] << 8) | (x[4 * c + 2] << 16) | (x[4 * c + 3] << 24)) ^ rk[4 * NR + c];
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 /* ---------------- GHASH with LDS position tables ----------------------- */
 /* Table PI (a power of H) holds T_k[n] = sum_{i<4} bit(3-i of n) * P * x^(4k+i)
  * at PI*8192 + k*256 + n*16, as the 16-byte GCM string.  Window k = 2b is the

@@ -27,7 +27,9 @@ struct SlotState {
     uint8_t h[16];            /* H = E_K(0^128) */
     uint8_t cid_len;          /* DTLS 1.2 connection ID of this transform direction */
     uint8_t cid[32];          /* (out_cid encrypting, in_cid decrypting), tlsrec_keytab_set_cid */
-    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16 - 33];
+    uint8_t pad0[3];
+    uint32_t ark[68];         /* ARIA-GCM: the nr + 1 round keys ek1.. (RFC 5794 2.2), 16 B each as LE words */
+    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16 - 33 - 3 - 272];
 };
 static_assert(sizeof(SlotState) == 1024, "SlotState layout");
 static_assert(sizeof(tlsrec_key_material) == 64, "key material layout");
@@ -77,7 +79,7 @@ struct BucketArgs {
     tlsrec_batch_res *res;
     uint32_t n;
     uint32_t capacity;
-    uint32_t *counts;         /* [4 * capacity + 1] records per (class, slot), then exclusive offsets */
+    uint32_t *counts;         /* [7 * capacity + 2] records per (class, slot), then exclusive offsets */
     uint32_t *cursor;         /* copy of the offsets, consumed by the scatter */
     uint32_t *cp_cursor;      /* ChaCha records appended after the GCM ones */
     uint32_t *perm;           /* [n] */
@@ -104,6 +106,7 @@ extern "C" {
 hipError_t tlsrec__launch_ccm(const tlsrec::CcmArgs *a, int dec, uint32_t nr_mask, hipStream_t st);
 hipError_t tlsrec__launch_keysetup(tlsrec::SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
                                    uint32_t first, uint32_t count, hipStream_t st);
+hipError_t tlsrec__launch_gcm_aria(const tlsrec::GcmArgs *a, int dec, int nr, int cid, uint32_t grid, hipStream_t st);
 hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int nr, int waves, uint32_t grid,
                               hipStream_t st);
 hipError_t tlsrec__launch_chachapoly(const tlsrec::CpArgs *a, int dec, int lanes, uint32_t grid,
