@@ -49,7 +49,7 @@ extern "C" const char *tlsrec_version_string(void)
 {
     return "tlsrec 0.2 gfx950: aes-128/192/256-gcm(L=4/8/16/64, T-tables in LDS, GHASH 4-bit position tables) "
            "aes-ccm/ccm_8(lane per record) chacha20-poly1305(L=1/2/4/8, 26-bit limbs) "
-           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer";
+           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer aria-128/192/256-gcm dtls1.2-cid";
 }
 
 extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
@@ -339,10 +339,10 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.hi = identity ? nullptr : bs.offs + base + cap;
         a.in = in;
         a.out = out;
-        a.rpw = pick_rpw(n, 16u, 8u, (uint32_t) cu);
+        a.rpw = pick_rpw(n, (uint32_t) ARIA_GCM_WAVES, 8u, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) c;
-        const uint64_t per_wg = (uint64_t) 16 * a.rpw;
+        const uint64_t per_wg = (uint64_t) ARIA_GCM_WAVES * a.rpw;
         const uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_aria_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)
             rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;

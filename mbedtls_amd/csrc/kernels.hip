@@ -1116,10 +1116,13 @@ static hipError_t launch_gcm_wp(const GcmArgs &a, uint32_t grid, hipStream_t st)
     return hipGetLastError();
 }
 
-/* ARIA-GCM: one configuration (8 lanes, 16 waves), with or without CIDs */
+/* ARIA-GCM: one configuration (8 lanes, ARIA_GCM_WAVES = 16 waves), with or
+ * without CIDs.  The ARIA round spills ~50 VGPRs at this budget; the 8-wave
+ * variant (no spills) measured 291 vs 357 GiB/s: occupancy wins. */
 template <int NR, bool DEC>
 static hipError_t launch_gcm_aria(const GcmArgs &a, uint32_t grid, hipStream_t st, bool cid)
 {
+    static_assert(ARIA_GCM_WAVES == 16, "ARIA-GCM launch shape");
     if (cid)
         hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, true, true>), dim3(grid), dim3(16 * 64), 0, st, a);
     else

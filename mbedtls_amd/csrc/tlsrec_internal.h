@@ -16,6 +16,7 @@ constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512;   /* uint4 entries per slot (5
 
 constexpr int GCM_WAVES = 16;                       /* default waves per workgroup (one WG per CU) */
 constexpr int CP_THREADS = 256;
+constexpr int ARIA_GCM_WAVES = 16;   /* waves per ARIA-GCM workgroup (kernels.hip launch_gcm_aria) */
 constexpr int CP_WAVES = CP_THREADS / 64;
 
 /* Expanded per-slot state, 1024 bytes. */
