@@ -28,7 +28,7 @@
  * is transformed in place and its data_offset / data_len / type are updated
  * exactly as the reference updates them.  Only the AEAD suites are supported
  * (AES-128/192/256-GCM, AES-128/192/256-CCM and CCM_8, ChaCha20-Poly1305,
- * ARIA-128/192/256-GCM;
+ * ARIA-128/192/256-GCM and -CCM;
  * TLS 1.2 and 1.3, and DTLS 1.2 records with an RFC 9146 connection ID).
  *
  * Every entry point that touches record data runs on the GPU; there is no CPU
@@ -77,7 +77,11 @@ extern "C" {
 #define TLSREC_CIPHER_ARIA_128_GCM       11
 #define TLSREC_CIPHER_ARIA_192_GCM       12
 #define TLSREC_CIPHER_ARIA_256_GCM       13
-#define TLSREC_CIPHER_MAX                13
+/* ARIA-CCM (PSA_KEY_TYPE_ARIA + PSA_ALG_CCM, ssl_tls.c:2241-2282), 16-byte tag */
+#define TLSREC_CIPHER_ARIA_128_CCM       14
+#define TLSREC_CIPHER_ARIA_192_CCM       15
+#define TLSREC_CIPHER_ARIA_256_CCM       16
+#define TLSREC_CIPHER_MAX                16
 
 #define TLSREC_MSG_APPLICATION_DATA  23      /* ssl.h:527 */
 #define TLSREC_MSG_CID               25      /* MBEDTLS_SSL_MSG_CID, ssl.h:528 */

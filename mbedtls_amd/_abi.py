@@ -38,7 +38,9 @@ CIPHER_AES_192_GCM = 4
 CIPHER_AES_128_CCM, CIPHER_AES_192_CCM, CIPHER_AES_256_CCM = 5, 6, 7
 CIPHER_AES_128_CCM_8, CIPHER_AES_192_CCM_8, CIPHER_AES_256_CCM_8 = 8, 9, 10
 CIPHER_ARIA_128_GCM, CIPHER_ARIA_192_GCM, CIPHER_ARIA_256_GCM = 11, 12, 13
-KEYLEN = {1: 16, 2: 32, 3: 32, 4: 24, 5: 16, 6: 24, 7: 32, 8: 16, 9: 24, 10: 32, 11: 16, 12: 24, 13: 32}
+CIPHER_ARIA_128_CCM, CIPHER_ARIA_192_CCM, CIPHER_ARIA_256_CCM = 14, 15, 16
+KEYLEN = {1: 16, 2: 32, 3: 32, 4: 24, 5: 16, 6: 24, 7: 32, 8: 16, 9: 24, 10: 32, 11: 16, 12: 24, 13: 32,
+          14: 16, 15: 24, 16: 32}
 TAGLEN = {c: (8 if 8 <= c <= 10 else 16) for c in KEYLEN}
 MSG_APPLICATION_DATA = 23
 MSG_CID = 25

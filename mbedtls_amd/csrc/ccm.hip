@@ -40,17 +40,31 @@ __device__ __forceinline__ uint32_t w4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
 
-template <int NR, bool DEC, bool CID = false>
+/* ARIA: ARIA-CCM (NR = 12/14/16; S-box tables in the same 64 KiB, round
+ * keys SlotState::ark) -- the CCM construction around it unchanged */
+template <int NR, bool ARIA, typename RK>
+__device__ __forceinline__ uint4 blk_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
+{
+    if constexpr (ARIA)
+        return aria_encrypt<NR, 0>(lds, lb, rk, in);
+    else
+        return aes_encrypt<NR, 0>(lds, lb, rk, in);
+}
+
+template <int NR, bool DEC, bool CID = false, bool ARIA = false>
 __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[65536];   /* T0/T1 x 32 copies at offset 0 */
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
+    const uint32_t lanebase = ARIA ? (uint32_t) (lane & 15) << 2 : (uint32_t) (lane & 31) << 2;
     const uint32_t lo = a.perm ? *a.lo : 0u;
     const uint32_t count = a.perm ? *a.hi - lo : (uint32_t) a.n;
     const uint64_t wg_base = (uint64_t) blockIdx.x * CCM_THREADS;
     if (wg_base >= count) return;                              /* uniform, before the barrier */
-    aes_fill_tables(lds, tid, CCM_THREADS);
+    if constexpr (ARIA)
+        aria_fill_tables(lds, tid, CCM_THREADS);
+    else
+        aes_fill_tables(lds, tid, CCM_THREADS);
     __syncthreads();
 
     /* this lane's record */
@@ -61,9 +75,11 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const uint32_t s = a.recs[my_rec].slot;
             const bool usable = s < a.capacity && a.slots[s].km.cipher != 0;
-            if (usable && tlsrec_cipher_is_ccm(a.slots[s].km.cipher) && tlsrec_cipher_nr(a.slots[s].km.cipher) == NR)
+            const int c = a.slots[s].km.cipher;
+            if (usable && (ARIA ? tlsrec_cipher_is_aria_ccm(c) && tlsrec_cipher_aria_nr(c) == NR
+                                : tlsrec_cipher_is_ccm(c) && tlsrec_cipher_nr(c) == NR))
                 my_slot = s;
-            else if (!a.perm && !usable && a.flag_nr == NR)
+            else if (!a.perm && !usable && a.flag_nr == (ARIA ? 100u + NR : (uint32_t) NR))
                 bad_slot_result(a.recs[my_rec], &a.res[my_rec]);   /* identity order: flagged by one launch */
         }
     }
@@ -74,7 +90,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
         const bool mine = my_slot == s;
         my_slot = mine ? 0xffffffffu : my_slot;
         if (!mine) continue;
-        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) a.slots[s].rkr;
+        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) (ARIA ? a.slots[s].ark : a.slots[s].rkr);
         const tlsrec_key_material km = a.slots[s].km;
         const tlsrec_batch_rec d = a.recs[my_rec];
         tlsrec_plan p;
@@ -96,7 +112,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
                        m2 = __builtin_amdgcn_alignbyte(n2, n1, 3), m3 = n2 >> 24;
         /* B0: flags = Adata | M' = (t-2)/2 | L' = q-1 = 2 */
         const uint32_t flags = 0x40u | (((taglen - 2) / 2) << 3) | 2u;
-        uint4 x = aes_encrypt<NR, 0>(lds, lanebase, rk,
+        uint4 x = blk_encrypt<NR, ARIA>(lds, lanebase, rk,
                                      make_uint4(m0 | flags, m1, m2,
                                                 m3 | w4(0, (aead_len >> 16) & 0xff, (aead_len >> 8) & 0xff,
                                                         aead_len & 0xff)));
@@ -113,12 +129,12 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
                 if (i < (int) p.aad_len) ab[2 + i] = p.aad[i];
             const uint4 a1 = make_uint4(w4(ab[0], ab[1], ab[2], ab[3]), w4(ab[4], ab[5], ab[6], ab[7]),
                                         w4(ab[8], ab[9], ab[10], ab[11]), w4(ab[12], ab[13], ab[14], ab[15]));
-            x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, a1));
+            x = blk_encrypt<NR, ARIA>(lds, lanebase, rk, xor4(x, a1));
             if (CID && p.aad_len > 14) {   /* DTLS 1.2 + CID: 23..55 AAD bytes after len16 */
                 const uint8_t *cid = a.slots[s].cid;
-                x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<1, 2>(p, d, cid)));
-                if (p.aad_len > 30) x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<2, 2>(p, d, cid)));
-                if (p.aad_len > 46) x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, cid_aad_block<3, 2>(p, d, cid)));
+                x = blk_encrypt<NR, ARIA>(lds, lanebase, rk, xor4(x, cid_aad_block<1, 2>(p, d, cid)));
+                if (p.aad_len > 30) x = blk_encrypt<NR, ARIA>(lds, lanebase, rk, xor4(x, cid_aad_block<2, 2>(p, d, cid)));
+                if (p.aad_len > 46) x = blk_encrypt<NR, ARIA>(lds, lanebase, rk, xor4(x, cid_aad_block<3, 2>(p, d, cid)));
             }
         }
         /* counter blocks: 2 || N || i24 */
@@ -133,19 +149,19 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             const bool wide = pos + 16 <= aead_len + taglen;
             const uint4 in = load_block(src, pos, content_len, aead_len, p.inner_type, wide);
             if (DEC) {
-                const uint4 ks = aes_encrypt<NR, 0>(lds, lanebase, rk, cb);
+                const uint4 ks = blk_encrypt<NR, ARIA>(lds, lanebase, rk, cb);
                 const uint4 pt = mask_block(xor4(in, ks), pos, aead_len);
                 store_block(dst, pos, aead_len, pt, true);
                 if (p.inner && (pt.x | pt.y | pt.z | pt.w)) nzpos = pos + 1;
-                x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, pt));
+                x = blk_encrypt<NR, ARIA>(lds, lanebase, rk, xor4(x, pt));
             } else {
                 /* MAC and keystream are independent: two AES chains interleave */
-                const uint4 ks = aes_encrypt<NR, 0>(lds, lanebase, rk, cb);
-                x = aes_encrypt<NR, 0>(lds, lanebase, rk, xor4(x, in));
+                const uint4 ks = blk_encrypt<NR, ARIA>(lds, lanebase, rk, cb);
+                x = blk_encrypt<NR, ARIA>(lds, lanebase, rk, xor4(x, in));
                 store_block(dst, pos, aead_len, mask_block(xor4(in, ks), pos, aead_len), true);
             }
         }
-        const uint4 s0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(c0, m1, m2, m3));
+        const uint4 s0 = blk_encrypt<NR, ARIA>(lds, lanebase, rk, make_uint4(c0, m1, m2, m3));
         const uint4 tag = xor4(x, s0);
         tlsrec_batch_res r;
         r.cid_len = 0;
@@ -203,20 +219,26 @@ extern "C" hipError_t tlsrec__launch_ccm(const CcmArgs *a, int dec, uint32_t nr_
     const uint32_t g = (uint32_t) ((a->n + CCM_THREADS - 1) / CCM_THREADS);
     if (g == 0) return hipSuccess;
     CcmArgs b = *a;
-    b.flag_nr = (nr_mask & (1u << 10)) ? 10 : (nr_mask & (1u << 12)) ? 12 : 14;
+    /* nr_mask: AES rounds at bit NR, ARIA rounds at bit NR + 4; the first
+     * variant present flags unusable slots in identity order (ARIA: 100 + NR) */
+    b.flag_nr = (nr_mask & (1u << 10)) ? 10 : (nr_mask & (1u << 12)) ? 12 : (nr_mask & (1u << 14)) ? 14
+              : (nr_mask & (1u << 16)) ? 112 : (nr_mask & (1u << 18)) ? 114 : 116;
     hipError_t e = hipSuccess;
-#define TLSREC_CCM_LAUNCH(NR)                                                                                  \
-    if (e == hipSuccess && (nr_mask & (1u << NR))) {                                                          \
+#define TLSREC_CCM_LAUNCH(NR, ARIA, BIT)                                                                      \
+    if (e == hipSuccess && (nr_mask & (1u << (BIT)))) {                                                       \
         if (b.cid) {                                                                                          \
-            if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true, true>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
-            else hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, false, true>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
-        } else if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
-        else hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, false>), dim3(g), dim3(CCM_THREADS), 0, st, b);        \
+            if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true, true, ARIA>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
+            else hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, false, true, ARIA>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
+        } else if (dec) hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, true, false, ARIA>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
+        else hipLaunchKernelGGL((tlsrec_ccm_kernel<NR, false, false, ARIA>), dim3(g), dim3(CCM_THREADS), 0, st, b); \
         e = hipGetLastError();                                                                                \
     }
-    TLSREC_CCM_LAUNCH(10)
-    TLSREC_CCM_LAUNCH(12)
-    TLSREC_CCM_LAUNCH(14)
+    TLSREC_CCM_LAUNCH(10, false, 10)
+    TLSREC_CCM_LAUNCH(12, false, 12)
+    TLSREC_CCM_LAUNCH(14, false, 14)
+    TLSREC_CCM_LAUNCH(12, true, 16)
+    TLSREC_CCM_LAUNCH(14, true, 18)
+    TLSREC_CCM_LAUNCH(16, true, 20)
 #undef TLSREC_CCM_LAUNCH
     return e;
 }

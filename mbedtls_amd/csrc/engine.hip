@@ -350,6 +350,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     uint32_t ccm_nr = 0;
     for (int c = TLSREC_CIPHER_AES_128_CCM; c <= TLSREC_CIPHER_AES_256_CCM_8; c++)
         if (kt->cipher_mask & (1u << c)) ccm_nr |= 1u << tlsrec_cipher_nr(c);
+    for (int c = TLSREC_CIPHER_ARIA_128_CCM; c <= TLSREC_CIPHER_ARIA_256_CCM; c++)   /* ARIA: bit nr + 4 */
+        if (kt->cipher_mask & (1u << c)) ccm_nr |= 1u << (tlsrec_cipher_aria_nr(c) + 4);
     if (!rc && ccm_nr) {
         CcmArgs a;
         a.slots = kt->d_slots;

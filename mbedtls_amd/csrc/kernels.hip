@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
      * the GHASH tables */
     const bool aes = tlsrec_cipher_nr(km.cipher) != 0;
     const bool aria = tlsrec_cipher_is_aria(km.cipher);
-    const bool gcm = tlsrec_cipher_is_gcm(km.cipher) || aria;
+    const bool gcm = tlsrec_cipher_is_gcm(km.cipher) || tlsrec_cipher_is_aria_gcm(km.cipher);
     if (tid == 0) {
         st->km = km;
         st->km.reserved[0] = 0;   /* CID length mirror (tlsrec_recdev.h plan_key) */
@@ -619,7 +619,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
  * after them; records without a usable slot get BAD_INPUT_DATA here.
  *   key index: AES-128-GCM -> slot, AES-256-GCM -> cap + slot, AES-192-GCM
  *   -> 2 cap + slot, AES-CCM (any size/tag) -> 3 cap + slot, ChaCha -> 4 cap,
- *   ARIA-128/192/256-GCM -> (4, 5, 6) cap + 1 + slot, none -> no index.
+ *   ARIA-128/192/256-GCM -> (4, 5, 6) cap + 1 + slot, ARIA-CCM -> the CCM
+ *   class, none -> no index.
  * Atomics are wave-aggregated when the wave's records share one key (a
  * batch already grouped by key costs one atomic per wave).
  * ==================================================================== */
@@ -636,7 +637,8 @@ __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec
         case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + 1 + d.slot;
         case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + 1 + d.slot;
         case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + 1 + d.slot;
-        default: return tlsrec_cipher_is_ccm(c) ? 3 * a.capacity + d.slot : 0xffffffffu;
+        default:
+            return (tlsrec_cipher_is_ccm(c) || tlsrec_cipher_is_aria_ccm(c)) ? 3 * a.capacity + d.slot : 0xffffffffu;
     }
 }
 

@@ -49,15 +49,17 @@
 TLSREC_HD uint32_t tlsrec_cipher_keylen(int c)
 {
     switch (c) {
-        case 1: case 5: case 8: case 11: return 16;     /* AES-128 GCM / CCM / CCM_8, ARIA-128-GCM */
-        case 4: case 6: case 9: case 12: return 24;     /* AES-192, ARIA-192 */
-        case 2: case 3: case 7: case 10: case 13: return 32;  /* AES-256, ChaCha20-Poly1305, ARIA-256 */
+        case 1: case 5: case 8: case 11: case 14: return 16;   /* AES-128 GCM / CCM / CCM_8, ARIA-128 GCM / CCM */
+        case 4: case 6: case 9: case 12: case 15: return 24;   /* AES-192, ARIA-192 */
+        case 2: case 3: case 7: case 10: case 13: case 16: return 32;  /* AES-256, ChaCha20-Poly1305, ARIA-256 */
         default: return 0;
     }
 }
 TLSREC_HD uint32_t tlsrec_cipher_taglen(int c) { return (c >= 8 && c <= 10) ? 8u : 16u; }
 TLSREC_HD int tlsrec_cipher_is_gcm(int c) { return c == 1 || c == 2 || c == 4; }   /* AES-GCM */
-TLSREC_HD int tlsrec_cipher_is_aria(int c) { return c >= 11 && c <= 13; }           /* ARIA-GCM */
+TLSREC_HD int tlsrec_cipher_is_aria_gcm(int c) { return c >= 11 && c <= 13; }      /* ARIA-GCM */
+TLSREC_HD int tlsrec_cipher_is_aria_ccm(int c) { return c >= 14 && c <= 16; }      /* ARIA-CCM */
+TLSREC_HD int tlsrec_cipher_is_aria(int c) { return c >= 11 && c <= 16; }          /* ARIA, any mode */
 /* ARIA rounds (RFC 5794 2.1): 12 / 14 / 16 */
 TLSREC_HD uint32_t tlsrec_cipher_aria_nr(int c) { return tlsrec_cipher_is_aria(c) ? tlsrec_cipher_keylen(c) / 4 + 8 : 0u; }
 TLSREC_HD int tlsrec_cipher_is_ccm(int c) { return c >= 5 && c <= 10; }

@@ -31,9 +31,11 @@ AES_192_GCM = 4
 AES_128_CCM, AES_192_CCM, AES_256_CCM = 5, 6, 7
 AES_128_CCM_8, AES_192_CCM_8, AES_256_CCM_8 = 8, 9, 10
 ARIA_128_GCM, ARIA_192_GCM, ARIA_256_GCM = 11, 12, 13
+ARIA_128_CCM, ARIA_192_CCM, ARIA_256_CCM = 14, 15, 16
 KEYLEN = {AES_128_GCM: 16, AES_256_GCM: 32, CHACHA20_POLY1305: 32, AES_192_GCM: 24, AES_128_CCM: 16,
           AES_192_CCM: 24, AES_256_CCM: 32, AES_128_CCM_8: 16, AES_192_CCM_8: 24, AES_256_CCM_8: 32,
-          ARIA_128_GCM: 16, ARIA_192_GCM: 24, ARIA_256_GCM: 32}
+          ARIA_128_GCM: 16, ARIA_192_GCM: 24, ARIA_256_GCM: 32,
+          ARIA_128_CCM: 16, ARIA_192_CCM: 24, ARIA_256_CCM: 32}
 TAGLEN = {c: (8 if AES_128_CCM_8 <= c <= AES_256_CCM_8 else 16) for c in KEYLEN}
 
 _lib = None

@@ -636,9 +636,9 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
         case ORC_CIPHER_AES_256_GCM: case ORC_CIPHER_AES_256_CCM: case ORC_CIPHER_AES_256_CCM_8:
         case ORC_CIPHER_CHACHA20_POLY1305: t->keylen = 32; break;
         /* ARIA-GCM (PSA_KEY_TYPE_ARIA + PSA_ALG_GCM, ssl_tls.c:2248-2289) */
-        case ORC_CIPHER_ARIA_128_GCM: t->keylen = 16; break;
-        case ORC_CIPHER_ARIA_192_GCM: t->keylen = 24; break;
-        case ORC_CIPHER_ARIA_256_GCM: t->keylen = 32; break;
+        case ORC_CIPHER_ARIA_128_GCM: case ORC_CIPHER_ARIA_128_CCM: t->keylen = 16; break;
+        case ORC_CIPHER_ARIA_192_GCM: case ORC_CIPHER_ARIA_192_CCM: t->keylen = 24; break;
+        case ORC_CIPHER_ARIA_256_GCM: case ORC_CIPHER_ARIA_256_CCM: t->keylen = 32; break;
         default: return ORC_ERR_SSL_FEATURE_UNAVAILABLE;
     }
     t->ivlen = 12;
@@ -746,7 +746,11 @@ static int parse_inner(const uint8_t *data, size_t *len, uint8_t *type)
     return 0;
 }
 
-static int is_ccm(int c) { return c >= ORC_CIPHER_AES_128_CCM && c <= ORC_CIPHER_AES_256_CCM_8; }
+static int is_ccm(int c)
+{
+    return (c >= ORC_CIPHER_AES_128_CCM && c <= ORC_CIPHER_AES_256_CCM_8) ||
+           (c >= ORC_CIPHER_ARIA_128_CCM && c <= ORC_CIPHER_ARIA_256_CCM);
+}
 
 static void aead_seal(const orc_transform *t, const uint8_t nonce[12],
                       const uint8_t *aad, size_t aad_len, uint8_t *data, size_t len)

@@ -78,6 +78,10 @@ extern "C" {
 #define ORC_CIPHER_ARIA_128_GCM       11
 #define ORC_CIPHER_ARIA_192_GCM       12
 #define ORC_CIPHER_ARIA_256_GCM       13
+/* ARIA-CCM (PSA_ALG_CCM with PSA_KEY_TYPE_ARIA, ssl_tls.c:2241-2282), 16-byte tag */
+#define ORC_CIPHER_ARIA_128_CCM       14
+#define ORC_CIPHER_ARIA_192_CCM       15
+#define ORC_CIPHER_ARIA_256_CCM       16
 
 #define ORC_OUT_CONTENT_LEN 16384     /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
 

@@ -30,6 +30,7 @@ def lib():
         L.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
         L.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
         for f in ("EVP_aria_128_gcm", "EVP_aria_192_gcm", "EVP_aria_256_gcm", "EVP_aria_128_ecb",
+                  "EVP_aria_128_ccm", "EVP_aria_192_ccm", "EVP_aria_256_ccm",
                   "EVP_aes_128_gcm", "EVP_aes_192_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305",
                   "EVP_aes_128_ccm", "EVP_aes_192_ccm", "EVP_aes_256_ccm"):
             getattr(L, f).restype = ctypes.c_void_p
@@ -57,6 +58,8 @@ def _cipher(name: str, keylen: int):
         return {16: L.EVP_aes_128_gcm, 24: L.EVP_aes_192_gcm, 32: L.EVP_aes_256_gcm}[keylen]()
     if name == "aria-gcm":
         return {16: L.EVP_aria_128_gcm, 24: L.EVP_aria_192_gcm, 32: L.EVP_aria_256_gcm}[keylen]()
+    if name == "aria-ccm":
+        return {16: L.EVP_aria_128_ccm, 24: L.EVP_aria_192_ccm, 32: L.EVP_aria_256_ccm}[keylen]()
     if name == "ccm":
         return {16: L.EVP_aes_128_ccm, 24: L.EVP_aes_192_ccm, 32: L.EVP_aes_256_ccm}[keylen]()
     return L.EVP_chacha20_poly1305()
@@ -114,12 +117,13 @@ def open_(name: str, key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes
         L.EVP_CIPHER_CTX_free(ctx)
 
 
-def ccm_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes, tag_len: int):
-    """AES-CCM through EVP (length-first call sequence of the CCM mode)."""
+def ccm_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes, tag_len: int, name: str = "ccm"):
+    """AES-CCM (or ARIA-CCM, name="aria-ccm") through EVP (length-first call
+    sequence of the CCM mode)."""
     L = lib()
     ctx = L.EVP_CIPHER_CTX_new()
     try:
-        assert L.EVP_EncryptInit_ex(ctx, _cipher("ccm", len(key)), None, None, None) == 1
+        assert L.EVP_EncryptInit_ex(ctx, _cipher(name, len(key)), None, None, None) == 1
         assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_IVLEN, len(nonce), None) == 1
         assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_TAG, tag_len, None) == 1
         assert L.EVP_EncryptInit_ex(ctx, None, None, key, nonce) == 1

@@ -1,4 +1,4 @@
-"""ARIA-GCM in the CPU restatement (the ARIA entries of
+"""ARIA-GCM and ARIA-CCM in the CPU restatement (the ARIA entries of
 mbedtls_ssl_cipher_to_psa, library/ssl_tls.c:2248-2289).
 
 ARIA itself lives in the absent TF-PSA-Crypto; oracle/aria.c restates RFC 5794.
@@ -17,7 +17,8 @@ from tests import _openssl as S
 from tests.prng import prng_bytes
 from tests.test_cid_oracle import build_cid_transforms
 
-ARIA = {"aria128gcm": O.ARIA_128_GCM, "aria192gcm": O.ARIA_192_GCM, "aria256gcm": O.ARIA_256_GCM}
+ARIA = {"aria128gcm": O.ARIA_128_GCM, "aria192gcm": O.ARIA_192_GCM, "aria256gcm": O.ARIA_256_GCM,
+        "aria128ccm": O.ARIA_128_CCM, "aria192ccm": O.ARIA_192_CCM, "aria256ccm": O.ARIA_256_CCM}
 h = bytes.fromhex
 
 
@@ -67,7 +68,10 @@ def test_aria_records_vs_openssl(cipher):
         rec = O.Record(ctr=ctr, type=23, ver=b"\x03\x03", buf=buf, data_offset=8, data_len=n)
         assert t.encrypt_buf(rec) == 0
         aad = ctr + b"\x17\x03\x03" + n.to_bytes(2, "big")
-        ct, tag = S.seal("aria-gcm", key, iv[:4] + ctr, aad, content)
+        if cipher >= O.ARIA_128_CCM:
+            ct, tag = S.ccm_seal(key, iv[:4] + ctr, aad, content, 16, name="aria-ccm")
+        else:
+            ct, tag = S.seal("aria-gcm", key, iv[:4] + ctr, aad, content)
         assert rec.data() == ctr + ct + tag
 
 
