@@ -110,7 +110,10 @@ CIPHERS = {"AES-128-GCM": O.AES_128_GCM, "AES-256-GCM": O.AES_256_GCM,
            # SURVEY 8(f)-2 (appended: the seeds of the cases above stay unchanged)
            "AES-192-GCM": O.AES_192_GCM, "AES-128-CCM": O.AES_128_CCM, "AES-192-CCM": O.AES_192_CCM,
            "AES-256-CCM": O.AES_256_CCM, "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-CCM-8": O.AES_192_CCM_8,
-           "AES-256-CCM-8": O.AES_256_CCM_8}
+           "AES-256-CCM-8": O.AES_256_CCM_8,
+           # ARIA-GCM / ARIA-CCM (appended likewise)
+           "ARIA-128-GCM": O.ARIA_128_GCM, "ARIA-192-GCM": O.ARIA_192_GCM, "ARIA-256-GCM": O.ARIA_256_GCM,
+           "ARIA-128-CCM": O.ARIA_128_CCM, "ARIA-192-CCM": O.ARIA_192_CCM, "ARIA-256-CCM": O.ARIA_256_CCM}
 VERSIONS = {"TLS1.2": O.TLS1_2, "TLS1.3": O.TLS1_3}
 LENGTHS = [0, 1, 15, 16, 17, 1400, 16383]
 SEED = 0x7115EC0DE
@@ -166,6 +169,10 @@ def make_records():
                     tl = O.TAGLEN[c]
                     if O.AES_128_CCM <= c <= O.AES_256_CCM_8:
                         ct, tag = S.ccm_seal(key_enc, nonce, aad, inner, tl)
+                    elif c >= O.ARIA_128_CCM:
+                        ct, tag = S.ccm_seal(key_enc, nonce, aad, inner, tl, name="aria-ccm")
+                    elif c >= O.ARIA_128_GCM:
+                        ct, tag = S.seal("aria-gcm", key_enc, nonce, aad, inner)
                     else:
                         name = "gcm" if c != O.CHACHA20_POLY1305 else "chacha"
                         ct, tag = S.seal(name, key_enc, nonce, aad, inner)

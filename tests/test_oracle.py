@@ -76,7 +76,9 @@ def test_standard_vectors():
 CIPHERS = {"AES-128-GCM": O.AES_128_GCM, "AES-256-GCM": O.AES_256_GCM,
            "CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-192-GCM": O.AES_192_GCM,
            "AES-128-CCM": O.AES_128_CCM, "AES-192-CCM": O.AES_192_CCM, "AES-256-CCM": O.AES_256_CCM,
-           "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-CCM-8": O.AES_192_CCM_8, "AES-256-CCM-8": O.AES_256_CCM_8}
+           "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-CCM-8": O.AES_192_CCM_8, "AES-256-CCM-8": O.AES_256_CCM_8,
+           "ARIA-128-GCM": O.ARIA_128_GCM, "ARIA-192-GCM": O.ARIA_192_GCM, "ARIA-256-GCM": O.ARIA_256_GCM,
+           "ARIA-128-CCM": O.ARIA_128_CCM, "ARIA-192-CCM": O.ARIA_192_CCM, "ARIA-256-CCM": O.ARIA_256_CCM}
 VERSIONS = {"TLS1.2": O.TLS1_2, "TLS1.3": O.TLS1_3}
 
 
