@@ -32,10 +32,14 @@ AES_128_CCM, AES_192_CCM, AES_256_CCM = 5, 6, 7
 AES_128_CCM_8, AES_192_CCM_8, AES_256_CCM_8 = 8, 9, 10
 ARIA_128_GCM, ARIA_192_GCM, ARIA_256_GCM = 11, 12, 13
 ARIA_128_CCM, ARIA_192_CCM, ARIA_256_CCM = 14, 15, 16
+CAMELLIA_128_GCM, CAMELLIA_192_GCM, CAMELLIA_256_GCM = 17, 18, 19
+CAMELLIA_128_CCM, CAMELLIA_192_CCM, CAMELLIA_256_CCM = 20, 21, 22
 KEYLEN = {AES_128_GCM: 16, AES_256_GCM: 32, CHACHA20_POLY1305: 32, AES_192_GCM: 24, AES_128_CCM: 16,
           AES_192_CCM: 24, AES_256_CCM: 32, AES_128_CCM_8: 16, AES_192_CCM_8: 24, AES_256_CCM_8: 32,
           ARIA_128_GCM: 16, ARIA_192_GCM: 24, ARIA_256_GCM: 32,
-          ARIA_128_CCM: 16, ARIA_192_CCM: 24, ARIA_256_CCM: 32}
+          ARIA_128_CCM: 16, ARIA_192_CCM: 24, ARIA_256_CCM: 32,
+          CAMELLIA_128_GCM: 16, CAMELLIA_192_GCM: 24, CAMELLIA_256_GCM: 32,
+          CAMELLIA_128_CCM: 16, CAMELLIA_192_CCM: 24, CAMELLIA_256_CCM: 32}
 TAGLEN = {c: (8 if AES_128_CCM_8 <= c <= AES_256_CCM_8 else 16) for c in KEYLEN}
 
 _lib = None
@@ -106,11 +110,25 @@ def aria_encrypt_block(key: bytes, block: bytes) -> bytes:
     return out.raw
 
 
-def aria_gcm_encrypt(key: bytes, iv: bytes, aad: bytes, pt: bytes):
+def camellia_encrypt_block(key: bytes, block: bytes) -> bytes:
+    """Camellia (RFC 3713), oracle/camellia.c."""
+    f = lib().orc_camellia_setkey_enc
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint]
+    ctx = _buf(1024)
+    assert f(ctx, key, len(key) * 8) == 0
+    out = _buf(16)
+    g = lib().orc_camellia_encrypt_block
+    g.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    g(ctx, block, out)
+    return out.raw
+
+
+def aria_gcm_encrypt(key: bytes, iv: bytes, aad: bytes, pt: bytes, bc: int = 1):
+    """GCM over ARIA (bc 1) or Camellia (bc 2)."""
     f = lib().orc_gcm_setkey_ex
     f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint, ctypes.c_int]
     ctx = _buf(_GCM_CTX)
-    assert f(ctx, key, len(key) * 8, 1) == 0
+    assert f(ctx, key, len(key) * 8, bc) == 0
     out, tag = _buf(max(1, len(pt))), _buf(16)
     lib().orc_gcm_encrypt(ctx, iv, aad, len(aad), pt, len(pt), out, tag, 16)
     return out.raw[:len(pt)], tag.raw

@@ -129,6 +129,10 @@ void orc_aes_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t
         orc_aria_encrypt_block(ctx, in, out);
         return;
     }
+    if (ctx->kind == 2) {               /* Camellia (camellia.c) */
+        orc_camellia_encrypt_block(ctx, in, out);
+        return;
+    }
     const uint32_t *rk = ctx->rk;
     uint32_t s[4], t[4];
     for (int c = 0; c < 4; c++) s[c] = ld32le(in + 4 * c) ^ rk[c];
@@ -193,11 +197,12 @@ int orc_gcm_setkey(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits)
     return orc_gcm_setkey_ex(ctx, key, keybits, 0);
 }
 
-int orc_gcm_setkey_ex(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits, int aria)
+int orc_gcm_setkey_ex(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits, int bc)
 {
     static const uint8_t zero[16] = { 0 };
     pthread_once(&g_once4, last4_init);
-    if ((aria ? orc_aria_setkey_enc(&ctx->aes, key, keybits) : orc_aes_setkey_enc(&ctx->aes, key, keybits)) != 0)
+    if ((bc == 2 ? orc_camellia_setkey_enc(&ctx->aes, key, keybits)
+         : bc ? orc_aria_setkey_enc(&ctx->aes, key, keybits) : orc_aes_setkey_enc(&ctx->aes, key, keybits)) != 0)
         return -1;
     orc_aes_encrypt_block(&ctx->aes, zero, ctx->h);
     uint64_t hi = ld64be(ctx->h), lo = ld64be(ctx->h + 8);
@@ -639,6 +644,10 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
         case ORC_CIPHER_ARIA_128_GCM: case ORC_CIPHER_ARIA_128_CCM: t->keylen = 16; break;
         case ORC_CIPHER_ARIA_192_GCM: case ORC_CIPHER_ARIA_192_CCM: t->keylen = 24; break;
         case ORC_CIPHER_ARIA_256_GCM: case ORC_CIPHER_ARIA_256_CCM: t->keylen = 32; break;
+        /* Camellia-GCM / -CCM (PSA_KEY_TYPE_CAMELLIA, ssl_tls.c:2297-2345) */
+        case ORC_CIPHER_CAMELLIA_128_GCM: case ORC_CIPHER_CAMELLIA_128_CCM: t->keylen = 16; break;
+        case ORC_CIPHER_CAMELLIA_192_GCM: case ORC_CIPHER_CAMELLIA_192_CCM: t->keylen = 24; break;
+        case ORC_CIPHER_CAMELLIA_256_GCM: case ORC_CIPHER_CAMELLIA_256_CCM: t->keylen = 32; break;
         default: return ORC_ERR_SSL_FEATURE_UNAVAILABLE;
     }
     t->ivlen = 12;
@@ -659,9 +668,9 @@ int orc_transform_setup(orc_transform *t, int tls_version, int cipher,
     memcpy(t->iv_enc, iv_enc, 16);
     memcpy(t->iv_dec, iv_dec, 16);
     if (cipher != ORC_CIPHER_CHACHA20_POLY1305) {
-        const int aria = cipher >= ORC_CIPHER_ARIA_128_GCM;
-        orc_gcm_setkey_ex(&t->gcm_enc, key_enc, (unsigned) t->keylen * 8, aria);
-        orc_gcm_setkey_ex(&t->gcm_dec, key_dec, (unsigned) t->keylen * 8, aria);
+        const int bc = cipher >= ORC_CIPHER_CAMELLIA_128_GCM ? 2 : cipher >= ORC_CIPHER_ARIA_128_GCM ? 1 : 0;
+        orc_gcm_setkey_ex(&t->gcm_enc, key_enc, (unsigned) t->keylen * 8, bc);
+        orc_gcm_setkey_ex(&t->gcm_dec, key_dec, (unsigned) t->keylen * 8, bc);
     }
     return 0;
 }
@@ -749,7 +758,8 @@ static int parse_inner(const uint8_t *data, size_t *len, uint8_t *type)
 static int is_ccm(int c)
 {
     return (c >= ORC_CIPHER_AES_128_CCM && c <= ORC_CIPHER_AES_256_CCM_8) ||
-           (c >= ORC_CIPHER_ARIA_128_CCM && c <= ORC_CIPHER_ARIA_256_CCM);
+           (c >= ORC_CIPHER_ARIA_128_CCM && c <= ORC_CIPHER_ARIA_256_CCM) ||
+           (c >= ORC_CIPHER_CAMELLIA_128_CCM && c <= ORC_CIPHER_CAMELLIA_256_CCM);
 }
 
 static void aead_seal(const orc_transform *t, const uint8_t nonce[12],

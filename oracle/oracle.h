@@ -82,12 +82,20 @@ extern "C" {
 #define ORC_CIPHER_ARIA_128_CCM       14
 #define ORC_CIPHER_ARIA_192_CCM       15
 #define ORC_CIPHER_ARIA_256_CCM       16
+/* Camellia-GCM / -CCM (PSA_KEY_TYPE_CAMELLIA, ssl_tls.c:2297-2345; RFC 6367 suites) */
+#define ORC_CIPHER_CAMELLIA_128_GCM   17
+#define ORC_CIPHER_CAMELLIA_192_GCM   18
+#define ORC_CIPHER_CAMELLIA_256_GCM   19
+#define ORC_CIPHER_CAMELLIA_128_CCM   20
+#define ORC_CIPHER_CAMELLIA_192_CCM   21
+#define ORC_CIPHER_CAMELLIA_256_CCM   22
 
 #define ORC_OUT_CONTENT_LEN 16384     /* MBEDTLS_SSL_OUT_CONTENT_LEN, ssl.h:409 */
 
 /* ---- primitives ------------------------------------------------------- */
-/* Block-cipher context of the GCM / CCM code: AES (kind 0) or ARIA (kind 1,
- * oracle/aria.c; nr = 12/14/16 rounds, ark = the nr + 1 round keys). */
+/* Block-cipher context of the GCM / CCM code: AES (kind 0), ARIA (kind 1,
+ * oracle/aria.c; nr = 12/14/16 rounds, ark = the nr + 1 round keys) or
+ * Camellia (kind 2, oracle/camellia.c; nr = 18/24, ark = the 64-bit subkeys). */
 typedef struct {
     uint32_t rk[60];
     int nr;
@@ -101,6 +109,10 @@ void orc_aes_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t
 int  orc_aria_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits);
 void orc_aria_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t out[16]);
 const uint8_t *orc_aria_sbox(int i);   /* SB1..SB4 as i = 0..3 */
+/* Camellia (RFC 3713) in the same context type */
+int  orc_camellia_setkey_enc(orc_aes_ctx *ctx, const uint8_t *key, unsigned keybits);
+void orc_camellia_encrypt_block(const orc_aes_ctx *ctx, const uint8_t in[16], uint8_t out[16]);
+const uint8_t *orc_camellia_sbox1(void);
 const uint8_t *orc_aes_sbox(void);
 
 typedef struct {
@@ -110,8 +122,8 @@ typedef struct {
 } orc_gcm_ctx;
 
 int  orc_gcm_setkey(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits);
-/* GCM over ARIA (aria != 0) or AES */
-int  orc_gcm_setkey_ex(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits, int aria);
+/* GCM over AES (bc 0), ARIA (bc 1) or Camellia (bc 2) */
+int  orc_gcm_setkey_ex(orc_gcm_ctx *ctx, const uint8_t *key, unsigned keybits, int bc);
 void orc_ghash_mult(const orc_gcm_ctx *ctx, const uint8_t x[16], uint8_t out[16]);
 /* one-shot GCM with a 12-byte IV; tag_len <= 16 */
 void orc_gcm_encrypt(const orc_gcm_ctx *ctx, const uint8_t iv[12],

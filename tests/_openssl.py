@@ -32,7 +32,9 @@ def lib():
         for f in ("EVP_aria_128_gcm", "EVP_aria_192_gcm", "EVP_aria_256_gcm", "EVP_aria_128_ecb",
                   "EVP_aria_128_ccm", "EVP_aria_192_ccm", "EVP_aria_256_ccm",
                   "EVP_aes_128_gcm", "EVP_aes_192_gcm", "EVP_aes_256_gcm", "EVP_chacha20_poly1305",
-                  "EVP_aes_128_ccm", "EVP_aes_192_ccm", "EVP_aes_256_ccm"):
+                  "EVP_aes_128_ccm", "EVP_aes_192_ccm", "EVP_aes_256_ccm",
+                  "EVP_camellia_128_ecb", "EVP_camellia_192_ecb", "EVP_camellia_256_ecb",
+                  "EVP_camellia_128_cbc", "EVP_camellia_192_cbc", "EVP_camellia_256_cbc"):
             getattr(L, f).restype = ctypes.c_void_p
         L.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_char_p, ctypes.c_char_p]
@@ -44,6 +46,7 @@ def lib():
         L.EVP_DecryptUpdate.argtypes = upd
         L.EVP_EncryptFinal_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         L.EVP_DecryptFinal_ex.argtypes = L.EVP_EncryptFinal_ex.argtypes
+        L.EVP_CIPHER_CTX_set_padding.argtypes = [ctypes.c_void_p, ctypes.c_int]
     return _lib
 
 
@@ -138,5 +141,22 @@ def ccm_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes, tag_len: int, name
         tag = ctypes.create_string_buffer(16)
         assert L.EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, tag_len, tag) == 1
         return out.raw[:total], tag.raw[:tag_len]
+    finally:
+        L.EVP_CIPHER_CTX_free(ctx)
+
+
+def camellia(key: bytes, data: bytes, mode: str = "ecb", iv: bytes | None = None) -> bytes:
+    """Camellia-ECB / -CBC (no padding) with OpenSSL, for whole blocks.  OpenSSL
+    has no Camellia-GCM / -CCM; the tests build those modes around this."""
+    L = lib()
+    c = getattr(L, f"EVP_camellia_{len(key) * 8}_{mode}")()
+    ctx = L.EVP_CIPHER_CTX_new()
+    try:
+        assert L.EVP_EncryptInit_ex(ctx, c, None, key, iv) == 1
+        L.EVP_CIPHER_CTX_set_padding(ctx, 0)
+        out = ctypes.create_string_buffer(len(data) + 16)
+        n = ctypes.c_int(0)
+        assert L.EVP_EncryptUpdate(ctx, out, ctypes.byref(n), data, len(data)) == 1
+        return out.raw[:n.value]
     finally:
         L.EVP_CIPHER_CTX_free(ctx)
