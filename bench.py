@@ -50,6 +50,8 @@ CONFIGS = {
                "AES-192-GCM decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
     "aria256": ("ARIA-256-GCM", "TLS1.2", "decrypt", 16384, 1 << 20, 1,
                 "ARIA-256-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
+    "camellia128": ("CAMELLIA-128-GCM", "TLS1.2", "decrypt", 16384, 1 << 20, 1,
+                    "Camellia-128-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
     "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
             "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 1.4 KiB TLS 1.3 decrypt"),
 }
@@ -107,7 +109,7 @@ def main():
     ciphers = {"AES-128-GCM": [M.CIPHER_AES_128_GCM], "AES-256-GCM": [M.CIPHER_AES_256_GCM],
                "AES-128-CCM": [M.CIPHER_AES_128_CCM], "AES-128-CCM-8": [M.CIPHER_AES_128_CCM_8],
                "AES-192-GCM": [M.CIPHER_AES_192_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
-               "ARIA-256-GCM": [M.CIPHER_ARIA_256_GCM],
+               "ARIA-256-GCM": [M.CIPHER_ARIA_256_GCM], "CAMELLIA-128-GCM": [M.CIPHER_CAMELLIA_128_GCM],
                "MIX": [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305]}[cname]
     nkeys = min(nkeys, n)
 
@@ -291,7 +293,7 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
     import oracle as O
     cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM, "AES-128-CCM": O.AES_128_CCM,
               "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-GCM": O.AES_192_GCM,
-              "ARIA-256-GCM": O.ARIA_256_GCM}.get(cname, O.AES_256_GCM)
+              "ARIA-256-GCM": O.ARIA_256_GCM, "CAMELLIA-128-GCM": O.CAMELLIA_128_GCM}.get(cname, O.AES_256_GCM)
     k = km[0]
     klen = O.KEYLEN[cipher]
     t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"][:klen]),
@@ -329,7 +331,8 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
         reps += 1
     n *= reps
     gib = n * inner / el / 2**30
-    impl = {"CHACHA20-POLY1305": "ChaCha20 + 44-bit-limb Poly1305", "ARIA-256-GCM": "byte-wise ARIA + 4-bit Shoup GHASH"}.get(
+    impl = {"CHACHA20-POLY1305": "ChaCha20 + 44-bit-limb Poly1305", "ARIA-256-GCM": "byte-wise ARIA + 4-bit Shoup GHASH",
+            "CAMELLIA-128-GCM": "byte-wise Camellia + 4-bit Shoup GHASH"}.get(
         cname, "table AES + 4-bit Shoup GHASH" if "GCM" in cname else "table AES CCM")
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{n} records ({reps} passes) x {inner} B inner plaintext, {direction}, oracle/liboracle.so "

@@ -81,7 +81,15 @@ extern "C" {
 #define TLSREC_CIPHER_ARIA_128_CCM       14
 #define TLSREC_CIPHER_ARIA_192_CCM       15
 #define TLSREC_CIPHER_ARIA_256_CCM       16
-#define TLSREC_CIPHER_MAX                16
+/* Camellia-GCM / -CCM (RFC 3713 block cipher; PSA_KEY_TYPE_CAMELLIA with
+ * PSA_ALG_GCM / PSA_ALG_CCM, ssl_tls.c:2297-2345; the RFC 6367 suites), 16-byte tag */
+#define TLSREC_CIPHER_CAMELLIA_128_GCM   17
+#define TLSREC_CIPHER_CAMELLIA_192_GCM   18
+#define TLSREC_CIPHER_CAMELLIA_256_GCM   19
+#define TLSREC_CIPHER_CAMELLIA_128_CCM   20
+#define TLSREC_CIPHER_CAMELLIA_192_CCM   21
+#define TLSREC_CIPHER_CAMELLIA_256_CCM   22
+#define TLSREC_CIPHER_MAX                22
 
 #define TLSREC_MSG_APPLICATION_DATA  23      /* ssl.h:527 */
 #define TLSREC_MSG_CID               25      /* MBEDTLS_SSL_MSG_CID, ssl.h:528 */

@@ -39,8 +39,10 @@ CIPHER_AES_128_CCM, CIPHER_AES_192_CCM, CIPHER_AES_256_CCM = 5, 6, 7
 CIPHER_AES_128_CCM_8, CIPHER_AES_192_CCM_8, CIPHER_AES_256_CCM_8 = 8, 9, 10
 CIPHER_ARIA_128_GCM, CIPHER_ARIA_192_GCM, CIPHER_ARIA_256_GCM = 11, 12, 13
 CIPHER_ARIA_128_CCM, CIPHER_ARIA_192_CCM, CIPHER_ARIA_256_CCM = 14, 15, 16
+CIPHER_CAMELLIA_128_GCM, CIPHER_CAMELLIA_192_GCM, CIPHER_CAMELLIA_256_GCM = 17, 18, 19
+CIPHER_CAMELLIA_128_CCM, CIPHER_CAMELLIA_192_CCM, CIPHER_CAMELLIA_256_CCM = 20, 21, 22
 KEYLEN = {1: 16, 2: 32, 3: 32, 4: 24, 5: 16, 6: 24, 7: 32, 8: 16, 9: 24, 10: 32, 11: 16, 12: 24, 13: 32,
-          14: 16, 15: 24, 16: 32}
+          14: 16, 15: 24, 16: 32, 17: 16, 18: 24, 19: 32, 20: 16, 21: 24, 22: 32}
 TAGLEN = {c: (8 if 8 <= c <= 10 else 16) for c in KEYLEN}
 MSG_APPLICATION_DATA = 23
 MSG_CID = 25

@@ -46,7 +46,7 @@ template <int NR, bool ARIA, typename RK>
 __device__ __forceinline__ uint4 blk_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
 {
     if constexpr (ARIA)
-        return aria_encrypt<NR, 0>(lds, lb, rk, in);
+        return alt_encrypt<NR, 0>(lds, lb, rk, in);
     else
         return aes_encrypt<NR, 0>(lds, lb, rk, in);
 }
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
     const uint64_t wg_base = (uint64_t) blockIdx.x * CCM_THREADS;
     if (wg_base >= count) return;                              /* uniform, before the barrier */
     if constexpr (ARIA)
-        aria_fill_tables(lds, tid, CCM_THREADS);
+        alt_fill_tables<NR>(lds, tid, CCM_THREADS);
     else
         aes_fill_tables(lds, tid, CCM_THREADS);
     __syncthreads();
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             const uint32_t s = a.recs[my_rec].slot;
             const bool usable = s < a.capacity && a.slots[s].km.cipher != 0;
             const int c = a.slots[s].km.cipher;
-            if (usable && (ARIA ? tlsrec_cipher_is_aria_ccm(c) && tlsrec_cipher_aria_nr(c) == NR
+            if (usable && (ARIA ? tlsrec_cipher_is_alt_ccm(c) && tlsrec_cipher_alt_nr(c) == NR
                                 : tlsrec_cipher_is_ccm(c) && tlsrec_cipher_nr(c) == NR))
                 my_slot = s;
             else if (!a.perm && !usable && a.flag_nr == (ARIA ? 100u + NR : (uint32_t) NR))
@@ -219,10 +219,12 @@ extern "C" hipError_t tlsrec__launch_ccm(const CcmArgs *a, int dec, uint32_t nr_
     const uint32_t g = (uint32_t) ((a->n + CCM_THREADS - 1) / CCM_THREADS);
     if (g == 0) return hipSuccess;
     CcmArgs b = *a;
-    /* nr_mask: AES rounds at bit NR, ARIA rounds at bit NR + 4; the first
-     * variant present flags unusable slots in identity order (ARIA: 100 + NR) */
+    /* nr_mask: AES rounds at bit NR, ARIA / Camellia rounds at bit NR + 4; the
+     * first variant present flags unusable slots in identity order (ARIA and
+     * Camellia: 100 + NR) */
     b.flag_nr = (nr_mask & (1u << 10)) ? 10 : (nr_mask & (1u << 12)) ? 12 : (nr_mask & (1u << 14)) ? 14
-              : (nr_mask & (1u << 16)) ? 112 : (nr_mask & (1u << 18)) ? 114 : 116;
+              : (nr_mask & (1u << 16)) ? 112 : (nr_mask & (1u << 18)) ? 114 : (nr_mask & (1u << 20)) ? 116
+              : (nr_mask & (1u << 22)) ? 118 : 124;
     hipError_t e = hipSuccess;
 #define TLSREC_CCM_LAUNCH(NR, ARIA, BIT)                                                                      \
     if (e == hipSuccess && (nr_mask & (1u << (BIT)))) {                                                       \
@@ -239,6 +241,8 @@ extern "C" hipError_t tlsrec__launch_ccm(const CcmArgs *a, int dec, uint32_t nr_
     TLSREC_CCM_LAUNCH(12, true, 16)
     TLSREC_CCM_LAUNCH(14, true, 18)
     TLSREC_CCM_LAUNCH(16, true, 20)
+    TLSREC_CCM_LAUNCH(18, true, 22)     /* Camellia-128 */
+    TLSREC_CCM_LAUNCH(24, true, 28)     /* Camellia-192 / -256 */
 #undef TLSREC_CCM_LAUNCH
     return e;
 }

@@ -49,7 +49,7 @@ extern "C" const char *tlsrec_version_string(void)
 {
     return "tlsrec 0.2 gfx950: aes-128/192/256-gcm(L=4/8/16/64, T-tables in LDS, GHASH 4-bit position tables) "
            "aes-ccm/ccm_8(lane per record) chacha20-poly1305(L=1/2/4/8, 26-bit limbs) "
-           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer aria-128/192/256-gcm dtls1.2-cid";
+           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer aria-128/192/256-gcm/ccm camellia-128/192/256-gcm/ccm dtls1.2-cid";
 }
 
 extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
@@ -225,8 +225,9 @@ struct BucketScratch {
 static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
                   hipStream_t st, BucketScratch &b)
 {
-    /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, ARIA-128/192/256-GCM slots, end */
-    const size_t nk = 7 * (size_t) kt->capacity + 2;
+    /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, ARIA-128/192/256-GCM,
+     * Camellia-128/192/256-GCM slots, end */
+    const size_t nk = 10 * (size_t) kt->capacity + 2;
     b.scan_bytes = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, b.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
                                          (int) nk, st) != hipSuccess)
@@ -323,11 +324,15 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
             rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    /* ARIA-GCM: the GCM kernel around ARIA (8 lanes, 16 waves); bucket classes
-     * (4, 5, 6) cap + 1 */
-    for (int c = TLSREC_CIPHER_ARIA_128_GCM; c <= TLSREC_CIPHER_ARIA_256_GCM && !rc; c++) {
+    /* ARIA-GCM and Camellia-GCM: the GCM kernel around the LDS-table cipher
+     * (8 lanes, 16 waves); bucket classes (4, 5, 6) cap + 1 and (7, 8, 9) cap + 1 */
+    static const int alt_gcm[6] = { TLSREC_CIPHER_ARIA_128_GCM, TLSREC_CIPHER_ARIA_192_GCM, TLSREC_CIPHER_ARIA_256_GCM,
+                                    TLSREC_CIPHER_CAMELLIA_128_GCM, TLSREC_CIPHER_CAMELLIA_192_GCM,
+                                    TLSREC_CIPHER_CAMELLIA_256_GCM };
+    for (int ci = 0; ci < 6 && !rc; ci++) {
+        const int c = alt_gcm[ci];
         if (!(kt->cipher_mask & (1u << c))) continue;
-        const size_t base = (size_t) (4 + (c - TLSREC_CIPHER_ARIA_128_GCM)) * cap + 1;
+        const size_t base = (size_t) (4 + ci) * cap + 1;
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;
@@ -344,14 +349,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.cipher = (uint32_t) c;
         const uint64_t per_wg = (uint64_t) ARIA_GCM_WAVES * a.rpw;
         const uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
-        if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_aria_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)
+        if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_alt_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)
             rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     uint32_t ccm_nr = 0;
     for (int c = TLSREC_CIPHER_AES_128_CCM; c <= TLSREC_CIPHER_AES_256_CCM_8; c++)
         if (kt->cipher_mask & (1u << c)) ccm_nr |= 1u << tlsrec_cipher_nr(c);
-    for (int c = TLSREC_CIPHER_ARIA_128_CCM; c <= TLSREC_CIPHER_ARIA_256_CCM; c++)   /* ARIA: bit nr + 4 */
-        if (kt->cipher_mask & (1u << c)) ccm_nr |= 1u << (tlsrec_cipher_aria_nr(c) + 4);
+    for (int c = TLSREC_CIPHER_ARIA_128_CCM; c <= TLSREC_CIPHER_CAMELLIA_256_CCM; c++)   /* ARIA / Camellia: bit nr + 4 */
+        if (tlsrec_cipher_is_alt_ccm(c) && (kt->cipher_mask & (1u << c))) ccm_nr |= 1u << (tlsrec_cipher_alt_nr(c) + 4);
     if (!rc && ccm_nr) {
         CcmArgs a;
         a.slots = kt->d_slots;

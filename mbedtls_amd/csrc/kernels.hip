@@ -135,6 +135,102 @@ __device__ inline void aria_encrypt_bytes(const uint8_t ek[17][16], int nr, uint
     for (int i = 0; i < 16; i++) st[i] ^= ek[nr][i];
 }
 
+/* Camellia key schedule and 64-bit-word block (RFC 3713 2.2-2.4), one lane:
+ * only for the subkeys and H = E_K(0^128) of a slot. */
+__device__ inline uint64_t cam_f64(uint64_t x, uint64_t k)
+{
+    x ^= k;
+    const uint32_t xh = (uint32_t) (x >> 32), xl = (uint32_t) x;
+    const uint32_t u = kCamSbox.sp[0][xh >> 24] ^ kCamSbox.sp[1][(xh >> 16) & 0xff] ^
+                       kCamSbox.sp[2][(xh >> 8) & 0xff] ^ kCamSbox.sp[3][xh & 0xff];
+    const uint32_t v = kCamSbox.sp[1][xl >> 24] ^ kCamSbox.sp[2][(xl >> 16) & 0xff] ^
+                       kCamSbox.sp[3][(xl >> 8) & 0xff] ^ kCamSbox.sp[0][xl & 0xff];
+    return ((uint64_t) (u ^ v) << 32) | (u ^ ((u >> 8) | (u << 24)) ^ v);
+}
+
+__device__ inline void cam_rol128(uint64_t hi, uint64_t lo, int n, uint64_t &oh, uint64_t &ol)
+{
+    if (n >= 64) { const uint64_t t = hi; hi = lo; lo = t; n -= 64; }
+    if (n == 0) { oh = hi; ol = lo; return; }
+    oh = (hi << n) | (lo >> (64 - n));
+    ol = (lo << n) | (hi >> (64 - n));
+}
+
+/* the 26 / 34 subkeys in use order (kw1 kw2 | k1..k6 | ke1 ke2 | ... | kw3 kw4) */
+__device__ inline int cam_key_expand(const uint8_t *key, int keylen, uint64_t sk[34])
+{
+    const uint64_t SIGMA[6] = { 0xA09E667F3BCC908BULL, 0xB67AE8584CAA73B2ULL, 0xC6EF372FE94F82BEULL,
+                                0x54FF53A5F1D36F1CULL, 0x10E527FADE682D1DULL, 0xB05688C2B3E6C1FDULL };
+    uint64_t w[4] = { 0, 0, 0, 0 };
+    for (int i = 0; i < keylen; i++) w[i / 8] = (w[i / 8] << 8) | key[i];
+    if (keylen == 24) w[3] = ~w[2];
+    /* src: 0 KL, 1 KR, 2 KA, 3 KB as (hi, lo) */
+    uint64_t src[4][2] = { { w[0], w[1] }, { w[2], w[3] }, { 0, 0 }, { 0, 0 } };
+    uint64_t d1 = w[0] ^ w[2], d2 = w[1] ^ w[3];
+    d2 ^= cam_f64(d1, SIGMA[0]);
+    d1 ^= cam_f64(d2, SIGMA[1]);
+    d1 ^= w[0];
+    d2 ^= w[1];
+    d2 ^= cam_f64(d1, SIGMA[2]);
+    d1 ^= cam_f64(d2, SIGMA[3]);
+    src[2][0] = d1; src[2][1] = d2;
+    d1 ^= w[2];
+    d2 ^= w[3];
+    d2 ^= cam_f64(d1, SIGMA[4]);
+    d1 ^= cam_f64(d2, SIGMA[5]);
+    src[3][0] = d1; src[3][1] = d2;
+    /* (source, rotation, halves: 3 both, 1 high, 2 low), RFC 3713 2.2 */
+    const uint8_t s128[14][3] = { { 0, 0, 3 }, { 2, 0, 3 }, { 0, 15, 3 }, { 2, 15, 3 }, { 2, 30, 3 },
+                                  { 0, 45, 3 }, { 2, 45, 1 }, { 0, 60, 2 }, { 2, 60, 3 }, { 0, 77, 3 },
+                                  { 0, 94, 3 }, { 2, 94, 3 }, { 0, 111, 3 }, { 2, 111, 3 } };
+    const uint8_t s256[17][3] = { { 0, 0, 3 }, { 3, 0, 3 }, { 1, 15, 3 }, { 2, 15, 3 }, { 1, 30, 3 },
+                                  { 3, 30, 3 }, { 0, 45, 3 }, { 2, 45, 3 }, { 0, 60, 3 }, { 1, 60, 3 },
+                                  { 3, 60, 3 }, { 0, 77, 3 }, { 2, 77, 3 }, { 1, 94, 3 }, { 2, 94, 3 },
+                                  { 0, 111, 3 }, { 3, 111, 3 } };
+    const int rows = keylen == 16 ? 14 : 17;
+    int n = 0;
+    for (int i = 0; i < rows; i++) {
+        const uint8_t *e = keylen == 16 ? s128[i] : s256[i];
+        uint64_t h, l;
+        cam_rol128(src[e[0]][0], src[e[0]][1], e[1], h, l);
+        if (e[2] & 1) sk[n++] = h;
+        if (e[2] & 2) sk[n++] = l;
+    }
+    for (int i = n; i < 34; i++) sk[i] = 0;
+    return keylen == 16 ? 18 : 24;
+}
+
+__device__ inline void cam_encrypt_u64(const uint64_t sk[34], int nr, uint64_t &hi, uint64_t &lo)
+{
+    uint64_t d1 = hi ^ sk[0], d2 = lo ^ sk[1];
+    int i = 2;
+    const int groups = nr / 6;
+    for (int g = 0; g < groups; g++) {
+        for (int r = 0; r < 3; r++) {
+            d2 ^= cam_f64(d1, sk[i++]);
+            d1 ^= cam_f64(d2, sk[i++]);
+        }
+        if (g != groups - 1) {
+            uint32_t x1 = (uint32_t) (d1 >> 32), x2 = (uint32_t) d1;
+            uint32_t k1 = (uint32_t) (sk[i] >> 32), k2 = (uint32_t) sk[i];
+            uint32_t t = x1 & k1;
+            x2 ^= (t << 1) | (t >> 31);
+            x1 ^= x2 | k2;
+            d1 = ((uint64_t) x1 << 32) | x2;
+            i++;
+            uint32_t y1 = (uint32_t) (d2 >> 32), y2 = (uint32_t) d2;
+            k1 = (uint32_t) (sk[i] >> 32); k2 = (uint32_t) sk[i];
+            y1 ^= y2 | k2;
+            t = y1 & k1;
+            y2 ^= (t << 1) | (t >> 31);
+            d2 = ((uint64_t) y1 << 32) | y2;
+            i++;
+        }
+    }
+    hi = d2 ^ sk[i];
+    lo = d1 ^ sk[i + 1];
+}
+
 /* One 256-thread workgroup per slot. */
 __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab,
                                                              const tlsrec_key_material *keys,
@@ -151,7 +247,8 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
      * the GHASH tables */
     const bool aes = tlsrec_cipher_nr(km.cipher) != 0;
     const bool aria = tlsrec_cipher_is_aria(km.cipher);
-    const bool gcm = tlsrec_cipher_is_gcm(km.cipher) || tlsrec_cipher_is_aria_gcm(km.cipher);
+    const bool cam = tlsrec_cipher_is_cam(km.cipher);
+    const bool gcm = tlsrec_cipher_is_gcm(km.cipher) || tlsrec_cipher_is_alt_gcm(km.cipher);
     if (tid == 0) {
         st->km = km;
         st->km.reserved[0] = 0;   /* CID length mirror (tlsrec_recdev.h plan_key) */
@@ -187,6 +284,20 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
             H.hi = 0; H.lo = 0;
             for (int i = 0; i < 8; i++) { H.hi = (H.hi << 8) | h[i]; H.lo = (H.lo << 8) | h[8 + i]; }
             for (int i = 0; i < 16; i++) st->h[i] = h[i];
+            pw[0] = H;
+            for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);
+        } else if (cam) {
+            /* Camellia: the subkeys as (high, low) word pairs (tlsrec_device.h cam_encrypt) */
+            uint64_t sk[34];
+            const int nr = cam_key_expand(km.key, (int) tlsrec_cipher_keylen(km.cipher), sk);
+            for (int i = 0; i < 34; i++) {
+                st->ark[2 * i] = (uint32_t) (sk[i] >> 32);
+                st->ark[2 * i + 1] = (uint32_t) sk[i];
+            }
+            G128 H;
+            H.hi = 0; H.lo = 0;
+            cam_encrypt_u64(sk, nr, H.hi, H.lo);
+            for (int i = 0; i < 8; i++) { st->h[i] = (uint8_t) (H.hi >> (56 - 8 * i)); st->h[8 + i] = (uint8_t) (H.lo >> (56 - 8 * i)); }
             pw[0] = H;
             for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);
         }
@@ -326,7 +437,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     if (wg_base >= count) return;                      /* uniform: before any barrier */
 
     if constexpr (ARIA)
-        aria_fill_tables(lds + LY::AES, tid, NTHR);
+        alt_fill_tables<NR>(lds + LY::AES, tid, NTHR);
     else
         aes_fill_tables(lds + LY::AES, tid, NTHR);
 
@@ -398,7 +509,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 nonce_words<DEC>(p, d, a.in, nw);
             }
             if constexpr (ARIA)
-                ej0 = aria_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+                ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
             else
                 ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
             reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
@@ -478,7 +589,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                         aes_ghash<NR, LY::AES, HPI>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
                     } else {
                         if constexpr (ARIA)
-                            ks = aria_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                            ks = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
                         else
                             ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
                         Zn = gmul<HPI>(hor, y);
@@ -637,8 +748,12 @@ __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec
         case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + 1 + d.slot;
         case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + 1 + d.slot;
         case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + 1 + d.slot;
+        /* Camellia-GCM classes after ARIA's: (7, 8, 9) cap + 1 + slot */
+        case TLSREC_CIPHER_CAMELLIA_128_GCM: return 7 * a.capacity + 1 + d.slot;
+        case TLSREC_CIPHER_CAMELLIA_192_GCM: return 8 * a.capacity + 1 + d.slot;
+        case TLSREC_CIPHER_CAMELLIA_256_GCM: return 9 * a.capacity + 1 + d.slot;
         default:
-            return (tlsrec_cipher_is_ccm(c) || tlsrec_cipher_is_aria_ccm(c)) ? 3 * a.capacity + d.slot : 0xffffffffu;
+            return (tlsrec_cipher_is_ccm(c) || tlsrec_cipher_is_alt_ccm(c)) ? 3 * a.capacity + d.slot : 0xffffffffu;
     }
 }
 
@@ -1207,6 +1322,9 @@ extern "C" hipError_t tlsrec__launch_gcm_aria(const GcmArgs *a, int dec, int nr,
         case 12: return dec ? launch_gcm_aria<12, true>(*a, grid, st, cid) : launch_gcm_aria<12, false>(*a, grid, st, cid);
         case 14: return dec ? launch_gcm_aria<14, true>(*a, grid, st, cid) : launch_gcm_aria<14, false>(*a, grid, st, cid);
         case 16: return dec ? launch_gcm_aria<16, true>(*a, grid, st, cid) : launch_gcm_aria<16, false>(*a, grid, st, cid);
+        /* Camellia-GCM: 18 / 24 rounds through the same slot */
+        case 18: return dec ? launch_gcm_aria<18, true>(*a, grid, st, cid) : launch_gcm_aria<18, false>(*a, grid, st, cid);
+        case 24: return dec ? launch_gcm_aria<24, true>(*a, grid, st, cid) : launch_gcm_aria<24, false>(*a, grid, st, cid);
         default: return hipErrorInvalidValue;
     }
 }

@@ -261,6 +261,144 @@ __device__ __forceinline__ uint4 aria_encrypt(const uint8_t *lds, uint32_t lb, R
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+/* ---------------- Camellia (RFC 3713) ----------------------------------- */
+/* SBOX1 (RFC 3713 2.4.4); SBOX2 = SBOX1 <<< 1, SBOX3 = SBOX1 <<< 7,
+ * SBOX4(x) = SBOX1(x <<< 1).  The F-function's P-layer folds into four dword
+ * tables, one per S-box, SP_i[x] = SBOX_i(x) placed in the bytes of the
+ * P-layer column it feeds (y1 = the top byte):
+ *   SP1 = s.s.s.0, SP2 = 0.s.s.s, SP3 = s.0.s.s, SP4 = s.s.0.s.
+ * For F's input halves xh = t1..t4, xl = t5..t8 (S-boxes 1234 and 2341):
+ *   U = SP1[t1]^SP2[t2]^SP3[t3]^SP4[t4],  V = SP2[t5]^SP3[t6]^SP4[t7]^SP1[t8],
+ *   y1..y4 = U ^ V,  y5..y8 = U ^ (U >>> 8) ^ V
+ * (the right half's U-columns are the byte-neighbour sums of the left's). */
+struct CamSboxGen {
+    uint8_t s1[256];
+    uint32_t sp[4][256];
+    constexpr CamSboxGen() : s1{
+    112, 130,  44, 236, 179,  39, 192, 229, 228, 133,  87,  53, 234,  12, 174,  65,
+     35, 239, 107, 147,  69,  25, 165,  33, 237,  14,  79,  78,  29, 101, 146, 189,
+    134, 184, 175, 143, 124, 235,  31, 206,  62,  48, 220,  95,  94, 197,  11,  26,
+    166, 225,  57, 202, 213,  71,  93,  61, 217,   1,  90, 214,  81,  86, 108,  77,
+    139,  13, 154, 102, 251, 204, 176,  45, 116,  18,  43,  32, 240, 177, 132, 153,
+    223,  76, 203, 194,  52, 126, 118,   5, 109, 183, 169,  49, 209,  23,   4, 215,
+     20,  88,  58,  97, 222,  27,  17,  28,  50,  15, 156,  22,  83,  24, 242,  34,
+    254,  68, 207, 178, 195, 181, 122, 145,  36,   8, 232, 168,  96, 252, 105,  80,
+    170, 208, 160, 125, 161, 137,  98, 151,  84,  91,  30, 149, 224, 255, 100, 210,
+     16, 196,   0,  72, 163, 247, 117, 219, 138,   3, 230, 218,   9,  63, 221, 148,
+    135,  92, 131,   2, 205,  74, 144,  51, 115, 103, 246, 243, 157, 127, 191, 226,
+     82, 155, 216,  38, 200,  55, 198,  59, 129, 150, 111,  75,  19, 190,  99,  46,
+    233, 121, 167, 140, 159, 110, 188, 142,  41, 245, 249, 182,  47, 253, 180,  89,
+    120, 152,   6, 106, 231,  70, 113, 186, 212,  37, 171,  66, 136, 162, 141, 250,
+    114,   7, 185,  85, 248, 238, 172,  10,  54,  73,  42, 104,  60,  56, 241, 164,
+     64,  40, 211, 123, 187, 201,  67, 193,  21, 227, 173, 244, 119, 199, 128, 158,
+    }, sp()
+    {
+        for (int x = 0; x < 256; x++) {
+            const uint32_t a = s1[x];
+            const uint32_t b = ((a << 1) | (a >> 7)) & 0xffu;                      /* SBOX2 */
+            const uint32_t c = ((a << 7) | (a >> 1)) & 0xffu;                      /* SBOX3 */
+            const uint32_t d = s1[((x << 1) | (x >> 7)) & 0xff];                   /* SBOX4 */
+            sp[0][x] = (a << 24) | (a << 16) | (a << 8);
+            sp[1][x] = (b << 16) | (b << 8) | b;
+            sp[2][x] = (c << 24) | (c << 8) | c;
+            sp[3][x] = (d << 24) | (d << 16) | d;
+        }
+    }
+};
+
+__constant__ const CamSboxGen kCamSbox{};
+
+/* LDS SP tables in the ARIA layout: SP_t[x] at t*16384 + x*64 + copy*4 */
+__device__ __forceinline__ void cam_fill_tables(uint8_t *lds, int tid, int nthreads)
+{
+    for (int i = tid; i < 4 * 256 * 4; i += nthreads) {
+        const int t = i >> 10, x = (i >> 2) & 255, part = i & 3;
+        const uint32_t v = kCamSbox.sp[t][x];
+        *reinterpret_cast<uint4 *>(lds + t * 16384 + x * 64 + part * 16) = make_uint4(v, v, v, v);
+    }
+}
+
+template <int OFF>
+__device__ __forceinline__ uint32_t cam_sp(const uint8_t *lds, uint32_t lb, int t, uint32_t x)
+{
+    return *reinterpret_cast<const uint32_t *>(lds + OFF + t * 16384 + (x << 6) + lb);
+}
+
+/* F(x ^ k) on the 64-bit half (h = the high word) */
+template <int OFF>
+__device__ __forceinline__ void cam_f(const uint8_t *lds, uint32_t lb, uint32_t xh, uint32_t xl, uint32_t kh,
+                                      uint32_t kl, uint32_t &oh, uint32_t &ol)
+{
+    xh ^= kh;
+    xl ^= kl;
+    const uint32_t u = xor3(cam_sp<OFF>(lds, lb, 0, xh >> 24), cam_sp<OFF>(lds, lb, 1, (xh >> 16) & 0xffu),
+                            cam_sp<OFF>(lds, lb, 2, (xh >> 8) & 0xffu)) ^ cam_sp<OFF>(lds, lb, 3, xh & 0xffu);
+    const uint32_t v = xor3(cam_sp<OFF>(lds, lb, 1, xl >> 24), cam_sp<OFF>(lds, lb, 2, (xl >> 16) & 0xffu),
+                            cam_sp<OFF>(lds, lb, 3, (xl >> 8) & 0xffu)) ^ cam_sp<OFF>(lds, lb, 0, xl & 0xffu);
+    oh = u ^ v;
+    ol = xor3(u, __builtin_amdgcn_alignbit(u, u, 8), v);
+}
+
+/* Camellia forward cipher (NR = 18 / 24 rounds) of one block per lane.  Words
+ * of in/out are little-endian byte quadruples of the block; rk = the 64-bit
+ * subkeys in use order (kw1 kw2 | k1..k6 | ke1 ke2 | ... | kw3 kw4) as
+ * (high, low) word pairs.  lb = (lane & 15) * 4. */
+template <int NR, int OFF, typename RK>
+__device__ __forceinline__ uint4 cam_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
+{
+    uint32_t d1h = bswap32(in.x) ^ rk[0], d1l = bswap32(in.y) ^ rk[1];
+    uint32_t d2h = bswap32(in.z) ^ rk[2], d2l = bswap32(in.w) ^ rk[3];
+    constexpr int G = NR / 6;
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const int base = 4 + g * 16;     /* 6 round keys + 2 FL keys per group, 2 words each */
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            uint32_t fh, fl;
+            cam_f<OFF>(lds, lb, d1h, d1l, rk[base + 4 * r], rk[base + 4 * r + 1], fh, fl);
+            d2h ^= fh;
+            d2l ^= fl;
+            cam_f<OFF>(lds, lb, d2h, d2l, rk[base + 4 * r + 2], rk[base + 4 * r + 3], fh, fl);
+            d1h ^= fh;
+            d1l ^= fl;
+        }
+        if (g != G - 1) {
+            /* FL(d1, ke_a), FL^-1(d2, ke_b) (RFC 3713 2.4.2) */
+            const uint32_t k1 = rk[base + 12], k2 = rk[base + 13], k3 = rk[base + 14], k4 = rk[base + 15];
+            d1l ^= __builtin_amdgcn_alignbit(d1h & k1, d1h & k1, 31);
+            d1h ^= (d1l | k2);
+            d2h ^= (d2l | k4);
+            d2l ^= __builtin_amdgcn_alignbit(d2h & k3, d2h & k3, 31);
+        }
+    }
+    constexpr int W = 4 + 16 * G - 4;    /* kw3 kw4 */
+    d2h ^= rk[W];
+    d2l ^= rk[W + 1];
+    d1h ^= rk[W + 2];
+    d1l ^= rk[W + 3];
+    return make_uint4(bswap32(d2h), bswap32(d2l), bswap32(d1h), bswap32(d1l));
+}
+
+/* The LDS-table block ciphers behind the GCM / CCM kernels' ARIA slot:
+ * NR 12 / 14 / 16 = ARIA, NR 18 / 24 = Camellia. */
+template <int NR>
+__device__ __forceinline__ void alt_fill_tables(uint8_t *lds, int tid, int nthreads)
+{
+    if constexpr (NR >= 18)
+        cam_fill_tables(lds, tid, nthreads);
+    else
+        aria_fill_tables(lds, tid, nthreads);
+}
+
+template <int NR, int OFF, typename RK>
+__device__ __forceinline__ uint4 alt_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
+{
+    if constexpr (NR >= 18)
+        return cam_encrypt<NR, OFF>(lds, lb, rk, in);
+    else
+        return aria_encrypt<NR, OFF>(lds, lb, rk, in);
+}
+
 /* ---------------- GHASH with LDS position tables ----------------------- */
 /* Table PI (a power of H) holds T_k[n] = sum_{i<4} bit(3-i of n) * P * x^(4k+i)
  * at PI*8192 + k*256 + n*16, as the 16-byte GCM string.  Window k = 2b is the

@@ -49,9 +49,9 @@
 TLSREC_HD uint32_t tlsrec_cipher_keylen(int c)
 {
     switch (c) {
-        case 1: case 5: case 8: case 11: case 14: return 16;   /* AES-128 GCM / CCM / CCM_8, ARIA-128 GCM / CCM */
-        case 4: case 6: case 9: case 12: case 15: return 24;   /* AES-192, ARIA-192 */
-        case 2: case 3: case 7: case 10: case 13: case 16: return 32;  /* AES-256, ChaCha20-Poly1305, ARIA-256 */
+        case 1: case 5: case 8: case 11: case 14: case 17: case 20: return 16;   /* AES-128, ARIA-128, Camellia-128 */
+        case 4: case 6: case 9: case 12: case 15: case 18: case 21: return 24;   /* AES-192, ARIA-192, Camellia-192 */
+        case 2: case 3: case 7: case 10: case 13: case 16: case 19: case 22: return 32;  /* AES-256, ChaCha20-Poly1305, ARIA-256, Camellia-256 */
         default: return 0;
     }
 }
@@ -62,6 +62,17 @@ TLSREC_HD int tlsrec_cipher_is_aria_ccm(int c) { return c >= 14 && c <= 16; }   
 TLSREC_HD int tlsrec_cipher_is_aria(int c) { return c >= 11 && c <= 16; }          /* ARIA, any mode */
 /* ARIA rounds (RFC 5794 2.1): 12 / 14 / 16 */
 TLSREC_HD uint32_t tlsrec_cipher_aria_nr(int c) { return tlsrec_cipher_is_aria(c) ? tlsrec_cipher_keylen(c) / 4 + 8 : 0u; }
+/* Camellia-GCM / -CCM (PSA_KEY_TYPE_CAMELLIA, ssl_tls.c:2297-2345) */
+TLSREC_HD int tlsrec_cipher_is_cam_gcm(int c) { return c >= 17 && c <= 19; }
+TLSREC_HD int tlsrec_cipher_is_cam_ccm(int c) { return c >= 20 && c <= 22; }
+TLSREC_HD int tlsrec_cipher_is_cam(int c) { return c >= 17 && c <= 22; }
+/* Camellia rounds (RFC 3713 2.3): 18 for 128-bit keys, 24 for 192 / 256 */
+TLSREC_HD uint32_t tlsrec_cipher_cam_nr(int c) { return tlsrec_cipher_is_cam(c) ? (tlsrec_cipher_keylen(c) == 16 ? 18u : 24u) : 0u; }
+/* The LDS-table block ciphers that share the GCM / CCM kernels' ARIA slot,
+ * told apart by their round count (ARIA 12 / 14 / 16, Camellia 18 / 24) */
+TLSREC_HD int tlsrec_cipher_is_alt_gcm(int c) { return tlsrec_cipher_is_aria_gcm(c) || tlsrec_cipher_is_cam_gcm(c); }
+TLSREC_HD int tlsrec_cipher_is_alt_ccm(int c) { return tlsrec_cipher_is_aria_ccm(c) || tlsrec_cipher_is_cam_ccm(c); }
+TLSREC_HD uint32_t tlsrec_cipher_alt_nr(int c) { return tlsrec_cipher_is_aria(c) ? tlsrec_cipher_aria_nr(c) : tlsrec_cipher_cam_nr(c); }
 TLSREC_HD int tlsrec_cipher_is_ccm(int c) { return c >= 5 && c <= 10; }
 /* AES rounds of an AES-based cipher, 0 otherwise */
 TLSREC_HD uint32_t tlsrec_cipher_nr(int c) { return (c == 3 || c > 10) ? 0u : tlsrec_cipher_keylen(c) / 4 + 6; }

@@ -29,7 +29,8 @@ struct SlotState {
     uint8_t cid_len;          /* DTLS 1.2 connection ID of this transform direction */
     uint8_t cid[32];          /* (out_cid encrypting, in_cid decrypting), tlsrec_keytab_set_cid */
     uint8_t pad0[3];
-    uint32_t ark[68];         /* ARIA-GCM: the nr + 1 round keys ek1.. (RFC 5794 2.2), 16 B each as LE words */
+    uint32_t ark[68];         /* ARIA: the nr + 1 round keys ek1.. (RFC 5794 2.2), 16 B each as LE words;
+                                 Camellia: the 26 / 34 64-bit subkeys as (high, low) words */
     uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16 - 33 - 3 - 272];
 };
 static_assert(sizeof(SlotState) == 1024, "SlotState layout");
@@ -80,7 +81,7 @@ struct BucketArgs {
     tlsrec_batch_res *res;
     uint32_t n;
     uint32_t capacity;
-    uint32_t *counts;         /* [7 * capacity + 2] records per (class, slot), then exclusive offsets */
+    uint32_t *counts;         /* [10 * capacity + 2] records per (class, slot), then exclusive offsets */
     uint32_t *cursor;         /* copy of the offsets, consumed by the scatter */
     uint32_t *cp_cursor;      /* ChaCha records appended after the GCM ones */
     uint32_t *perm;           /* [n] */

@@ -17,7 +17,10 @@ CIPHERS = {"AES-128-GCM": M.CIPHER_AES_128_GCM, "AES-256-GCM": M.CIPHER_AES_256_
            "AES-192-CCM-8": M.CIPHER_AES_192_CCM_8, "AES-256-CCM-8": M.CIPHER_AES_256_CCM_8,
            "ARIA-128-GCM": M.CIPHER_ARIA_128_GCM, "ARIA-192-GCM": M.CIPHER_ARIA_192_GCM,
            "ARIA-256-GCM": M.CIPHER_ARIA_256_GCM, "ARIA-128-CCM": M.CIPHER_ARIA_128_CCM,
-           "ARIA-192-CCM": M.CIPHER_ARIA_192_CCM, "ARIA-256-CCM": M.CIPHER_ARIA_256_CCM}
+           "ARIA-192-CCM": M.CIPHER_ARIA_192_CCM, "ARIA-256-CCM": M.CIPHER_ARIA_256_CCM,
+           "CAMELLIA-128-GCM": M.CIPHER_CAMELLIA_128_GCM, "CAMELLIA-192-GCM": M.CIPHER_CAMELLIA_192_GCM,
+           "CAMELLIA-256-GCM": M.CIPHER_CAMELLIA_256_GCM, "CAMELLIA-128-CCM": M.CIPHER_CAMELLIA_128_CCM,
+           "CAMELLIA-192-CCM": M.CIPHER_CAMELLIA_192_CCM, "CAMELLIA-256-CCM": M.CIPHER_CAMELLIA_256_CCM}
 VERSIONS = {"TLS1.2": M.VERSION_TLS1_2, "TLS1.3": M.VERSION_TLS1_3}
 
 

@@ -78,7 +78,10 @@ CIPHERS = {"AES-128-GCM": O.AES_128_GCM, "AES-256-GCM": O.AES_256_GCM,
            "AES-128-CCM": O.AES_128_CCM, "AES-192-CCM": O.AES_192_CCM, "AES-256-CCM": O.AES_256_CCM,
            "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-CCM-8": O.AES_192_CCM_8, "AES-256-CCM-8": O.AES_256_CCM_8,
            "ARIA-128-GCM": O.ARIA_128_GCM, "ARIA-192-GCM": O.ARIA_192_GCM, "ARIA-256-GCM": O.ARIA_256_GCM,
-           "ARIA-128-CCM": O.ARIA_128_CCM, "ARIA-192-CCM": O.ARIA_192_CCM, "ARIA-256-CCM": O.ARIA_256_CCM}
+           "ARIA-128-CCM": O.ARIA_128_CCM, "ARIA-192-CCM": O.ARIA_192_CCM, "ARIA-256-CCM": O.ARIA_256_CCM,
+           "CAMELLIA-128-GCM": O.CAMELLIA_128_GCM, "CAMELLIA-192-GCM": O.CAMELLIA_192_GCM,
+           "CAMELLIA-256-GCM": O.CAMELLIA_256_GCM, "CAMELLIA-128-CCM": O.CAMELLIA_128_CCM,
+           "CAMELLIA-192-CCM": O.CAMELLIA_192_CCM, "CAMELLIA-256-CCM": O.CAMELLIA_256_CCM}
 VERSIONS = {"TLS1.2": O.TLS1_2, "TLS1.3": O.TLS1_3}
 
 
