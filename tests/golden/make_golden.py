@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 import oracle as O  # noqa: E402
 from tests import _openssl as S  # noqa: E402
+from tests.test_camellia_oracle import ccm_ref, gcm_ref  # noqa: E402
 from tests.prng import prng_bytes  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
@@ -113,7 +114,13 @@ CIPHERS = {"AES-128-GCM": O.AES_128_GCM, "AES-256-GCM": O.AES_256_GCM,
            "AES-256-CCM-8": O.AES_256_CCM_8,
            # ARIA-GCM / ARIA-CCM (appended likewise)
            "ARIA-128-GCM": O.ARIA_128_GCM, "ARIA-192-GCM": O.ARIA_192_GCM, "ARIA-256-GCM": O.ARIA_256_GCM,
-           "ARIA-128-CCM": O.ARIA_128_CCM, "ARIA-192-CCM": O.ARIA_192_CCM, "ARIA-256-CCM": O.ARIA_256_CCM}
+           "ARIA-128-CCM": O.ARIA_128_CCM, "ARIA-192-CCM": O.ARIA_192_CCM, "ARIA-256-CCM": O.ARIA_256_CCM,
+           # Camellia-GCM / Camellia-CCM (appended likewise; OpenSSL has no Camellia AEAD, so the
+           # cross-check is SP 800-38D / 38C assembled on OpenSSL Camellia-ECB/-CBC,
+           # tests/test_camellia_oracle.py gcm_ref / ccm_ref)
+           "CAMELLIA-128-GCM": O.CAMELLIA_128_GCM, "CAMELLIA-192-GCM": O.CAMELLIA_192_GCM,
+           "CAMELLIA-256-GCM": O.CAMELLIA_256_GCM, "CAMELLIA-128-CCM": O.CAMELLIA_128_CCM,
+           "CAMELLIA-192-CCM": O.CAMELLIA_192_CCM, "CAMELLIA-256-CCM": O.CAMELLIA_256_CCM}
 VERSIONS = {"TLS1.2": O.TLS1_2, "TLS1.3": O.TLS1_3}
 LENGTHS = [0, 1, 15, 16, 17, 1400, 16383]
 SEED = 0x7115EC0DE
@@ -167,7 +174,11 @@ def make_records():
                             assert wire[:8] == ctr
                             body = wire[8:]
                     tl = O.TAGLEN[c]
-                    if O.AES_128_CCM <= c <= O.AES_256_CCM_8:
+                    if c >= O.CAMELLIA_128_CCM:
+                        ct, tag = ccm_ref(key_enc, nonce, aad, inner, tl)
+                    elif c >= O.CAMELLIA_128_GCM:
+                        ct, tag = gcm_ref(key_enc, nonce, aad, inner)
+                    elif O.AES_128_CCM <= c <= O.AES_256_CCM_8:
                         ct, tag = S.ccm_seal(key_enc, nonce, aad, inner, tl)
                     elif c >= O.ARIA_128_CCM:
                         ct, tag = S.ccm_seal(key_enc, nonce, aad, inner, tl, name="aria-ccm")
