@@ -57,6 +57,10 @@ CONFIGS = {
 }
 
 
+KERNEL_OF = {"CHACHA20-POLY1305": "tlsrec_chachapoly_kernel", "AES-128-CCM": "tlsrec_ccm_kernel",
+             "AES-128-CCM-8": "tlsrec_ccm_kernel", "MIX": "tlsrec_gcm_kernel + tlsrec_chachapoly_kernel"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,6 +73,8 @@ def parse():
     ap.add_argument("--align", type=int, default=128, help="record slot alignment in the arena (bytes; 128 = HBM/L2 line)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of the CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (pinned H2D/D2H) leg")
+    ap.add_argument("--e2e-records", type=int, default=0, help="records of the end-to-end leg (0 = ~2 GiB worth)")
     ap.add_argument("--verify", type=int, default=64, help="records spot-checked against the oracle")
     return ap.parse_args()
 
@@ -241,14 +247,31 @@ def main():
     achieved = alg_per_rec * n / kern_avg_s / 1e9
     # HBM traffic per launch: PMC FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE
     # per record, measured by profiles/run_profile.sh on this config and
-    # committed as profiles/traffic_<config>.json, scaled to this launch.
-    traffic = None
+    # committed as profiles/traffic_<config>.json, scaled to this launch (not
+    # re-measured in this run: counters need their own rocprofv3 passes).
+    traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
         if tj.get("direction") == direction and tj.get("record_inner_bytes") == inner:
             traffic = round(tj["hbm_bytes_per_record"] * n)
+            traffic_src = (f"profiles/traffic_{args.config}.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                           f"run {tj.get('source', '?')}, {tj['hbm_bytes_per_record']:.0f} B/record x {n} records)")
+    # The unit that actually bounds the kernel (LDS for the table ciphers):
+    # its busy fraction from the committed PMC run (profiles/ceiling_<config>.json)
+    # and the rate this kernel would reach with that unit 100 % busy.
+    ceiling = None
+    cpath = os.path.join(ROOT, "profiles", f"ceiling_{args.config}.json")
+    if os.path.exists(cpath):
+        with open(cpath) as f:
+            cj = json.load(f)
+        busy = cj["limiter_busy_frac"]
+        ceiling = {"limiter": cj["limiter"], "busy_frac": busy,
+                   "ceiling_GBps": round(achieved / busy, 1) if busy > 0 else None,
+                   "ceiling_frac_of_hbm": round(achieved / busy / HBM_PEAK_GBS, 4) if busy > 0 else None,
+                   "clock_ghz": cj.get("effective_clock_ghz"), "units": cj.get("units"),
+                   "source": f"profiles/ceiling_{args.config}.json ({cj.get('source', '?')})"}
 
     steps_s = wall / args.steps
     payload_total = float(n) * inner * world
@@ -257,6 +280,14 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cname, ver, content, inner, wire, stride, km, args.cpu_seconds, direction)
+
+    # records in host memory: pinned socket buffers -> device -> pinned (the
+    # boundary the reference's callers hand over, ssl_msg.c:1855 / :2058);
+    # reported beside the device-resident value, never as it
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = end_to_end(M, kt, recs, arena, out_arena, n, stride, head, content, wire, inner, direction,
+                         args.e2e_records)
 
     out = {
         "metric": METRIC,
@@ -276,9 +307,12 @@ def main():
                    "lanes_per_record": args.lanes or "auto", "slot_align": args.align, "parallelism": f"shard{world}"},
         "records_per_s": round(n * world / steps_s, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_record": alg_per_rec, "kernel_ms_avg": round(kern_avg_s * 1e3, 4)},
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": KERNEL_OF.get(cname, "tlsrec_gcm_kernel"), "ceiling": ceiling,
+                     "algorithmic_bytes_per_record": alg_per_rec, "kernel_ms_avg": round(kern_avg_s * 1e3, 4),
+                     "timing": "HIP events on the launch stream around each timed step"},
         "cpu_baseline": cpu,
+        "e2e": e2e,
         "check": {"bad_records": bad, "oracle_sample_ok": oracle_ok},
     }
     if rank == 0:
@@ -287,56 +321,180 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, direction):
-    """oracle/ (the CPU restatement, kind 'port') timed on this host's cores on
-    a bounded sample of the same workload."""
-    import oracle as O
-    cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM, "AES-128-CCM": O.AES_128_CCM,
-              "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-GCM": O.AES_192_GCM,
-              "ARIA-256-GCM": O.ARIA_256_GCM, "CAMELLIA-128-GCM": O.CAMELLIA_128_GCM}.get(cname, O.AES_256_GCM)
-    k = km[0]
-    klen = O.KEYLEN[cipher]
-    t = O.Transform(O.TLS1_3 if ver == 0x0304 else O.TLS1_2, cipher, bytes(k["key"][:klen]),
-                    bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
-    threads = min(16, os.cpu_count() or 1)
-    from tests.prng import prng_array
-    # grow the sample up to a 512 MiB arena, then repeat the timed pass over it
-    # (resealed untimed for decrypt) until about target_s of wall time
+def end_to_end(M, kt, recs, arena, out_arena, n, stride, head, content, wire, inner, direction, e2e_records):
+    """tlsrec_host_batch_* over pinned host buffers: chunked H2D -> kernels ->
+    D2H on three streams (engine.hip).  Input = the first E records of the
+    bench batch (ciphertexts for decrypt), output into a second pinned buffer;
+    statuses and a byte sample are checked against the device-resident run."""
+    import torch
+    E = min(n, e2e_records or max(1, (2 << 30) // stride))
+    span = E * stride
+    host_in = torch.empty(span, dtype=torch.uint8).pin_memory()
+    host_out = torch.empty(span, dtype=torch.uint8).pin_memory()
+    host_in.copy_(arena[:span])
+    d = recs[:E].copy()
+    if direction == "decrypt":
+        d["data_offset"] = 0
+        d["data_len"] = wire
+    res = M.results(E)
+    chunk = 64 << 20
+    dec = direction == "decrypt"
+    M.host_batch(dec, kt, d, res, E, host_in, host_out, chunk_bytes=chunk)      # warm-up
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        M.host_batch(dec, kt, d, res, E, host_in, host_out, chunk_bytes=chunk)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    ok = bool((res["status"] == 0).all())
+    lo, hi = (head, head + content) if dec else (0, wire)
+    ref = out_arena                  # the device-resident run of the same records
+    for i in sorted({0, E // 2, E - 1}):
+        ok &= bool(torch.equal(host_out[i * stride + lo:i * stride + hi], ref[i * stride + lo:i * stride + hi].cpu()))
+    dev = torch.empty(span, dtype=torch.uint8, device=arena.device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev.copy_(host_in, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = span / (time.perf_counter() - t0) / 1e9
+    t0 = time.perf_counter()
+    host_out.copy_(dev, non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = span / (time.perf_counter() - t0) / 1e9
+    del dev
+    return {"value": round(E * inner / best / 2**30, 3), "unit": "GiB/s", "records_per_s": round(E / best, 1),
+            "records": E, "chunk_bytes": chunk, "device_slots": 3, "streams": "H2D / kernels / D2H",
+            "h2d_only_GBps": round(h2d, 2), "d2h_only_GBps": round(d2h, 2), "check_ok": ok,
+            "what": "pinned host records -> device -> pinned host (tlsrec_host_batch_%s); PCIe-inclusive, "
+                    "not the device-resident headline" % direction}
+
+
+def host_cores():
+    """Threads the CPU legs use: the host CPUs this process may run on
+    (affinity), capped by a cgroup CPU quota and by OMP_NUM_THREADS, which the
+    GPU pool sets to the box's CPU share (os.cpu_count() there shows the whole
+    machine).  Returns (threads, how they were determined)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n, why = aff, [f"affinity {aff} CPUs", f"os.cpu_count {os.cpu_count()}"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            qc = max(1, -(-int(q) // int(per)))
+            n = min(n, qc)
+            why.append(f"cgroup quota {qc} CPUs")
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+        why.append(f"OMP_NUM_THREADS {omp} (the box's CPU share)")
+    return max(1, n), "; ".join(why)
+
+
+def _timed_sample(target_s, stride, n0, seal, run):
+    """Grow the sample (up to a 512 MiB arena) until one pass takes about
+    target_s, then repeat passes until target_s of wall time; seal() prepares
+    the arena untimed before each pass (decrypt inputs)."""
     cap = 512 << 20
-    n = 1024
+    n = n0
     while True:
-        arena = np.zeros(n * stride, dtype=np.uint8)
-        payload = prng_array(SEED ^ 0xC0FFEE, n * content).reshape(n, content)
-        arena.reshape(n, stride)[:, :content] = payload
-        st = np.zeros(n, dtype=np.int32)
-        if direction == "decrypt":
-            t.bench(1, arena, stride, content, n, 0, threads, st)     # seal (untimed)
-            assert (st == 0).all()
-            el = t.bench(0, arena, stride, wire, n, 0, threads, st)
-        else:
-            el = t.bench(1, arena, stride, content, n, 0, threads, st)
-        assert (st == 0).all()
+        arena = seal(n, None)
+        el = run(arena, n)
         if el >= target_s or n * stride * 2 > cap:
             break
         n = min(int(n * max(2.0, min(8.0, target_s / max(el, 1e-3)))), cap // stride)
     reps = 1
     while el < target_s:
-        if direction == "decrypt":
-            arena.reshape(n, stride)[:, :content] = payload
-            t.bench(1, arena, stride, content, n, 0, threads, st)     # reseal (untimed)
-            el += t.bench(0, arena, stride, wire, n, 0, threads, st)
-        else:
-            el += t.bench(1, arena, stride, content, n, 0, threads, st)
-        assert (st == 0).all()
+        seal(n, arena)
+        el += run(arena, n)
         reps += 1
-    n *= reps
-    gib = n * inner / el / 2**30
-    impl = {"CHACHA20-POLY1305": "ChaCha20 + 44-bit-limb Poly1305", "ARIA-256-GCM": "byte-wise ARIA + 4-bit Shoup GHASH",
-            "CAMELLIA-128-GCM": "byte-wise Camellia + 4-bit Shoup GHASH"}.get(
-        cname, "table AES + 4-bit Shoup GHASH" if "GCM" in cname else "table AES CCM")
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} records ({reps} passes) x {inner} B inner plaintext, {direction}, oracle/liboracle.so "
-                      f"({impl}), {el:.2f} s wall on {threads} threads"}
+    return n, reps, el
+
+
+def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, direction):
+    """Two CPU legs on the same record shape, timed on this host's cores
+    (threads = host_cores()): 'evp' -- the record framing around OpenSSL 3
+    EVP AEADs (AES-NI/VAES GCM, SIMD ChaCha20-Poly1305), the stand-in for the
+    reference's default x86 path (AES-NI on by default, ChangeLog:1021-1024);
+    'port' -- this repository's C restatement (oracle/, table AES + 4-bit
+    Shoup GHASH, the Mbed TLS builtin design).  The first available is the
+    headline cpu_baseline value; both are listed."""
+    import oracle as O
+    from tests.prng import prng_array
+    cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM, "AES-128-CCM": O.AES_128_CCM,
+              "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-GCM": O.AES_192_GCM,
+              "ARIA-256-GCM": O.ARIA_256_GCM, "CAMELLIA-128-GCM": O.CAMELLIA_128_GCM}.get(cname, O.AES_256_GCM)
+    k = km[0]
+    klen = O.KEYLEN[cipher]
+    key, iv = bytes(k["key"][:klen]), bytes(k["iv"])
+    tls = O.TLS1_3 if ver == 0x0304 else O.TLS1_2
+    head = 8 if tls == O.TLS1_2 and cipher != O.CHACHA20_POLY1305 else 0
+    threads, how = host_cores()
+    payload = prng_array(SEED ^ 0xC0FFEE, 4096 * content).reshape(4096, content) if content else None
+    st_cache = {}
+
+    def fresh(n, arena):
+        if arena is None:
+            arena = np.zeros(n * stride, dtype=np.uint8)
+        if content:
+            v = arena.reshape(n, stride)
+            for lo in range(0, n, 4096):
+                hi = min(n, lo + 4096)
+                v[lo:hi, head:head + content] = payload[:hi - lo]
+        st_cache[n] = np.zeros(n, dtype=np.int32)
+        return arena
+
+    legs = []
+    t = O.Transform(tls, cipher, key, key, iv, iv)
+    impls = {"CHACHA20-POLY1305": "ChaCha20 + 44-bit-limb Poly1305",
+             "ARIA-256-GCM": "byte-wise ARIA + 4-bit Shoup GHASH",
+             "CAMELLIA-128-GCM": "byte-wise Camellia (unoptimised oracle port) + 4-bit Shoup GHASH"}
+
+    def port_seal(n, arena):
+        arena = fresh(n, arena)
+        if direction == "decrypt":
+            t.bench(1, arena, stride, content, n, 0, threads, st_cache[n])
+            assert (st_cache[n] == 0).all()
+        return arena
+
+    def port_run(arena, n):
+        el = t.bench(0 if direction == "decrypt" else 1, arena, stride, wire if direction == "decrypt" else content,
+                     n, 0, threads, st_cache[n])
+        assert (st_cache[n] == 0).all()
+        return el
+
+    if cipher in O.EVP_CIPHERS:
+        def evp_seal(n, arena):
+            arena = fresh(n, arena)
+            if direction == "decrypt":
+                O.evp_bench(cipher, tls, key, iv, 1, arena, stride, content, n, 0, threads, st_cache[n])
+                assert (st_cache[n] == 0).all()
+            return arena
+
+        def evp_run(arena, n):
+            el = O.evp_bench(cipher, tls, key, iv, 0 if direction == "decrypt" else 1, arena, stride,
+                             wire if direction == "decrypt" else content, n, 0, threads, st_cache[n])
+            assert (st_cache[n] == 0).all()
+            return el
+
+        n, reps, el = _timed_sample(target_s, stride, 1024, evp_seal, evp_run)
+        legs.append({"value": round(n * reps * inner / el / 2**30, 3), "unit": "GiB/s", "cores": threads,
+                     "kind": "port", "leg": "evp",
+                     "sample": f"{n} records ({reps} passes) x {inner} B inner plaintext, {direction}: ssl_msg.c "
+                               f"record framing around OpenSSL 3 EVP AEAD (AES-NI/VAES GCM, SIMD ChaCha20-Poly1305; "
+                               f"oracle/libevpbench.so), one key context per thread, {el:.2f} s wall on {threads} "
+                               f"threads"})
+    n, reps, el = _timed_sample(target_s, stride, 1024, port_seal, port_run)
+    impl = impls.get(cname, "table AES + 4-bit Shoup GHASH" if "GCM" in cname else "table AES CCM")
+    legs.append({"value": round(n * reps * inner / el / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                 "leg": "port",
+                 "sample": f"{n} records ({reps} passes) x {inner} B inner plaintext, {direction}: oracle/liboracle.so "
+                           f"C restatement ({impl}), {el:.2f} s wall on {threads} threads"})
+    out = dict(legs[0])
+    out["cores_how"] = how
+    out["legs"] = legs
+    return out
 
 
 if __name__ == "__main__":

@@ -251,6 +251,25 @@ int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
                          tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
                          uint8_t *out_arena, uint32_t lanes_per_record, void *stream);
 
+/* Records in HOST memory (the socket-buffer boundary of ssl_msg.c:2058 /
+ * :1855): the same per-record semantics as tlsrec_batch_*, with `recs` /
+ * `res` host arrays and buf_off offsets into the host arenas in_arena /
+ * out_arena (pinned memory, e.g. hipHostMalloc, gives the full PCIe rate).
+ * The batch is cut into chunks of consecutive records of at most
+ * chunk_bytes (0 = 256 MiB) of arena; each chunk's byte range is copied to
+ * the device, protected there in place and copied back to the same offsets
+ * of out_arena (gaps between records inside a chunk carry the input bytes),
+ * with host-to-device copies, kernels and device-to-host copies overlapped on
+ * three streams.  Records must be in ascending buf_off order and must not
+ * overlap (else TLSREC_ERR_SSL_BAD_INPUT_DATA).  Synchronous: returns when
+ * every result is in `res`. */
+int tlsrec_host_batch_encrypt(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                              uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
+                              uint32_t lanes_per_record, uint64_t chunk_bytes);
+int tlsrec_host_batch_decrypt(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                              uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
+                              uint32_t lanes_per_record, uint64_t chunk_bytes);
+
 /* Host-only: run the record-framing checks of encrypt_buf / decrypt_buf
  * (everything decided before the AEAD, tlsrec_frame.h) for one batch record
  * under `km`.  Returns 1 if the record proceeds to the AEAD (aead_pos /

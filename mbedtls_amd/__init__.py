@@ -17,7 +17,7 @@ from ._abi import (CIPHER_AES_128_GCM, CIPHER_AES_256_GCM, CIPHER_CHACHA20_POLY1
                    ERR_SSL_INVALID_RECORD, ERR_SSL_UNEXPECTED_CID, MSG_APPLICATION_DATA, MSG_CID,
                    CID_LEN_MAX, VERSION_TLS1_2, VERSION_TLS1_3,
                    BATCH_REC, BATCH_RES, KEY_MATERIAL, load)
-from .batch import (KeyTable, batch_decrypt, batch_encrypt, frame_check, key_material,  # noqa: F401
+from .batch import (KeyTable, batch_decrypt, batch_encrypt, frame_check, host_batch, key_material,  # noqa: F401
                     records, results, seq_bytes)
 from .record import Record, Transform, decrypt_buf, encrypt_buf  # noqa: F401
 from .shard import Shard, broadcast_keys, reduce_status, shard_bounds, status_counts  # noqa: F401

@@ -114,6 +114,17 @@ def batch_decrypt(kt: KeyTable, recs, res, n: int, in_arena, out_arena=None, lan
         raise RuntimeError(f"tlsrec_batch_decrypt failed: {r:#x}")
 
 
+def host_batch(decrypt: bool, kt: KeyTable, recs, res, n: int, in_arena, out_arena=None, lanes: int = 0,
+               chunk_bytes: int = 0) -> None:
+    """tlsrec_host_batch_encrypt / _decrypt: descriptors, results and arenas
+    in HOST memory (numpy arrays or pinned CPU tensors); synchronous."""
+    out_arena = in_arena if out_arena is None else out_arena
+    fn = _abi.load().tlsrec_host_batch_decrypt if decrypt else _abi.load().tlsrec_host_batch_encrypt
+    r = fn(kt.handle, _ptr(recs), _ptr(res), n, _ptr(in_arena), _ptr(out_arena), lanes, chunk_bytes)
+    if r != 0:
+        raise RuntimeError(f"tlsrec_host_batch_{'decrypt' if decrypt else 'encrypt'} failed: {r:#x}")
+
+
 def frame_check(decrypt: bool, km, rec):
     """Host-only framing verdict for one record (tlsrec_frame_check)."""
     km = np.ascontiguousarray(km, dtype=_abi.KEY_MATERIAL)

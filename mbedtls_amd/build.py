@@ -20,13 +20,16 @@ OBJ = os.path.join(ROOT, "build")
 LIB = os.path.join(PKG, "libtlsrec.so")
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# parallel compiles: the box exports MAX_JOBS=16; here 8 CPUs (and ~2 GB per hipcc)
+JOBS = max(1, min(int(os.environ.get("MAX_JOBS", "8")), os.cpu_count() or 1, 8))
 ARCH = "gfx950"
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
              "-Wno-unused-value", "-I" + INC, "-I" + CSRC]
 C_FLAGS = ["-O2", "-fPIC", "-std=c11", "-Wall", "-Wextra", "-I" + INC, "-I" + CSRC]
 
-HEADERS = ["tlsrec_device.h", "tlsrec_frame.h", "tlsrec_internal.h", "tlsrec_recdev.h"]
-UNITS = [("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("ccm.hip", "hip"), ("ticket.hip", "hip"), ("tlsrec_host.c", "c")]
+HEADERS = ["tlsrec_device.h", "tlsrec_frame.h", "tlsrec_internal.h", "tlsrec_recdev.h", "tlsrec_gcm.h"]
+UNITS = [("gcm_dec.hip", "hip"), ("gcm_enc.hip", "hip"), ("gcm_alt_dec.hip", "hip"), ("gcm_alt_enc.hip", "hip"),
+         ("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("ccm.hip", "hip"), ("ticket.hip", "hip"), ("tlsrec_host.c", "c")]
 
 
 def _mtime(p):
@@ -57,7 +60,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-    with ThreadPoolExecutor(max_workers=min(4, max(1, len(cmds)))) as ex:
+    with ThreadPoolExecutor(max_workers=min(JOBS, max(1, len(cmds)))) as ex:
         list(ex.map(run, cmds))
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const uint32_t s = a.recs[my_rec].slot;
             const bool usable = s < a.capacity && a.slots[s].km.cipher != 0;
-            const int c = a.slots[s].km.cipher;
+            const int c = usable ? a.slots[s].km.cipher : 0;   /* no read past the table */
             if (usable && (ARIA ? tlsrec_cipher_is_alt_ccm(c) && tlsrec_cipher_alt_nr(c) == NR
                                 : tlsrec_cipher_is_ccm(c) && tlsrec_cipher_nr(c) == NR))
                 my_slot = s;

@@ -19,16 +19,21 @@
 
 using namespace tlsrec;
 
+struct HostPipe;   /* tlsrec_host_batch_*: device slots and streams, made on first use */
+
 struct tlsrec_keytab {
     uint32_t capacity;
     int device;
+    int cu;                   /* compute units of the device (launch sizing), read once at create */
     SlotState *d_slots;
     uint4 *d_ghtab;
     tlsrec_key_material *d_stage;
     uint8_t *h_cipher;        /* host mirror of each slot's cipher */
     uint32_t cipher_mask;     /* 1 << TLSREC_CIPHER_* of every loaded slot */
     uint32_t nloaded;         /* slots holding a key */
-    uint32_t has_cid;         /* some slot was given a DTLS connection ID: launch the CID kernels */
+    volatile uint32_t has_cid; /* some slot was given a DTLS connection ID: launch the CID kernels */
+    HostPipe *pipe;
+    pthread_mutex_t pipe_mu;
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED; }
@@ -61,6 +66,13 @@ extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
     if (!kt) return TLSREC_ERR_SSL_ALLOC_FAILED;
     kt->capacity = capacity;
     hipGetDevice(&kt->device);
+    kt->cu = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, kt->device) == hipSuccess && prop.multiProcessorCount > 0)
+            kt->cu = prop.multiProcessorCount;
+    }
+    pthread_mutex_init(&kt->pipe_mu, NULL);
     kt->h_cipher = (uint8_t *) calloc(capacity, 1);
     if (!kt->h_cipher ||
         hipMalloc((void **) &kt->d_slots, sizeof(SlotState) * (size_t) capacity) != hipSuccess ||
@@ -98,9 +110,13 @@ extern "C" int tlsrec_keytab_set_cid(tlsrec_keytab *kt, uint32_t slot, const uns
     return e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
 }
 
+static void host_pipe_free(HostPipe *p);
+
 extern "C" void tlsrec_keytab_free(tlsrec_keytab *kt)
 {
     if (!kt) return;
+    host_pipe_free(kt->pipe);
+    pthread_mutex_destroy(&kt->pipe_mu);
     if (kt->d_slots) {
         /* zeroize key material (ssl_msg.c:6084-6099 zeroizes transforms) */
         hipMemset(kt->d_slots, 0, sizeof(SlotState) * (size_t) kt->capacity);
@@ -260,23 +276,22 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     return 0;
 }
 
+/* only_cipher: launch only that cipher's kernel (the single-record engine,
+ * which knows the record's slot on the host); 0 = every cipher loaded. */
 static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
-                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec)
+                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec, uint32_t only_cipher = 0)
 {
     if (!kt || (!recs && n) || (!res && n)) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t) stream;
-    int cu = 256;
-    {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, kt->device) == hipSuccess && prop.multiProcessorCount > 0)
-            cu = prop.multiProcessorCount;
-    }
-    /* A table holding a single key needs no grouping: the kernels walk the
-     * descriptors in order and flag records naming an unusable slot.
-     * Otherwise the bucket pass groups GCM records by key (then ChaCha). */
+    const int cu = kt->cu;
+    const uint32_t cmask = only_cipher ? (kt->cipher_mask & (1u << only_cipher)) : kt->cipher_mask;
+    /* A table holding a single key, or a batch of one record, needs no
+     * grouping: the kernels walk the descriptors in order and flag records
+     * naming an unusable slot.  Otherwise the bucket pass groups GCM records
+     * by key (then ChaCha). */
     BucketScratch bs;
-    const bool identity = kt->nloaded == 1;
+    const bool identity = kt->nloaded == 1 || n == 1;
     if (!identity) {
         int r = bucket(kt, recs, res, n, st, bs);
         if (r) {
@@ -290,16 +305,17 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
                                         TLSREC_CIPHER_AES_192_GCM };
     for (int ci = 0; ci < 3 && !rc; ci++) {
         const int cipher = gcm_ciphers[ci];     /* bucket class ci: keys [ci * cap, (ci + 1) * cap) */
-        if (!(kt->cipher_mask & (1u << cipher))) continue;
+        if (!(cmask & (1u << cipher))) continue;
         /* (ARIA-GCM below: one configuration) */
         /* lanes per record: a key pass should still fill the 16 waves of a
          * workgroup.  8 for a single key or >= 128 records per key; 16
          * (4 records per wave) down to 48 records per key; 64 (one record per
          * wave) below that -- the many-connections, few-records regime of
          * the stream path. */
-        const uint32_t rpk = kt->nloaded > 1 ? n / kt->nloaded : n;
+        const uint32_t nl = kt->nloaded;     /* read once: the engine's pages change under it */
+        const uint32_t rpk = nl > 1 ? n / nl : n;
         int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
-                : (kt->nloaded <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
+                : (nl <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
         if (kt->has_cid) L = 8;     /* the CID variant: one configuration */
         GcmArgs a;
         a.slots = kt->d_slots;
@@ -331,7 +347,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
                                     TLSREC_CIPHER_CAMELLIA_256_GCM };
     for (int ci = 0; ci < 6 && !rc; ci++) {
         const int c = alt_gcm[ci];
-        if (!(kt->cipher_mask & (1u << c))) continue;
+        if (!(cmask & (1u << c))) continue;
         const size_t base = (size_t) (4 + ci) * cap + 1;
         GcmArgs a;
         a.slots = kt->d_slots;
@@ -354,9 +370,9 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     }
     uint32_t ccm_nr = 0;
     for (int c = TLSREC_CIPHER_AES_128_CCM; c <= TLSREC_CIPHER_AES_256_CCM_8; c++)
-        if (kt->cipher_mask & (1u << c)) ccm_nr |= 1u << tlsrec_cipher_nr(c);
+        if (cmask & (1u << c)) ccm_nr |= 1u << tlsrec_cipher_nr(c);
     for (int c = TLSREC_CIPHER_ARIA_128_CCM; c <= TLSREC_CIPHER_CAMELLIA_256_CCM; c++)   /* ARIA / Camellia: bit nr + 4 */
-        if (tlsrec_cipher_is_alt_ccm(c) && (kt->cipher_mask & (1u << c))) ccm_nr |= 1u << (tlsrec_cipher_alt_nr(c) + 4);
+        if (tlsrec_cipher_is_alt_ccm(c) && (cmask & (1u << c))) ccm_nr |= 1u << (tlsrec_cipher_alt_nr(c) + 4);
     if (!rc && ccm_nr) {
         CcmArgs a;
         a.slots = kt->d_slots;
@@ -373,7 +389,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.cid = kt->has_cid;
         if (tlsrec__launch_ccm(&a, dec, ccm_nr, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    if (!rc && (kt->cipher_mask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
+    if (!rc && (cmask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
         int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;
         if (kt->has_cid) L = 2;     /* the CID variant: one configuration */
         CpArgs a;
@@ -411,32 +427,228 @@ extern "C" int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_
     return batch(kt, recs, res, n, in_arena, out_arena, lanes_per_record, stream, 1);
 }
 
-/* ======================================================================
- * Engine used by the single-record API (tlsrec_host.c): a process-wide key
- * table with a slot allocator and a device staging area.
- * ==================================================================== */
-#define TLSREC_ENGINE_SLOTS 4096
 
-static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
-static tlsrec_keytab *g_kt = NULL;
-static uint8_t g_used[TLSREC_ENGINE_SLOTS];
-static hipStream_t g_stream = NULL;
-static uint8_t *g_dbuf = NULL;
-static size_t g_dbuf_len = 0;
-static void *g_dmeta = NULL;
+/* ======================================================================
+ * Records in host memory: chunked H2D -> kernel -> D2H pipeline
+ * (tlsrec_host_batch_*).  Records start and end in host socket buffers
+ * (SURVEY.md 8(d)); a chunk is a run of consecutive records, its byte range
+ * [buf_off of the first, end of the last) goes to one of NSLOT device slots,
+ * is protected there in place, and comes back to the same offsets of the
+ * output arena.  Three streams (H2D, kernels, D2H) chained by events keep
+ * both copy directions and the kernels busy at once.
+ * ==================================================================== */
+static constexpr int PIPE_SLOTS = 3;
+
+struct HostPipe {
+    hipStream_t h2d, cmp, d2h;
+    hipEvent_t ev_h2d[PIPE_SLOTS], ev_cmp[PIPE_SLOTS], ev_d2h[PIPE_SLOTS];
+    uint8_t *slot[PIPE_SLOTS];
+    size_t slot_bytes;
+    tlsrec_batch_rec *d_recs;
+    tlsrec_batch_res *d_res;
+    size_t nrec_cap;
+};
+
+static void host_pipe_free(HostPipe *p)
+{
+    if (!p) return;
+    if (p->h2d) hipStreamSynchronize(p->h2d);
+    if (p->cmp) hipStreamSynchronize(p->cmp);
+    if (p->d2h) hipStreamSynchronize(p->d2h);
+    for (int i = 0; i < PIPE_SLOTS; i++) {
+        hipFree(p->slot[i]);
+        if (p->ev_h2d[i]) hipEventDestroy(p->ev_h2d[i]);
+        if (p->ev_cmp[i]) hipEventDestroy(p->ev_cmp[i]);
+        if (p->ev_d2h[i]) hipEventDestroy(p->ev_d2h[i]);
+    }
+    hipFree(p->d_recs);
+    hipFree(p->d_res);
+    if (p->h2d) hipStreamDestroy(p->h2d);
+    if (p->cmp) hipStreamDestroy(p->cmp);
+    if (p->d2h) hipStreamDestroy(p->d2h);
+    delete p;
+}
+
+static int host_pipe_reserve(tlsrec_keytab *kt, size_t slot_bytes, size_t nrec)
+{
+    HostPipe *p = kt->pipe;
+    if (!p) {
+        p = new (std::nothrow) HostPipe();
+        if (!p) return TLSREC_ERR_SSL_ALLOC_FAILED;
+        kt->pipe = p;
+        if (hipStreamCreateWithFlags(&p->h2d, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&p->cmp, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&p->d2h, hipStreamNonBlocking) != hipSuccess)
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        for (int i = 0; i < PIPE_SLOTS; i++)
+            if (hipEventCreateWithFlags(&p->ev_h2d[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_cmp[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_d2h[i], hipEventDisableTiming) != hipSuccess)
+                return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (p->slot_bytes < slot_bytes) {
+        for (int i = 0; i < PIPE_SLOTS; i++) {
+            hipFree(p->slot[i]);
+            p->slot[i] = NULL;
+        }
+        p->slot_bytes = 0;
+        for (int i = 0; i < PIPE_SLOTS; i++)
+            if (hipMalloc((void **) &p->slot[i], slot_bytes) != hipSuccess) return TLSREC_ERR_SSL_ALLOC_FAILED;
+        p->slot_bytes = slot_bytes;
+    }
+    if (p->nrec_cap < nrec) {
+        hipFree(p->d_recs);
+        hipFree(p->d_res);
+        p->d_recs = NULL;
+        p->d_res = NULL;
+        p->nrec_cap = 0;
+        if (hipMalloc((void **) &p->d_recs, nrec * sizeof(tlsrec_batch_rec)) != hipSuccess ||
+            hipMalloc((void **) &p->d_res, nrec * sizeof(tlsrec_batch_res)) != hipSuccess)
+            return TLSREC_ERR_SSL_ALLOC_FAILED;
+        p->nrec_cap = nrec;
+    }
+    return 0;
+}
+
+static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
+                      const uint8_t *in, uint8_t *out, uint32_t lanes, uint64_t chunk_bytes, int dec)
+{
+    if (!kt || (n && (!recs || !res || !in || !out))) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (n == 0) return 0;
+    if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+    /* records in ascending, non-overlapping order; chunks of whole records */
+    struct Chunk { uint32_t first, count; uint64_t base, span; };
+    Chunk *ch = (Chunk *) malloc(sizeof(Chunk) * n);
+    if (!ch) return TLSREC_ERR_SSL_ALLOC_FAILED;
+    uint32_t nch = 0;
+    uint64_t maxspan = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t lo = recs[i].buf_off, hi = lo + recs[i].buf_len;
+        if (i && lo < recs[i - 1].buf_off + recs[i - 1].buf_len) {
+            free(ch);
+            return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+        }
+        if (nch && hi - ch[nch - 1].base <= chunk_bytes) {
+            ch[nch - 1].count++;
+            ch[nch - 1].span = hi - ch[nch - 1].base;
+        } else {
+            ch[nch++] = Chunk{ i, 1, lo, hi - lo };
+        }
+        if (ch[nch - 1].span > maxspan) maxspan = ch[nch - 1].span;
+    }
+    pthread_mutex_lock(&kt->pipe_mu);
+    int rc = host_pipe_reserve(kt, (maxspan + 255) / 256 * 256, n);
+    HostPipe *p = kt->pipe;
+    if (!rc && hipMemcpyAsync(p->d_recs, recs, (size_t) n * sizeof(*recs), hipMemcpyHostToDevice, p->cmp) != hipSuccess)
+        rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    for (uint32_t c = 0; c < nch && !rc; c++) {
+        const int k = (int) (c % PIPE_SLOTS);
+        const Chunk &C = ch[c];
+        hipError_t e = hipSuccess;
+        if (c >= PIPE_SLOTS) e = hipStreamWaitEvent(p->h2d, p->ev_d2h[k], 0);      /* slot drained */
+        if (e == hipSuccess) e = hipMemcpyAsync(p->slot[k], in + C.base, C.span, hipMemcpyHostToDevice, p->h2d);
+        if (e == hipSuccess) e = hipEventRecord(p->ev_h2d[k], p->h2d);
+        if (e == hipSuccess) e = hipStreamWaitEvent(p->cmp, p->ev_h2d[k], 0);
+        if (e != hipSuccess) {
+            rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+            break;
+        }
+        /* the descriptors' buf_off are offsets into the host arena: shift the
+         * device arena base so that base + buf_off lands in the slot */
+        uint8_t *dev = (uint8_t *) ((uintptr_t) p->slot[k] - (uintptr_t) C.base);
+        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, dev, lanes, p->cmp, dec);
+        if (rc) break;
+        e = hipEventRecord(p->ev_cmp[k], p->cmp);
+        if (e == hipSuccess) e = hipStreamWaitEvent(p->d2h, p->ev_cmp[k], 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(out + C.base, p->slot[k], C.span, hipMemcpyDeviceToHost, p->d2h);
+        if (e == hipSuccess) e = hipEventRecord(p->ev_d2h[k], p->d2h);
+        if (e != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (!rc && (hipStreamSynchronize(p->cmp) != hipSuccess ||
+                hipMemcpyAsync(res, p->d_res, (size_t) n * sizeof(*res), hipMemcpyDeviceToHost, p->d2h) != hipSuccess))
+        rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (p) {
+        /* drain every stream before the caller may reuse its buffers */
+        if (hipStreamSynchronize(p->h2d) != hipSuccess || hipStreamSynchronize(p->cmp) != hipSuccess ||
+            hipStreamSynchronize(p->d2h) != hipSuccess)
+            rc = rc ? rc : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    pthread_mutex_unlock(&kt->pipe_mu);
+    free(ch);
+    return rc;
+}
+
+extern "C" int tlsrec_host_batch_encrypt(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                         uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
+                                         uint32_t lanes_per_record, uint64_t chunk_bytes)
+{
+    return host_batch(kt, recs, res, n, in_arena, out_arena, lanes_per_record, chunk_bytes, 0);
+}
+
+extern "C" int tlsrec_host_batch_decrypt(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                         uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
+                                         uint32_t lanes_per_record, uint64_t chunk_bytes)
+{
+    return host_batch(kt, recs, res, n, in_arena, out_arena, lanes_per_record, chunk_bytes, 1);
+}
+
+/* ======================================================================
+ * Engine used by the single-record API (tlsrec_host.c).
+ *
+ * Key slots live in pages of ENGINE_PAGE_SLOTS (one key table each), added
+ * as connections arrive -- ENGINE_MAX_PAGES x 4096 = 1 M slots, i.e. 512 K
+ * connections per process.  Records run on one of ENGINE_CTXS staging
+ * contexts (stream + pinned host buffer + device buffer), so threads serving
+ * different connections do not serialise on one lock.  A record is one
+ * H2D copy (descriptor + buffer + CID), one kernel of its own cipher (no
+ * bucket pass: a batch of one), one D2H copy (result + buffer), one sync.
+ * ==================================================================== */
+#define ENGINE_PAGE_SLOTS 4096
+#define ENGINE_MAX_PAGES 256
+#define ENGINE_CTXS 8
+
+struct EnginePage {
+    tlsrec_keytab *kt;
+    uint8_t used[ENGINE_PAGE_SLOTS];
+    uint32_t nused;
+};
+
+struct EngineCtx {
+    pthread_mutex_t mu;
+    hipStream_t st;
+    uint8_t *h;              /* pinned: [rec 64][res 64][buffer][cid] */
+    uint8_t *d;
+    size_t cap;
+};
+
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;   /* slot allocation, page growth */
+static EnginePage g_pages[ENGINE_MAX_PAGES];
+static volatile int g_npages = 0;
+static hipStream_t g_load = NULL;
+static EngineCtx g_ctx[ENGINE_CTXS];
+static volatile int g_ctx_ready = 0;
 
 static int engine_init_locked(void)
 {
-    if (g_kt) return 0;
-    int r = tlsrec_keytab_create(&g_kt, TLSREC_ENGINE_SLOTS);
-    if (r) return r;
-    if (hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&g_dmeta, 64) != hipSuccess) {
-        tlsrec_keytab_free(g_kt);
-        g_kt = NULL;
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (g_ctx_ready) return 0;
+    if (tlsrec_device_check() != 0) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (hipStreamCreateWithFlags(&g_load, hipStreamNonBlocking) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    for (int i = 0; i < ENGINE_CTXS; i++) {
+        pthread_mutex_init(&g_ctx[i].mu, NULL);
+        if (hipStreamCreateWithFlags(&g_ctx[i].st, hipStreamNonBlocking) != hipSuccess)
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
+    g_ctx_ready = 1;
     return 0;
+}
+
+static tlsrec_keytab *slot_table(int slot, uint32_t *idx)
+{
+    if (slot < 0) return NULL;
+    const int pg = slot / ENGINE_PAGE_SLOTS;
+    if (pg >= g_npages) return NULL;
+    *idx = (uint32_t) (slot % ENGINE_PAGE_SLOTS);
+    return g_pages[pg].kt;
 }
 
 extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
@@ -444,15 +656,30 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
     pthread_mutex_lock(&g_mu);
     int r = engine_init_locked();
     int slot = -1;
+    int pg = 0;
     if (r == 0) {
-        for (int i = 0; i < TLSREC_ENGINE_SLOTS; i++)
-            if (!g_used[i]) { slot = i; break; }
-        if (slot < 0) r = TLSREC_ERR_SSL_ALLOC_FAILED;
+        for (pg = 0; pg < g_npages; pg++)
+            if (g_pages[pg].nused < ENGINE_PAGE_SLOTS) break;
+        if (pg == g_npages) {
+            if (pg == ENGINE_MAX_PAGES) {
+                r = TLSREC_ERR_SSL_ALLOC_FAILED;
+            } else {
+                r = tlsrec_keytab_create(&g_pages[pg].kt, ENGINE_PAGE_SLOTS);
+                if (r == 0) g_npages = pg + 1;
+            }
+        }
     }
     if (r == 0) {
-        r = tlsrec_keytab_load(g_kt, (uint32_t) slot, 1, km, 0, g_stream);
-        if (r == 0 && hipStreamSynchronize(g_stream) != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) g_used[slot] = 1;
+        EnginePage &P = g_pages[pg];
+        for (int i = 0; i < ENGINE_PAGE_SLOTS; i++)
+            if (!P.used[i]) { slot = i; break; }
+        r = tlsrec_keytab_load(P.kt, (uint32_t) slot, 1, km, 0, g_load);
+        if (r == 0 && hipStreamSynchronize(g_load) != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) {
+            P.used[slot] = 1;
+            P.nused++;
+            slot += pg * ENGINE_PAGE_SLOTS;
+        }
     }
     pthread_mutex_unlock(&g_mu);
     return r ? r : slot;
@@ -460,66 +687,112 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
 
 extern "C" void tlsrec__engine_slot_free(int slot)
 {
-    if (slot < 0 || slot >= TLSREC_ENGINE_SLOTS) return;
     pthread_mutex_lock(&g_mu);
-    if (g_kt && g_used[slot]) {
-        hipMemsetAsync(g_kt->d_slots + slot, 0, sizeof(SlotState), g_stream);
-        hipMemsetAsync(g_kt->d_ghtab + (size_t) slot * KEY_TABLE_WORDS, 0, sizeof(uint4) * KEY_TABLE_WORDS,
-                       g_stream);
-        hipStreamSynchronize(g_stream);
-        g_used[slot] = 0;
+    uint32_t i = 0;
+    tlsrec_keytab *kt = slot_table(slot, &i);
+    EnginePage *P = kt ? &g_pages[slot / ENGINE_PAGE_SLOTS] : NULL;
+    if (kt && P->used[i]) {
+        /* zeroize (ssl_msg.c:6084-6099); the slot's cipher stays recorded in the
+         * table's mask, so a later batch of this page may launch one kernel more */
+        hipMemsetAsync(kt->d_slots + i, 0, sizeof(SlotState), g_load);
+        hipMemsetAsync(kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS, 0, sizeof(uint4) * KEY_TABLE_WORDS, g_load);
+        hipStreamSynchronize(g_load);
+        kt->h_cipher[i] = 0;
+        kt->nloaded--;
+        P->used[i] = 0;
+        P->nused--;
     }
     pthread_mutex_unlock(&g_mu);
 }
 
 extern "C" int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, size_t cid_len)
 {
-    if (slot < 0 || slot >= TLSREC_ENGINE_SLOTS) return TLSREC_ERR_SSL_INTERNAL_ERROR;
     pthread_mutex_lock(&g_mu);
-    int r = g_kt && g_used[slot] ? tlsrec_keytab_set_cid(g_kt, (uint32_t) slot, cid, cid_len, g_stream)
-                                 : TLSREC_ERR_SSL_INTERNAL_ERROR;
+    uint32_t i = 0;
+    tlsrec_keytab *kt = slot_table(slot, &i);
+    int r = kt && g_pages[slot / ENGINE_PAGE_SLOTS].used[i] ? tlsrec_keytab_set_cid(kt, i, cid, cid_len, g_load)
+                                                            : TLSREC_ERR_SSL_INTERNAL_ERROR;
     pthread_mutex_unlock(&g_mu);
     return r;
 }
 
-/* Run one record through the batch kernels: host buffer -> device -> host.
- * A decrypted record's CID (cid_len bytes) is staged right after the buffer
+/* a staging context: the first free one from a per-thread start, else wait */
+static EngineCtx *ctx_acquire(void)
+{
+    static volatile unsigned next = 0;
+    static __thread int home = -1;
+    if (home < 0) home = (int) (__atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED) % ENGINE_CTXS);
+    for (int k = 0; k < ENGINE_CTXS; k++) {
+        EngineCtx *c = &g_ctx[(home + k) % ENGINE_CTXS];
+        if (pthread_mutex_trylock(&c->mu) == 0) return c;
+    }
+    EngineCtx *c = &g_ctx[home];
+    pthread_mutex_lock(&c->mu);
+    return c;
+}
+
+/* Run one record through the kernels: host buffer -> device -> host.  A
+ * decrypted record's CID (cid_len bytes) is staged right after the buffer
  * (rec->cid_off = buf_len). */
 extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
                                   const unsigned char *cid, tlsrec_batch_res *out)
 {
-    pthread_mutex_lock(&g_mu);
-    int r = engine_init_locked();
-    if (r == 0 && g_dbuf_len < buf_len + 16 + TLSREC_CID_LEN_MAX) {
-        hipFree(g_dbuf);
-        g_dbuf = NULL;
-        g_dbuf_len = 0;
-        size_t want = buf_len + 16 + TLSREC_CID_LEN_MAX > 65536 ? buf_len + 16 + TLSREC_CID_LEN_MAX : 65536;
-        if (hipMalloc((void **) &g_dbuf, want) != hipSuccess) r = TLSREC_ERR_SSL_ALLOC_FAILED;
-        else g_dbuf_len = want;
+    if (!g_ctx_ready) {
+        pthread_mutex_lock(&g_mu);
+        int r = engine_init_locked();
+        pthread_mutex_unlock(&g_mu);
+        if (r) return r;
+    }
+    uint32_t idx = 0;
+    tlsrec_keytab *kt = slot_table((int) rec->slot, &idx);
+    if (!kt) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    const uint32_t cipher = kt->h_cipher[idx];
+    if (cipher == 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
+    EngineCtx *c = ctx_acquire();
+    int r = 0;
+    const size_t need = 128 + buf_len + TLSREC_CID_LEN_MAX + 16;
+    if (c->cap < need) {
+        hipHostFree(c->h);
+        hipFree(c->d);
+        c->h = NULL;
+        c->d = NULL;
+        c->cap = 0;
+        const size_t want = need > 65536 ? need : 65536;
+        if (hipHostMalloc((void **) &c->h, want, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void **) &c->d, want) != hipSuccess)
+            r = TLSREC_ERR_SSL_ALLOC_FAILED;
+        else
+            c->cap = want;
     }
     if (r == 0) {
         tlsrec_batch_rec d = *rec;
+        d.slot = idx;
         d.buf_off = 0;
-        tlsrec_batch_rec *d_rec = (tlsrec_batch_rec *) g_dmeta;
-        tlsrec_batch_res *d_res = (tlsrec_batch_res *) ((uint8_t *) g_dmeta + 48);
-        hipError_t e = hipSuccess;
-        if (buf_len) e = hipMemcpyAsync(g_dbuf, buf, buf_len, hipMemcpyHostToDevice, g_stream);
-        if (e == hipSuccess && d.cid_len) {
-            e = hipMemcpyAsync(g_dbuf + buf_len, cid, d.cid_len, hipMemcpyHostToDevice, g_stream);
+        size_t up = 128 + buf_len;
+        if (d.cid_len) {
+            memcpy(c->h + 128 + buf_len, cid, d.cid_len);
             const uint32_t off = (uint32_t) buf_len;
             d.cid_off[0] = (uint8_t) off; d.cid_off[1] = (uint8_t) (off >> 8);
             d.cid_off[2] = (uint8_t) (off >> 16); d.cid_off[3] = (uint8_t) (off >> 24);
+            up += d.cid_len;
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(d_rec, &d, sizeof(d), hipMemcpyHostToDevice, g_stream);
+        memcpy(c->h, &d, sizeof(d));
+        if (buf_len) memcpy(c->h + 128, buf, buf_len);
+        tlsrec_batch_rec *d_rec = (tlsrec_batch_rec *) c->d;
+        tlsrec_batch_res *d_res = (tlsrec_batch_res *) (c->d + 64);
+        hipError_t e = hipMemcpyAsync(c->d, c->h, up, hipMemcpyHostToDevice, c->st);
         if (e == hipSuccess) {
-            r = batch(g_kt, d_rec, d_res, 1, g_dbuf, g_dbuf, 0, g_stream, dec);
-            if (r == 0 && buf_len) e = hipMemcpyAsync(buf, g_dbuf, buf_len, hipMemcpyDeviceToHost, g_stream);
-            if (r == 0 && e == hipSuccess) e = hipMemcpyAsync(out, d_res, sizeof(*out), hipMemcpyDeviceToHost, g_stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
+            r = batch(kt, d_rec, d_res, 1, c->d + 128, c->d + 128, 0, c->st, dec, cipher);
+            if (r == 0)
+                e = hipMemcpyAsync(c->h + 64, c->d + 64, 64 + buf_len, hipMemcpyDeviceToHost, c->st);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->st);
         }
         if (e != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) {
+            memcpy(out, c->h + 64, sizeof(*out));
+            if (buf_len) memcpy(buf, c->h + 128, buf_len);
+        }
     }
-    pthread_mutex_unlock(&g_mu);
+    pthread_mutex_unlock(&c->mu);
     return r;
 }

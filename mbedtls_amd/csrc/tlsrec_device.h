@@ -859,6 +859,16 @@ __device__ __forceinline__ uint4 p_finish(P5 h, uint4 s)
     return make_uint4(o0, o1, o2, (uint32_t) f);
 }
 
+/* compile-time log2 of a power of two (lanes per record, tree depths) */
+template <int L> struct Log2;
+template <> struct Log2<1> { static constexpr int v = 0; };
+template <> struct Log2<2> { static constexpr int v = 1; };
+template <> struct Log2<4> { static constexpr int v = 2; };
+template <> struct Log2<8> { static constexpr int v = 3; };
+template <> struct Log2<16> { static constexpr int v = 4; };
+template <> struct Log2<32> { static constexpr int v = 5; };
+template <> struct Log2<64> { static constexpr int v = 6; };
+
 } /* namespace tlsrec */
 
 #endif /* TLSREC_DEVICE_H */

@@ -1,0 +1,512 @@
+/*
+ * tlsrec_gcm.h -- the GCM record kernel (AES, and ARIA / Camellia through the
+ * LDS-table cipher slot) and its launch dispatch.  Included by the per-
+ * direction translation units gcm_enc.hip / gcm_dec.hip / gcm_alt_enc.hip /
+ * gcm_alt_dec.hip, which instantiate it (the instantiations dominate the
+ * build; one unit per direction lets them compile in parallel).
+ */
+#ifndef TLSREC_GCM_H
+#define TLSREC_GCM_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <type_traits>
+
+#include "tlsrec.h"
+#include "tlsrec_device.h"
+#include "tlsrec_frame.h"
+#include "tlsrec_internal.h"
+#include "tlsrec_recdev.h"
+
+namespace tlsrec {
+
+/* ======================================================================
+ * AES-GCM
+ * ==================================================================== */
+/* WP (wave passes): each wave keeps only its current key's H^L table in its
+ * own 8 KiB of LDS; the once-per-record multiplies (AAD fold, tree, final)
+ * read the key's tables in global memory. */
+template <int L, int W, bool WP = false>
+struct GcmLds {
+    static constexpr int NT = WP ? W : Log2<L>::v + 1;  /* GHASH tables H^1 .. H^L, or one H^L per wave */
+    static constexpr int GH = 0;
+    static constexpr int AES = NT * 8192;               /* T0/T1 x 32 copies */
+    static constexpr int EJ0 = AES + 65536;             /* W waves x 64 x 16 B */
+    static constexpr int FOLD = EJ0 + W * 64 * 16;      /* W waves x 64 x 16 B: AAD fold */
+    static constexpr int CTL = FOLD + W * 64 * 16;
+    static constexpr int BYTES = CTL + 16;
+};
+
+/* Per-record state that the AEAD loop reads (kept small: it lives in
+ * VGPRs across the loop). */
+struct GcmJob {
+    bool run, aligned, inner;   /* inner: TLS 1.3 / DTLS 1.2 + CID inner plaintext */
+    uint8_t inner_type;
+    uint32_t aead_len, content_len, aad_len;
+    uint32_t nw0, nw1, nw2;
+    uint4 aadw;
+    const uint8_t *src;
+    uint8_t *dst;
+
+    template <bool DEC>
+    __device__ __forceinline__ void setup(const tlsrec_plan &p, const tlsrec_batch_rec &d, const uint8_t *in,
+                                          uint8_t *out)
+    {
+        uint32_t nw[3];
+        nonce_words<DEC>(p, d, in, nw);
+        nw0 = nw[0]; nw1 = nw[1]; nw2 = nw[2];
+        aadw = aad_words(p);
+        aad_len = p.aad_len;
+        aead_len = p.aead_len;
+        content_len = DEC ? p.aead_len : p.content_len;
+        inner_type = p.inner_type;
+        inner = p.inner;
+        src = in + d.buf_off + p.aead_pos;
+        dst = out + d.buf_off + p.aead_pos;
+        /* 16-byte global accesses need no 16-byte alignment on gfx950: the
+         * HSA target runs in unaligned-access mode (hipcc emits
+         * global_load_dwordx4 for a byte-aligned 16-byte memcpy), so records
+         * at any byte offset -- the stream path's records follow 5-byte
+         * headers -- take the wide path; the wide read of a block never
+         * leaves the record buffer (tag / tag room follows the AEAD data) */
+        aligned = true;
+        run = true;
+    }
+};
+
+/* GHASH Horner over blocks 0..3 of a CID record's AAD (block 0 = a0), leaving
+ * the last block un-multiplied (the kernel's AAD fold applies that H).  Out
+ * of line: CID records are rare, the record kernel's registers are not. */
+__device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, const tlsrec_plan &p,
+                                               const tlsrec_batch_rec &d, const uint8_t *cid)
+{
+    uint4 f = xor4(gmul<0>(gp, a0), cid_aad_block<1, 0>(p, d, cid));
+    if (p.aad_len > 32) f = xor4(gmul<0>(gp, f), cid_aad_block<2, 0>(p, d, cid));
+    if (p.aad_len > 48) f = xor4(gmul<0>(gp, f), cid_aad_block<3, 0>(p, d, cid));
+    return f;
+}
+
+/* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0 */
+template <int SH>
+__device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
+{
+    if constexpr (SH >= 1) {
+        uint4 o = shfl4(Y, (lane + SH) & 63);
+        Y = xor4(gmul<Log2<SH>::v>(lds, Y), o);
+        return gtree<SH / 2>(lds, Y, lane);
+    } else {
+        return Y;
+    }
+}
+
+/* ARIA: the block cipher is ARIA (NR = 12/14/16 rounds, S-box tables in the
+ * T-table LDS region, round keys SlotState::ark) -- GCM around it unchanged */
+template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false, bool ARIA = false>
+__global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
+{
+    using LY = GcmLds<L, W, WP>;
+    constexpr int NTHR = W * 64;
+    constexpr int LOGL = Log2<L>::v;
+    constexpr int R = 64 / L;
+    /* the kernel's only LDS object, so it starts at LDS address 0 and every
+     * table offset folds into the ds_read immediate */
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LY::BYTES];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g = lane / L, q = lane % L;
+    const uint32_t lanebase = ARIA ? (uint32_t) (lane & 15) << 2 : (uint32_t) (lane & 31) << 2;
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + LY::CTL);
+
+    /* This workgroup's positions: wave w owns positions base + k*W + w,
+     * k < rpw (interleaved, so a key's run of records in perm spreads over
+     * all waves of the workgroup within one key pass). */
+    const uint32_t lo = a.perm ? *a.lo : 0u;
+    const uint32_t count = a.perm ? *a.hi - lo : (uint32_t) a.n;
+    const uint64_t wg_base = (uint64_t) blockIdx.x * W * a.rpw;
+    if (wg_base >= count) return;                      /* uniform: before any barrier */
+
+    if constexpr (ARIA)
+        alt_fill_tables<NR>(lds + LY::AES, tid, NTHR);
+    else
+        aes_fill_tables(lds + LY::AES, tid, NTHR);
+
+    /* pass membership: lane l tracks the record at chunk position k = l */
+    uint32_t my_slot = 0xffffffffu, my_rec = 0;
+    {
+        /* WP: a wave's positions are contiguous (its key runs stay together) */
+        const uint64_t pos = WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
+        if (lane < (int) a.rpw && pos < count) {
+            my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
+            const uint32_t s = a.recs[my_rec].slot;
+            if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
+                my_slot = s;
+            } else if (!a.perm && !(s < a.capacity && a.slots[s].km.cipher != 0)) {
+                /* identity order: this kernel is the only one that sees the record */
+                bad_slot_result(a.recs[my_rec], &a.res[my_rec]);
+            }
+        }
+    }
+    if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
+    __syncthreads();
+
+    /* Horner multiplier table H^L (hor) and the per-record tables H^1..H^(L/2) (gp) */
+    constexpr int HPI = WP ? 0 : LOGL;                   /* H^L table index from hor */
+    const uint8_t *hor = WP ? lds + LY::GH + wave * 8192 : lds + LY::GH;
+    for (int iter = 0;; iter++) {
+        uint32_t s;
+        if constexpr (WP) {
+            /* wave pass: the wave's smallest pending slot; stage its H^L table
+             * into the wave's LDS (in-order LDS queue: the wave's writes land
+             * before its reads; the asm keeps the compiler from hoisting) */
+            s = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
+            if (s == 0xffffffffu) break;
+            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
+            uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
+            for (int i = lane; i < 512; i += 64) dst[i] = src[i];
+            asm volatile("" ::: "memory");
+        } else {
+            uint32_t *cur = &ctl[iter & 1];
+            if (my_slot != 0xffffffffu) atomicMin(cur, my_slot);
+            __syncthreads();
+            s = __builtin_amdgcn_readfirstlane(*cur);
+            if (s == 0xffffffffu) break;
+            if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
+            /* stage the slot's GHASH tables and round keys */
+            {
+                const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
+                uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
+                for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
+            }
+            __syncthreads();
+        }
+        const uint8_t *gp = WP ? reinterpret_cast<const uint8_t *>(a.ghtab + (size_t) s * KEY_TABLE_WORDS) : lds + LY::GH;
+        /* Round keys through the constant address space: scalar loads.  (Read
+         * through a.slots they compile to vector loads + vmcnt(0) waits in
+         * every round, since the kernel's own stores might alias the table.) */
+        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) (ARIA ? a.slots[s].ark : a.slots[s].rkr);
+        const tlsrec_key_material km = a.slots[s].km;
+
+        /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
+        {
+            uint4 ej0 = make_uint4(0, 0, 0, 0);
+            bool mine = my_slot == s;
+            uint32_t nw[3] = { 0, 0, 0 };
+            if (mine) {
+                const tlsrec_batch_rec d = a.recs[my_rec];
+                tlsrec_plan p;
+                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+                nonce_words<DEC>(p, d, a.in, nw);
+            }
+            if constexpr (ARIA)
+                ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+            else
+                ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+            reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
+        }
+        /* lanes of this wave read other lanes' E(J0): the wave's own LDS
+         * writes complete before its later reads (in-order LDS queue). */
+
+        /* ---- record rounds: L lanes per record, R records per wave ---- */
+        for (uint32_t rr = 0; rr < a.rpw; rr += R) {
+            const uint32_t slot_in_chunk = rr + (uint32_t) g;
+            const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
+            const bool active = slot_in_chunk < a.rpw && owner_slot == s;
+            /* a key's records sit in a contiguous run of each wave's chunk
+             * positions: rounds holding none of them are skipped (wave-uniform,
+             * no barrier inside the round) -- with many keys of few records
+             * each, the pass would otherwise walk all rpw positions */
+            if (__ballot(active) == 0) continue;
+            const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
+            /* Only what the AEAD loop needs stays live across it; the plan is
+             * re-derived from the (cached) descriptor afterwards. */
+            GcmJob jb;
+            jb.run = false;
+            if (active) {
+                const tlsrec_batch_rec d = a.recs[ridx];
+                tlsrec_plan p;
+                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+                if (p.status != 0) {
+                    if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
+                } else {
+                    jb.setup<DEC>(p, d, a.in, a.out);
+                    /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
+                     * into the block the AAD fold multiplies by H below */
+                    if (CID && p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
+                }
+            }
+            const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
+            const uint32_t mm = m ? m : 1;
+            constexpr uint32_t BL = (uint32_t) (B * L);
+            const uint32_t z = (BL - mm % BL) % BL;                    /* front padding */
+            const uint32_t J = jb.run ? (mm + z) / BL : 0;
+            const uint32_t Jmax = wave_max(J);
+            /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
+             * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
+             * only the step with cc == 0 reads it. */
+            uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + wave * 64 + lane;
+            {
+                const uint4 aadh = gmul<0>(gp, jb.aadw);
+                *fold = m ? aadh : jb.aadw;
+            }
+            /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
+             * does not depend on step j's keystream, so its table reads share
+             * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
+            uint4 Z = make_uint4(0, 0, 0, 0), Xp = make_uint4(0, 0, 0, 0);
+            /* TLS 1.3 inner type: position + 1 of the last non-zero output block */
+            uint32_t nzpos = 0;
+            /* a readable 16-byte address for lanes with nothing to load */
+            const uint8_t *safe = jb.run ? jb.src : reinterpret_cast<const uint8_t *>(a.recs);
+            /* Body steps [1, jh): every lane of the wave holds a full, aligned
+             * block inside its record's content (wave-uniform bound), so they run
+             * without masks or branches.  Step 0 (AAD fold, front padding) and
+             * the tail (partial blocks, ragged lengths) take the general step. */
+            uint32_t jh = 0;
+            {
+                const uint32_t mfast = (jb.run && jb.aligned) ? jb.content_len / 16 : 0;
+                uint32_t h = jb.run ? (mfast + z) / BL : 0;
+                h = wave_min(h);
+                jh = h > 1 ? h : 0;
+            }
+            const uint32_t jl = jh ? 1u : Jmax;
+            auto steps = [&](auto cached) {
+                constexpr bool CACHED = decltype(cached)::value;
+                CtrCache ccache;
+                if constexpr (CACHED) ccache = ctr_cache<LY::AES>(lds, lanebase, rk, jb.nw0, jb.nw1, jb.nw2);
+                auto crypt = [&](int32_t cc, uint4 y, uint4 &ks, uint4 &Zn) {
+                    const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
+                    if constexpr (CACHED) {
+                        aes_ghash<NR, LY::AES, HPI>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
+                    } else {
+                        if constexpr (ARIA)
+                            ks = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                        else
+                            ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                        Zn = gmul<HPI>(hor, y);
+                    }
+                };
+                auto general = [&](uint32_t j) {
+                    const bool live = jb.run && j < J;
+#pragma unroll
+                    for (int b = 0; b < B; b++) {
+                        const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                        const bool valid = live && cc >= 0 && (uint32_t) cc < m;
+                        const uint32_t pos = (uint32_t) cc * 16;
+                        /* full, aligned interior block: plain 16-byte load/store */
+                        const bool fast = valid && jb.aligned && pos + 16 <= jb.content_len;
+                        uint4 blk = gload16(fast ? jb.src + pos : safe);
+                        uint4 ks, Zn;
+                        crypt(cc, xor4(Z, Xp), ks, Zn);
+                        uint4 X = make_uint4(0, 0, 0, 0);
+                        if (fast) {
+                            const uint4 o = xor4(blk, ks);
+                            gstore16(jb.dst + pos, o);
+                            X = DEC ? blk : o;
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                        } else if (valid) {
+                            blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type, jb.aligned);
+                            const uint4 o = mask_block(xor4(blk, ks), pos, jb.aead_len);
+                            store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
+                            X = DEC ? blk : o;
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                        }
+                        if (live && cc == 0) X = xor4(X, *fold);
+                        if (live) { Z = Zn; Xp = X; }
+                    }
+                };
+                uint32_t j = 0;
+                for (; j < jl; j++) general(j);
+                {
+                    const uint8_t *sp = jb.src + (size_t) (BL * j + q - z) * 16;
+                    uint8_t *dp = jb.dst + (size_t) (BL * j + q - z) * 16;
+                    for (; j < jh; j++) {
+#pragma unroll
+                        for (int b = 0; b < B; b++) {
+                            const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                            const uint4 blk = gload16(sp + 16 * L * b);
+                            uint4 ks, Zn;
+                            crypt(cc, xor4(Z, Xp), ks, Zn);
+                            const uint4 o = xor4(blk, ks);
+                            gstore16(dp + 16 * L * b, o);
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
+                            Z = Zn;
+                            Xp = DEC ? blk : o;
+                        }
+                        sp += 16 * BL;
+                        dp += 16 * BL;
+                    }
+                }
+                for (; j < Jmax; j++) general(j);
+            };
+            /* counters stay below 2^16 (any TLS record): cached rounds 1-2 */
+            if constexpr (ARIA) {
+                steps(std::integral_constant<bool, false>());   /* no cached rounds for ARIA */
+            } else {
+                if (wave_max(m) + 2 < 65536u)
+                    steps(std::integral_constant<bool, true>());
+                else
+                    steps(std::integral_constant<bool, false>());
+            }
+            uint4 Y = xor4(Z, Xp);
+            uint32_t nzkey = 0;
+            if (DEC && jb.inner && nzpos) {
+                /* the lane's last non-zero plaintext block, as written above */
+                const uint32_t pos = nzpos - 1;
+                nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
+            }
+            /* tree: sum_q Y_q H^(L-q) */
+            Y = gtree<L / 2>(gp, Y, lane);
+            Y = gmul<0>(gp, Y);                                      /* T */
+            uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
+            Y = gmul<0>(gp, xor4(Y, lenw));                          /* GHASH */
+            if (!jb.run) continue;
+            const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
+            const uint4 tag = xor4(Y, ej0);
+            const tlsrec_batch_rec d = a.recs[ridx];
+            tlsrec_plan p;
+            make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+            if (!DEC) {
+                if (q == 0) {
+                    store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
+                    if (p.explicit_iv && p.post_status == 0) {
+                        uint8_t *e = a.out + d.buf_off + p.data_offset;
+                        for (int i = 0; i < 8; i++) e[i] = d.ctr[i];
+                    }
+                    tlsrec_batch_res r;
+                    r.status = p.post_status;
+                    r.data_offset = p.data_offset;
+                    r.data_len = p.data_len;
+                    r.type = p.type;
+                    r.cid_len = p.cid_set ? p.cid_len : 0;
+                    r.reserved[0] = r.reserved[1] = 0;
+                    a.res[ridx] = r;
+                }
+            } else {
+                uint4 want = load_block(jb.src, jb.aead_len, jb.aead_len + 16, jb.aead_len + 16, 0, false);
+                uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
+                diff = __shfl(diff, lane - q);                        /* group leader's verdict */
+                uint32_t key = group_max<L>(nzkey);
+                tlsrec_batch_res r;
+                r.data_offset = p.data_offset;
+                r.data_len = p.data_len;
+                r.type = d.type;
+                r.cid_len = 0;
+                r.reserved[0] = r.reserved[1] = 0;
+                if (diff != 0) {
+                    /* PSA wipes the whole output buffer on a bad tag */
+                    zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
+                    r.status = TLSREC_E_INVALID_MAC;
+                } else if (p.inner) {                                /* ssl_msg.c:1809-1829 */
+                    if (key == 0) {
+                        r.status = TLSREC_E_INVALID_RECORD;
+                    } else {
+                        r.status = 0;
+                        r.data_len = (key >> 8) - 1;
+                        r.type = (uint8_t) (key & 0xff);
+                    }
+                } else {
+                    r.status = 0;
+                }
+                if (q == 0) a.res[ridx] = r;
+            }
+        }
+        my_slot = (my_slot == s) ? 0xffffffffu : my_slot;
+    }
+}
+
+/* ======================================================================
+ * Launchers
+ * ==================================================================== */
+template <int L, int NR, bool DEC>
+static hipError_t launch_gcm_wp(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    /* wave passes: 8 waves x 2 blocks per lane (LDS: 8 x 8 KiB H^L + 64 KiB T-tables) */
+    hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 8, 2, true>), dim3(grid), dim3(8 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
+/* ARIA-GCM: one configuration (8 lanes, ARIA_GCM_WAVES = 16 waves), with or
+ * without CIDs.  The ARIA round spills ~50 VGPRs at this budget; the 8-wave
+ * variant (no spills) measured 291 vs 357 GiB/s: occupancy wins. */
+template <int NR, bool DEC>
+static hipError_t launch_gcm_aria(const GcmArgs &a, uint32_t grid, hipStream_t st, bool cid)
+{
+    static_assert(ARIA_GCM_WAVES == 16, "ARIA-GCM launch shape");
+    if (cid)
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, true, true>), dim3(grid), dim3(16 * 64), 0, st, a);
+    else
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, false, true>), dim3(grid), dim3(16 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
+/* key tables with DTLS connection IDs: one configuration (8 lanes, 16 waves) */
+template <int NR, bool DEC>
+static hipError_t launch_gcm_cid(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((tlsrec_gcm_kernel<8, NR, DEC, 16, 1, false, true>), dim3(grid), dim3(16 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int L, int NR, bool DEC, int W>
+static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    /* 16 waves x 1 block per lane, or 8 waves x 2 independent blocks per lane */
+    if constexpr (W == 8)
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 8, 2>), dim3(grid), dim3(8 * 64), 0, st, a);
+    else
+        hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 16, 1>), dim3(grid), dim3(16 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int L, bool DEC>
+static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t grid, hipStream_t st)
+{
+    if (waves == -16) {  /* CID variant (engine: the key table holds connection IDs; L = 8) */
+        if constexpr (L == 8) {
+            if (nr == 10) return launch_gcm_cid<10, DEC>(a, grid, st);
+            if (nr == 12) return launch_gcm_cid<12, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_cid<14, DEC>(a, grid, st);
+        }
+        return hipErrorInvalidValue;
+    }
+    if (waves == -8) {   /* wave-pass variant (engine: many keys, few records each) */
+        if constexpr (L == 16 || L == 64) {
+            if (nr == 10) return launch_gcm_wp<L, 10, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_wp<L, 14, DEC>(a, grid, st);
+        }
+        return hipErrorInvalidValue;
+    }
+    if (nr == 12) return launch_gcm_t<L, 12, DEC, 16>(a, grid, st);   /* AES-192: 16-wave variant only */
+    if (waves == 8)
+        return nr == 10 ? launch_gcm_t<L, 10, DEC, 8>(a, grid, st) : launch_gcm_t<L, 14, DEC, 8>(a, grid, st);
+    return nr == 10 ? launch_gcm_t<L, 10, DEC, 16>(a, grid, st) : launch_gcm_t<L, 14, DEC, 16>(a, grid, st);
+}
+
+template <bool DEC>
+hipError_t gcm_dispatch(const GcmArgs &a, int lanes, int nr, int waves, uint32_t grid, hipStream_t st)
+{
+    switch (lanes) {
+        case 4: return launch_gcm_nr<4, DEC>(a, nr, waves, grid, st);
+        case 8: return launch_gcm_nr<8, DEC>(a, nr, waves, grid, st);
+        case 16: return launch_gcm_nr<16, DEC>(a, nr, waves, grid, st);
+        case 64: return launch_gcm_nr<64, DEC>(a, nr, waves, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+/* ARIA (12/14/16 rounds) and Camellia (18/24) through the LDS-table cipher slot */
+template <bool DEC>
+hipError_t gcm_alt_dispatch(const GcmArgs &a, int nr, int cid, uint32_t grid, hipStream_t st)
+{
+    switch (nr) {
+        case 12: return launch_gcm_aria<12, DEC>(a, grid, st, cid);
+        case 14: return launch_gcm_aria<14, DEC>(a, grid, st, cid);
+        case 16: return launch_gcm_aria<16, DEC>(a, grid, st, cid);
+        case 18: return launch_gcm_aria<18, DEC>(a, grid, st, cid);
+        case 24: return launch_gcm_aria<24, DEC>(a, grid, st, cid);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+} /* namespace tlsrec */
+
+#endif /* TLSREC_GCM_H */

@@ -506,3 +506,41 @@ def ticket_parse(keys, ticket: bytes):
     r = f(_tkeys(keys), buf, len(ticket), ctypes.byref(cl))
     raw = buf.raw[:len(ticket)]
     return r, (raw[18:18 + cl.value] if r == 0 else b""), raw
+
+
+# ---- CPU-baseline leg on OpenSSL EVP (oracle/evp_bench.c) ----------------------
+EVP_LIB_PATH = os.path.join(HERE, "libevpbench.so")
+_evp = None
+
+
+def evp_lib():
+    """libevpbench.so: the record framing around OpenSSL 3 EVP AEADs (AES-NI /
+    VAES GCM, SIMD ChaCha20-Poly1305), the accelerated x86 stand-in for the
+    reference's CPU path in bench.py's cpu_baseline (AES-128/256-GCM and
+    ChaCha20-Poly1305 only)."""
+    global _evp
+    if _evp is None:
+        if not os.path.exists(EVP_LIB_PATH):
+            build()
+        L = ctypes.CDLL(EVP_LIB_PATH)
+        L.evp_bench_records.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
+                                        ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        L.evp_bench_records.restype = ctypes.c_double
+        _evp = L
+    return _evp
+
+
+EVP_CIPHERS = (AES_128_GCM, AES_256_GCM, CHACHA20_POLY1305)
+
+
+def evp_bench(cipher: int, tls_version: int, key: bytes, iv: bytes, direction: int, arena, stride: int,
+              data_len: int, n: int, seq0: int, threads: int, status) -> float:
+    """Time evp_bench_records: n records at `stride` in the numpy `arena`,
+    direction 1 = encrypt (data_len = content bytes, at offset 8 for TLS 1.2
+    GCM), 0 = decrypt (data_len = protected body).  Returns seconds."""
+    if cipher not in EVP_CIPHERS:
+        raise ValueError("evp_bench: AES-128/256-GCM and ChaCha20-Poly1305 only")
+    return evp_lib().evp_bench_records(cipher, int(tls_version == TLS1_3), bytes(key), bytes(iv), direction,
+                                       arena.ctypes.data, stride, data_len, n, seq0, threads,
+                                       status.ctypes.data)

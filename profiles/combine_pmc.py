@@ -2,8 +2,12 @@
 """Combine a run_profile.sh output directory into one summary JSON:
 per-dispatch means of every --pmc pass for the dominant kernel, plus derived
 per-record figures (instructions, HBM bytes with the gfx950 FETCH_SIZE x2
-correction, effective shader clock = GRBM_GUI_ACTIVE / 8 XCDs / duration).
-    python profiles/combine_pmc.py gpurun_out/prof_<tag> <kernel-substring> <records-per-dispatch> > profiles/<tag>_pmc_summary.json
+correction, effective shader clock = GRBM_GUI_ACTIVE / 8 XCDs / duration) and
+the busy fraction of the LDS array and the VALU:
+    lds_busy  = SQ_LDS_IDX_ACTIVE (LDS-array cycles, all CUs) / (CUs x cycles)
+    valu_issue = SQ_INSTS_VALU x 2 cycles (wave64 on SIMD32) / (4 SIMDs x CUs x cycles)
+    python profiles/combine_pmc.py gpurun_out/prof_<tag> <kernel-substring> <records-per-dispatch> \
+        [--ceiling profiles/ceiling_<config>.json] > profiles/<tag>_pmc_summary.json
 """
 import json
 import os
@@ -12,18 +16,47 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from summarize_pmc import summarize  # noqa: E402
 
-root, kern, records = sys.argv[1], sys.argv[2], int(sys.argv[3])
+CUS = 256
+args = sys.argv[1:]
+ceil_path = None
+if "--ceiling" in args:
+    k = args.index("--ceiling")
+    ceil_path = args[k + 1]
+    del args[k:k + 2]
+root, kern, records = args[0], args[1], int(args[2])
 out = {}
-for p in ("pmc_sq1", "pmc_sq2", "pmc_fetch", "pmc_write"):
-    out[p] = summarize(os.path.join(root, p), kern)
+for p in ("pmc_sq1", "pmc_sq2", "pmc_sq3", "pmc_fetch", "pmc_write"):
+    if os.path.isdir(os.path.join(root, p)):
+        out[p] = summarize(os.path.join(root, p), kern)
 sq1, sq2 = out["pmc_sq1"], out["pmc_sq2"]
 dur = sq2.get("_mean_dispatch_s") or sq1.get("_mean_dispatch_s")
-out["derived"] = {
+cycles = sq2["GRBM_GUI_ACTIVE"] / 8                      # per XCD = shader clock cycles of the dispatch
+d = {
     "records_per_dispatch": records,
     "lds_insts_per_record": sq1["SQ_INSTS_LDS"] / records,
     "valu_insts_per_record": sq1["SQ_INSTS_VALU"] / records,
-    "effective_clock_ghz": sq2["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9,
+    "effective_clock_ghz": cycles / dur / 1e9,
     "valu_active_frac_of_wave_cycles": sq2["SQ_ACTIVE_INST_VALU"] / sq1["SQ_WAVE_CYCLES"],
-    "hbm_bytes_per_record": (out["pmc_fetch"]["hbm_read_bytes_corrected"] + out["pmc_write"]["hbm_write_bytes"]) / records,
+    "valu_issue_frac": sq1["SQ_INSTS_VALU"] * 2 / (4 * CUS * cycles),
 }
+if "pmc_sq3" in out:
+    sq3 = out["pmc_sq3"]
+    c3 = sq3["GRBM_GUI_ACTIVE"] / 8
+    d["lds_busy_frac"] = sq3["SQ_LDS_IDX_ACTIVE"] / (CUS * c3)
+    d["lds_cycles_per_record"] = sq3["SQ_LDS_IDX_ACTIVE"] / records     # summed over CUs: per record
+    d["lds_bank_conflict_frac"] = sq3["SQ_LDS_BANK_CONFLICT"] / max(1.0, sq3["SQ_LDS_IDX_ACTIVE"])
+if "pmc_fetch" in out and "pmc_write" in out:
+    d["hbm_bytes_per_record"] = (out["pmc_fetch"]["hbm_read_bytes_corrected"] +
+                                 out["pmc_write"]["hbm_write_bytes"]) / records
+out["derived"] = d
 print(json.dumps(out, indent=1))
+if ceil_path:
+    units = {"lds": d.get("lds_busy_frac", 0.0), "valu": d["valu_issue_frac"]}
+    lim = max(units, key=units.get)
+    with open(ceil_path, "w") as f:
+        json.dump({"limiter": lim, "limiter_busy_frac": round(units[lim], 4),
+                   "units": {k: round(v, 4) for k, v in units.items()},
+                   "effective_clock_ghz": round(d["effective_clock_ghz"], 3),
+                   "lds_bank_conflict_frac": round(d.get("lds_bank_conflict_frac", 0.0), 5),
+                   "source": os.path.basename(os.path.normpath(root)) + " (rocprofv3 --pmc, " + kern + ")"}, f, indent=1)
+        f.write("\n")

@@ -1,0 +1,82 @@
+"""A plain C program (tests/c/abi_host.c, gcc, include/tlsrec.h only) as the
+host of libtlsrec.so -- the way Mbed TLS C code would call the engine.
+
+  - not gpu: tlsrec_record's field offsets equal a mirror of mbedtls_record
+    (ssl_misc.h:1163-1188), and the batch structs have the kernels' sizes;
+  - gpu: the reference's 4 TLS 1.3 record KATs (test_suite_ssl.data:2776-2834)
+    through tlsrec_encrypt_buf / tlsrec_decrypt_buf from C, single-record
+    round trips with latency percentiles, and concurrent C threads each with
+    its own transform (every payload checked).
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "c", "abi_host")
+
+
+def _exe():
+    if not os.path.exists(EXE) or os.path.getmtime(EXE) < os.path.getmtime(os.path.join(ROOT, "tests", "c", "abi_host.c")):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c")], check=True)
+    return EXE
+
+
+def _run(*args, timeout=120):
+    p = subprocess.run([_exe(), *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    out = json.loads(p.stdout.strip().splitlines()[-1]) if p.stdout.strip() else {}
+    return p.returncode, out, p.stderr
+
+
+def test_c_layout_matches_mbedtls_record():
+    rc, out, err = _run("layout")
+    assert rc == 0, (out, err)
+    assert out["ok"] is True
+    for field, (a, b) in out["layout"].items():
+        assert a == b, field
+
+
+def _gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.gpu
+def test_c_reference_kats():
+    if not _gpu():
+        pytest.skip("needs a GPU")
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        kats = json.load(f)
+    for k in kats:
+        rc, out, err = _run("kat", k["endpoint"], k["ctr"], k["server_key"], k["server_iv"], k["client_key"],
+                            k["client_iv"], k["plaintext"], k["ciphertext"])
+        assert rc == 0, (k["name"], out, err)
+        assert out["ciphertext_equal"] and out["plaintext_equal"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cipher,tls,content", [(2, "1.3", 16383), (2, "1.3", 1400), (3, "1.3", 1400),
+                                                (1, "1.2", 1400), (5, "1.3", 1400)])
+def test_c_single_record_latency(cipher, tls, content):
+    if not _gpu():
+        pytest.skip("needs a GPU")
+    rc, out, err = _run("latency", cipher, tls, content, 200)
+    assert rc == 0, (out, err)
+    assert out["bad"] == 0
+    lat = out["latency_us"]
+    print(json.dumps(lat))
+    assert lat["encrypt_p50"] > 0 and lat["decrypt_p50"] > 0
+
+
+@pytest.mark.gpu
+def test_c_threads_concurrent_transforms():
+    if not _gpu():
+        pytest.skip("needs a GPU")
+    rc, out, err = _run("threads", 12, 100)
+    assert rc == 0, (out, err)
+    assert out["bad"] == 0
