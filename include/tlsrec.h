@@ -256,11 +256,15 @@ int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
  * `res` host arrays and buf_off offsets into the host arenas in_arena /
  * out_arena (pinned memory, e.g. hipHostMalloc, gives the full PCIe rate).
  * The batch is cut into chunks of consecutive records of at most
- * chunk_bytes (0 = 256 MiB) of arena; each chunk's byte range is copied to
- * the device, protected there in place and copied back to the same offsets
- * of out_arena (gaps between records inside a chunk carry the input bytes),
- * with host-to-device copies, kernels and device-to-host copies overlapped on
- * three streams.  Records must be in ascending buf_off order and must not
+ * chunk_bytes (0 = 64 MiB) of arena; each chunk's byte range is copied to
+ * the device and protected there, copies and kernels overlapped on separate
+ * streams.  Output: if out_arena is pinned host memory the device can
+ * address (hipHostMalloc, hipHostRegister), the kernels write straight into
+ * it -- exactly the bytes tlsrec_batch_* writes to its out_arena, so with
+ * out_arena != in_arena the other bytes of a record are left as they were;
+ * otherwise each chunk is protected in place on the device and its whole byte
+ * range copied back to the same offsets of out_arena (gaps between records
+ * carry the input bytes).  Records must be in ascending buf_off order and must not
  * overlap (else TLSREC_ERR_SSL_BAD_INPUT_DATA).  Synchronous: returns when
  * every result is in `res`. */
 int tlsrec_host_batch_encrypt(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,

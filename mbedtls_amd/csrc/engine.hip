@@ -314,8 +314,15 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
          * the stream path. */
         const uint32_t nl = kt->nloaded;     /* read once: the engine's pages change under it */
         const uint32_t rpk = nl > 1 ? n / nl : n;
+        /* ... and the batch should fill the chip: with fewer than 8 records
+         * per wave of a full grid (cu x 16 waves), more lanes per record
+         * (measured at 16 K x 16 KiB records: L = 8 363, L = 16 611, L = 64
+         * 536 GiB/s) */
+        const uint64_t rpwave = (uint64_t) n / ((uint64_t) cu * GCM_WAVES);
+        const int Lfill = rpwave >= 8 ? 8 : (rpwave >= 2 ? 16 : 64);
         int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
                 : (nl <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
+        if (!(lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) && Lfill > L) L = Lfill;
         if (kt->has_cid) L = 8;     /* the CID variant: one configuration */
         GcmArgs a;
         a.slots = kt->d_slots;
@@ -390,7 +397,11 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (tlsrec__launch_ccm(&a, dec, ccm_nr, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (!rc && (cmask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
-        int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes : 2;
+        /* 2 lanes per record, more when the batch would not fill the chip
+         * (cu x 8 resident waves: 2 per SIMD) */
+        const uint64_t rpwave = (uint64_t) n / ((uint64_t) cu * 8);
+        int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes
+                : (rpwave >= 32 ? 2 : (rpwave >= 16 ? 4 : 8));
         if (kt->has_cid) L = 2;     /* the CID variant: one configuration */
         CpArgs a;
         a.slots = kt->d_slots;
@@ -515,7 +526,7 @@ static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_ba
 {
     if (!kt || (n && (!recs || !res || !in || !out))) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (n == 0) return 0;
-    if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+    if (chunk_bytes == 0) chunk_bytes = 64ull << 20;   /* measured best of 16 / 64 / 256 / 1024 MiB */
     /* records in ascending, non-overlapping order; chunks of whole records */
     struct Chunk { uint32_t first, count; uint64_t base, span; };
     Chunk *ch = (Chunk *) malloc(sizeof(Chunk) * n);
@@ -535,6 +546,20 @@ static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_ba
             ch[nch++] = Chunk{ i, 1, lo, hi - lo };
         }
         if (ch[nch - 1].span > maxspan) maxspan = ch[nch - 1].span;
+    }
+    /* Output arena in pinned host memory the device can address: the kernels
+     * write their output straight into it over PCIe (measured 48-49 GiB/s
+     * for c2-shaped records, the link rate) while the next chunk's H2D copy
+     * runs on the copy engine -- a D2H copy instead shares that engine with
+     * the H2D copies and the two directions serialise.  Pageable output:
+     * protect in place in the device slot and copy the chunk back. */
+    uint8_t *zc = NULL;
+    {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+            zc = (uint8_t *) at.devicePointer;
+        else
+            (void) hipGetLastError();    /* pageable memory: clear the sticky error */
     }
     pthread_mutex_lock(&kt->pipe_mu);
     int rc = host_pipe_reserve(kt, (maxspan + 255) / 256 * 256, n);
@@ -556,11 +581,16 @@ static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_ba
         /* the descriptors' buf_off are offsets into the host arena: shift the
          * device arena base so that base + buf_off lands in the slot */
         uint8_t *dev = (uint8_t *) ((uintptr_t) p->slot[k] - (uintptr_t) C.base);
-        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, dev, lanes, p->cmp, dec);
+        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, zc ? zc : dev, lanes, p->cmp, dec);
         if (rc) break;
         e = hipEventRecord(p->ev_cmp[k], p->cmp);
-        if (e == hipSuccess) e = hipStreamWaitEvent(p->d2h, p->ev_cmp[k], 0);
-        if (e == hipSuccess) e = hipMemcpyAsync(out + C.base, p->slot[k], C.span, hipMemcpyDeviceToHost, p->d2h);
+        if (zc) {
+            /* the slot is free once its kernel is done */
+            if (e == hipSuccess) e = hipStreamWaitEvent(p->d2h, p->ev_cmp[k], 0);
+        } else {
+            if (e == hipSuccess) e = hipStreamWaitEvent(p->d2h, p->ev_cmp[k], 0);
+            if (e == hipSuccess) e = hipMemcpyAsync(out + C.base, p->slot[k], C.span, hipMemcpyDeviceToHost, p->d2h);
+        }
         if (e == hipSuccess) e = hipEventRecord(p->ev_d2h[k], p->d2h);
         if (e != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
