@@ -52,6 +52,8 @@ CONFIGS = {
                 "ARIA-256-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
     "camellia128": ("CAMELLIA-128-GCM", "TLS1.2", "decrypt", 16384, 1 << 20, 1,
                     "Camellia-128-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
+    "chacha16k": ("CHACHA20-POLY1305", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
+                  "ChaCha20-Poly1305 decrypt, 1M x 16 KiB TLS 1.3 records, single key (the c4 ChaCha share)"),
     "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
             "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 1.4 KiB TLS 1.3 decrypt"),
 }

@@ -453,11 +453,12 @@ struct CpRec {
     uint32_t key[8];
     uint32_t nonce[3];
     uint32_t pad0;
-    uint32_t s[4];           /* Poly1305 s */
-    uint32_t r1[5], r2[5], r3[5], rl[5];   /* r, r^2, r^3, r^(4L) (26-bit limbs) */
-    uint32_t aadf[5];        /* DTLS 1.2 + CID: the 2..4 AAD blocks Horner-folded */
+    uint32_t s[4];                          /* Poly1305 s */
+    uint32_t r1[5];                         /* r (26-bit limbs) */
+    uint32_t rl[4][5];                      /* r^L, r^2L, r^3L, r^4L */
 };
 static_assert(sizeof(CpRec) == 164, "CpRec layout");
+static_assert(sizeof(tlsrec_batch_rec) == 40 && sizeof(tlsrec_key_material) == 64, "descriptor words");
 
 __device__ __forceinline__ P5 p_lds(const uint32_t *v)
 {
@@ -485,7 +486,7 @@ __device__ __forceinline__ void p_mac(D5 &d, const P5 &h, const P5 &r)
               (uint64_t) h.v[3] * r.v[1] + (uint64_t) h.v[4] * r.v[0];
 }
 
-/* carry-propagate a D5 of up to four limb products plus a block (< 2^59 per
+/* carry-propagate a D5 of up to four limb products plus a block (< 2^61 per
  * limb) into limbs < 2^26, limb 1 < 2^26 + 2^10 -- the form p_mul returns */
 __device__ __forceinline__ P5 p_reduce(D5 d)
 {
@@ -512,12 +513,42 @@ __device__ __forceinline__ void chacha_block_kn(const uint32_t *kn, uint32_t cou
     chacha_block(key, counter, nw, out);
 }
 
+/* Keystream exchange slot of (chunk lane c, 16-B group g) in a wave's 4 KiB
+ * LDS row: the group rotates with c >> 1 so that the eight lanes of a
+ * ds_write_b128 lane group hit 32 distinct banks. */
+__device__ __forceinline__ uint32_t ks_slot(uint32_t c, uint32_t g)
+{
+    return 4u * c + ((g + (c >> 1)) & 3u);
+}
+
+/*
+ * ChaCha20-Poly1305 record kernel (RFC 8439 2.8 around the framing plan).
+ *
+ * Slot layout.  L lanes serve one record; a step covers L ChaCha20 blocks =
+ * 4L 16-byte slots of the record, and in load / store t (0..3) lane q touches
+ * slot L*t + q -- the record's L lanes move L*16 contiguous bytes per
+ * instruction, whole 128-B lines at L = 8 and 32-B runs at L = 2, instead of
+ * each lane walking its own 64-byte block (which held the kernel to ~4 TB/s of
+ * HBM).  Lane q still computes ChaCha20 block L*j - z + q of the record (z =
+ * front padding in blocks, so that every record ends in its last step); the
+ * 64-byte keystream goes through the wave's LDS row (4 x ds_write_b128,
+ * 4 x ds_read_b128) to the lanes that hold its slots.
+ *
+ * Poly1305.  Lane q owns the slots = q (mod L), in order, as a Horner chain
+ * with multiplier r^L: per step acc*r^(4L) + X_0 r^(3L) + X_1 r^(2L) + X_2 r^L
+ * + X_3, front-padding slots X = 0, slots past the record's last block
+ * skipped.  A lane's chain then ends at one of the record's last L blocks, d
+ * blocks before the end, and the record's sum is  sum_q acc_q r^(d_q)  (a
+ * shuffle-add over the L lanes), then the length block and s.
+ */
 template <int L, bool DEC, bool CID = false>
-__global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void tlsrec_chachapoly_kernel(CpArgs a)
+__global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
 {
     constexpr int R = 64 / L;
     constexpr int LOGL = Log2<L>::v;
     __shared__ CpRec crec[CP_WAVES][64];
+    __shared__ uint4 kst[CP_WAVES][256];                  /* keystream exchange, 4 KiB per wave */
+    __shared__ uint32_t cidf[CP_WAVES][CID ? 64 : 1][5];   /* CID: AAD blocks Horner-folded */
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane / L, q = lane % L;
     const uint32_t lo = a.perm ? *a.lo : 0u;
@@ -528,6 +559,9 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
      * Poly1305 key (ChaCha20 block 0, RFC 8439 2.6) and powers of r ---- */
     bool mine = false;
     uint32_t my_rec = 0;
+    /* the chunk position's descriptor and key material, kept for the record
+     * rounds (shuffled to the record's lanes: no second trip to memory) */
+    uint32_t dm[10] = { 0 }, kmm[8] = { 0 };
     {
         const uint64_t pos = chunk + (uint64_t) lane;
         CpRec &cr = crec[wave][lane];
@@ -540,6 +574,8 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
             if (d.slot < a.capacity && a.slots[d.slot].km.cipher == TLSREC_CIPHER_CHACHA20_POLY1305) {
                 mine = true;
                 const tlsrec_key_material km = a.slots[d.slot].km;
+                __builtin_memcpy(dm, &d, sizeof(dm));
+                __builtin_memcpy(kmm, &km, sizeof(kmm));    /* all but the key: the plan's inputs */
                 tlsrec_plan p;
                 make_plan<DEC, CID>(p, d, km, &a.slots[d.slot], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
@@ -552,18 +588,31 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         for (int i = 0; i < 3; i++) cr.nonce[i] = nw[i];
         for (int i = 0; i < 4; i++) cr.s[i] = blk[4 + i];
         const P5 r1 = p_from_r(blk[0], blk[1], blk[2], blk[3]);
-        const P5 r2 = p_mul(r1, r1);
-        const P5 r3 = p_mul(r2, r1);
-        P5 rl = p_mul(r2, r2);                                  /* r^4 */
-        for (int i = 0; i < LOGL; i++) rl = p_mul(rl, rl);      /* r^(4L) */
+        P5 rL = r1;
+        for (int i = 0; i < LOGL; i++) rL = p_mul(rL, rL);     /* r^L */
+        const P5 r2L = p_mul(rL, rL);
+        const P5 r3L = p_mul(r2L, rL);
+        const P5 r4L = p_mul(r2L, r2L);
         for (int i = 0; i < 5; i++) {
             cr.r1[i] = r1.v[i];
-            cr.r2[i] = r2.v[i];
-            cr.r3[i] = r3.v[i];
-            cr.rl[i] = rl.v[i];
+            cr.rl[0][i] = rL.v[i];
+            cr.rl[1][i] = r2L.v[i];
+            cr.rl[2][i] = r3L.v[i];
+            cr.rl[3][i] = r4L.v[i];
         }
     }
     /* lanes read other lanes' CpRec: the wave's own LDS writes land first */
+
+    /* this lane's keystream exchange slots: writes (own block, group t) and
+     * reads (slot L*t + q of its record) */
+    uint4 *const krow = kst[wave];
+    uint32_t kw[4], kr[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        kw[t] = ks_slot((uint32_t) lane, (uint32_t) t);
+        const uint32_t u = (uint32_t) (L * t + q);
+        kr[t] = ks_slot((uint32_t) (lane - q) + u / 4, u % 4);
+    }
 
     for (uint32_t rr = 0; rr < a.rpw; rr += R) {
         const uint32_t slot_in_chunk = rr + (uint32_t) g;
@@ -571,204 +620,186 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         const bool active = slot_in_chunk < a.rpw && owner_mine;
         const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
         const CpRec &cr = crec[wave][slot_in_chunk & 63];
+        const uint32_t *aadf = cidf[wave][CID ? (slot_in_chunk & 63) : 0];
         tlsrec_batch_rec d;
         tlsrec_plan p;
         bool run = false;
-        if (active) {
-            d = a.recs[ridx];
-            const tlsrec_key_material km = a.slots[d.slot].km;
-            make_plan<DEC, CID>(p, d, km, &a.slots[d.slot], a.in);
-            if (p.status != 0) {
-                if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
-            } else {
-                run = true;
+        {
+            uint32_t w[10], k[16] = { 0 };
+#pragma unroll
+            for (int i = 0; i < 10; i++) w[i] = (uint32_t) __shfl((int) dm[i], (int) slot_in_chunk & 63);
+#pragma unroll
+            for (int i = 0; i < 8; i++) k[i] = (uint32_t) __shfl((int) kmm[i], (int) slot_in_chunk & 63);
+            __builtin_memcpy(&d, w, sizeof(w));
+            if (active) {
+                tlsrec_key_material km;
+                __builtin_memcpy(&km, k, sizeof(km));
+                make_plan<DEC, CID>(p, d, km, &a.slots[d.slot], a.in);
+                if (p.status != 0) {
+                    if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
+                } else {
+                    run = true;
+                }
             }
         }
         const uint32_t aead_len = run ? p.aead_len : 0;
-        const uint32_t B = (aead_len + 63) >> 6;              /* ChaCha20 chunks */
-        const uint32_t M = (aead_len + 15) >> 4;              /* Poly1305 C blocks */
-        const uint32_t v = B ? M - 4 * (B - 1) : 0;
-        const uint32_t z = (L - B % L) % L;
+        const uint32_t B = (aead_len + 63) >> 6;              /* ChaCha20 blocks (64 B) */
+        const uint32_t M = (aead_len + 15) >> 4;              /* Poly1305 C blocks (16 B) */
+        const uint32_t z = (L - B % L) % L;                   /* front padding, in 64-B blocks */
         const uint32_t J = run ? (B + z) / L : 0;
         const uint32_t Jmax = wave_max(J);
         uint4 aadw = make_uint4(0, 0, 0, 0);
-        bool cidaad = false;  /* AAD of 2..4 blocks, folded into cr.aadf */
+        bool cidaad = false;  /* AAD of 2..4 blocks, folded into aadf */
         const uint8_t *src = a.in;
         uint8_t *dst = a.out;
-        bool aligned = false;
         uint32_t content_len = 0;
         if (run) {
             aadw = aad_words(p);
             cidaad = CID && p.aad_len > 16;
             if (cidaad && q == 0) {   /* DTLS 1.2 + CID: one lane folds, all read */
                 const P5 f = cp_cid_aad_fold(p_from_words(aadw), cr.r1, p, d, a.slots[d.slot].cid);
-                uint32_t *w = const_cast<uint32_t *>(cr.aadf);
+                uint32_t *w = const_cast<uint32_t *>(aadf);
 #pragma unroll
                 for (int i = 0; i < 5; i++) w[i] = f.v[i];
             }
             src = a.in + d.buf_off + p.aead_pos;
             dst = a.out + d.buf_off + p.aead_pos;
-            aligned = true;   /* any byte offset: see GcmJob::setup */
             content_len = DEC ? aead_len : p.content_len;
         }
         const uint8_t inner_type = run ? p.inner_type : 0;
         const bool tls13 = run && p.inner;   /* TLS 1.3 or DTLS 1.2 + CID inner plaintext */
         /* a readable 16-byte address for lanes with nothing to load */
         const uint8_t *safe = run ? src : reinterpret_cast<const uint8_t *>(a.recs);
+        /* slot (L*t + q) of step j is record block 4(L j - z) + L t + q */
+        const int32_t base0 = (int32_t) q - 4 * (int32_t) z;
 
-        P5 acc = p_zero(), vf = p_zero();
+        P5 acc = p_zero();
         uint32_t nzpos = 0;                 /* TLS 1.3: 1 + position of the last non-zero 16-B block */
+        /* decrypt: the received tag (after the AEAD data in the record
+         * buffer), loaded now and compared after the loop */
+        const uint4 want = (DEC && run) ? gload16(src + aead_len) : make_uint4(0, 0, 0, 0);
 
-        /* general step: any chunk (front padding, AAD fold at chunk 0, the
-         * final chunk with v <= 4 Poly1305 blocks, partial or unaligned data) */
+        /* this lane's keystream block of step j, exchanged: K[t] = the
+         * keystream of slot L*t + q */
+        auto keystream = [&](uint32_t j, uint4 (&K)[4]) {
+            uint32_t ks[16];
+            chacha_block_kn(cr.key, L * j - z + (uint32_t) q + 1u, ks);
+            asm volatile("" ::: "memory");   /* after the previous step's reads */
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                krow[kw[t]] = make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]);
+            /* other lanes' writes: same wave, in-order LDS queue */
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int t = 0; t < 4; t++) K[t] = krow[kr[t]];
+        };
+
+        /* general step: any step (front padding, the AAD fold at block 0,
+         * partial or ragged blocks, the record's end) */
         auto general = [&](uint32_t j) {
-            const int32_t b = (int32_t) (L * j + q) - (int32_t) z;
             const bool live = run && j < J;
-            const bool valid = live && b >= 0 && (uint32_t) b < B;
-            /* all four loads first (full aligned blocks directly, the rest from
-             * a safe address and redone below), a ChaCha block ahead of use */
             uint4 ct[4];
             bool fast[4];
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                const uint32_t pos = (uint32_t) b * 64 + 16 * t;
-                fast[t] = valid && aligned && pos + 16 <= content_len;
+                const int32_t i = (int32_t) (4 * L * j) + base0 + L * t;
+                const uint32_t pos = (uint32_t) i * 16;
+                fast[t] = live && i >= 0 && pos + 16 <= content_len;
                 ct[t] = gload16(fast[t] ? src + pos : safe);
             }
-            asm volatile("" ::: "memory");
-            uint32_t ks[16];
-            chacha_block_kn(cr.key, (uint32_t) b + 1u, ks);
+            uint4 K[4];
+            keystream(j, K);
+            const P5 r1 = p_lds(cr.r1), rL = p_lds(cr.rl[0]);
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                const uint32_t pos = (uint32_t) b * 64 + 16 * t;
-                const uint4 k = make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]);
+                const int32_t i = (int32_t) (4 * L * j) + base0 + L * t;
+                const uint32_t pos = (uint32_t) i * 16;
+                const bool valid = live && i >= 0 && (uint32_t) i < M;
+                P5 x = p_zero();
                 if (fast[t]) {
-                    const uint4 o = xor4(ct[t], k);
+                    const uint4 o = xor4(ct[t], K[t]);
                     gstore16(dst + pos, o);
-                    if (!DEC) ct[t] = o;
                     if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
-                } else if (valid && pos < aead_len) {
-                    const uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, aligned);
-                    const uint4 o = mask_block(xor4(blk, k), pos, aead_len);
-                    store_block(dst, pos, aead_len, o, aligned);
-                    ct[t] = DEC ? blk : o;
+                    x = p_from_words(DEC ? ct[t] : o);
+                } else if (valid) {
+                    const uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, true);
+                    const uint4 o = mask_block(xor4(blk, K[t]), pos, aead_len);
+                    store_block(dst, pos, aead_len, o, true);
                     if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
-                } else {
-                    ct[t] = make_uint4(0, 0, 0, 0);
+                    x = p_from_words(DEC ? blk : o);
                 }
+                /* the AAD block(s) enter as A*r folded into C_0 */
+                if (valid && i == 0) x = p_add(x, p_mul(cidaad ? p_lds(aadf) : p_from_words(aadw), r1));
+                /* Horner link of this lane's chain: slots past the record's
+                 * last block leave it where it ended */
+                const P5 y = p_add(p_mul(acc, rL), x);
+                if (live && i < (int32_t) M) acc = y;
             }
-            /* Horner over this chunk's Poly1305 blocks (AAD folded before C_0) */
-            const P5 r1 = p_lds(cr.r1);
-            const uint32_t vv = (valid && (uint32_t) b == B - 1) ? v : 4;
-            P5 x = p_from_words(ct[0]);
-            if (b == 0) x = p_add(x, p_mul(cidaad ? p_lds(cr.aadf) : p_from_words(aadw), r1));
-#pragma unroll
-            for (int t = 1; t < 4; t++) {
-                P5 y = p_add(p_mul(x, r1), p_from_words(ct[t]));
-                x = p_sel((uint32_t) t < vv, y, x);
-            }
-            const bool is_final = valid && (uint32_t) b == B - 1;
-            if (is_final) vf = x;
-            P5 an = (j == 0) ? p_zero() : p_mul(acc, p_lds(cr.rl));
-            an = p_add(an, (valid && !is_final) ? x : p_zero());
-            if (live && !is_final) acc = an;
         };
 
-        /* Body chunks [1, jh): every lane of the wave holds a full, aligned,
-         * non-final chunk inside its record's content (wave-uniform bound):
-         * no masks, and Poly1305 as acc*r^(4L) + c0 r^3 + c1 r^2 + c2 r + c3
-         * with one carry propagation per chunk. */
+        /* Body steps [1, jh): every slot of every lane of the wave is a full
+         * 16-byte block inside its record's content (wave-uniform bound): no
+         * masks, Poly1305 as acc*r^(4L) + X_0 r^(3L) + X_1 r^(2L) + X_2 r^L + X_3
+         * with one carry propagation per step. */
         uint32_t jh = 0;
         {
-            const uint32_t bmax = (run && aligned && B > 0) ? min(B - 1, content_len / 64) : 0;
-            const uint32_t h = wave_min(run ? (bmax + z) / L : 0);
+            const uint32_t cfull = run ? content_len / 64 : 0;      /* full 64-B blocks of content */
+            const uint32_t h = wave_min(run ? (cfull + z) / L : 0);
             jh = h > 1 ? h : 0;
         }
         const uint32_t jl = jh ? 1u : Jmax;
         uint32_t j = 0;
         for (; j < jl; j++) general(j);
-        /* one body chunk: load (a ChaCha20 block ahead of use), XOR, store,
-         * Horner step acc*r^(4L) + c0 r^3 + c1 r^2 + c2 r + c3 */
-        auto absorb = [&](uint4 (&c)[4], const uint32_t (&ks)[16], uint32_t b) {
-            uint8_t *dp = dst + (size_t) b * 64;
+        for (; j < jh; j++) {
+            const uint32_t pos0 = (uint32_t) ((int32_t) (4 * L * j) + base0) * 16;
+            uint4 c[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) c[t] = gload16(src + pos0 + 16 * L * t);
+            uint4 K[4];
+            keystream(j, K);
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                const uint4 o = xor4(c[t], make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]));
-                gstore16(dp + 16 * t, o);
-                if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = b * 64 + 16 * t + 1;
+                const uint32_t pos = pos0 + 16 * L * t;
+                const uint4 o = xor4(c[t], K[t]);
+                gstore16(dst + pos, o);
+                if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                 if (!DEC) c[t] = o;
             }
             D5 dd;
-            const P5 c3 = p_from_words(c[3]);
+            const P5 x3 = p_from_words(c[3]);
 #pragma unroll
-            for (int i = 0; i < 5; i++) dd.v[i] = c3.v[i];
-            p_mac(dd, acc, p_lds(cr.rl));
-            p_mac(dd, p_from_words(c[0]), p_lds(cr.r3));
-            p_mac(dd, p_from_words(c[1]), p_lds(cr.r2));
-            p_mac(dd, p_from_words(c[2]), p_lds(cr.r1));
+            for (int i = 0; i < 5; i++) dd.v[i] = x3.v[i];
+            p_mac(dd, acc, p_lds(cr.rl[3]));
+            p_mac(dd, p_from_words(c[0]), p_lds(cr.rl[2]));
+            p_mac(dd, p_from_words(c[1]), p_lds(cr.rl[1]));
+            p_mac(dd, p_from_words(c[2]), p_lds(cr.rl[0]));
             acc = p_reduce(dd);
-        };
-        /* two chunks per lane per step: two key-stream blocks in lockstep */
-        for (; j + 1 < jh; j += 2) {
-            const uint32_t b0 = L * j + q - z, b1 = b0 + L;
-            uint4 c0[4], c1[4];
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                c0[t] = gload16(src + (size_t) b0 * 64 + 16 * t);
-                c1[t] = gload16(src + (size_t) b1 * 64 + 16 * t);
-            }
-            asm volatile("" ::: "memory");
-            uint32_t ks0[16], ks1[16];
-            {
-                uint32_t key[8], nw[3];
-#pragma unroll
-                for (int i = 0; i < 8; i++) key[i] = cr.key[i];
-#pragma unroll
-                for (int i = 0; i < 3; i++) nw[i] = cr.nonce[i];
-                chacha_block2(key, b0 + 1u, b1 + 1u, nw, ks0, ks1);
-            }
-            absorb(c0, ks0, b0);
-            absorb(c1, ks1, b1);
-        }
-        for (; j < jh; j++) {
-            const uint32_t b = L * j + q - z;
-            const uint8_t *sp = src + (size_t) b * 64;
-            uint4 c[4];
-#pragma unroll
-            for (int t = 0; t < 4; t++) c[t] = gload16(sp + 16 * t);
-            /* keep the loads here, a ChaCha20 block ahead of their use: left
-             * alone, the scheduler sinks each to just before its XOR and the
-             * step pays four serial memory latencies */
-            asm volatile("" ::: "memory");
-            uint32_t ks[16];
-            chacha_block_kn(cr.key, b + 1u, ks);
-            absorb(c, ks, b);
         }
         for (; j < Jmax; j++) general(j);
 
-        if (run && B == 0 && q == L - 1) vf = cidaad ? p_lds(cr.aadf) : p_from_words(aadw);
-        /* rotated tree: logical ql = (q+1) % L, anchored at chunk B-2;
-         * level i combines with r^(4 * 2^i) */
-        const P5 r1 = p_lds(cr.r1), r2 = p_lds(cr.r2);
-        const P5 r4 = p_mul(r2, r2);
-        P5 rpow[LOGL + 1];
-        rpow[0] = r4;
+        /* sum_q acc_q r^(d_q), d_q = blocks from the end of lane q's chain to
+         * the record's last block (K = slot of that block) */
+        const P5 r1 = p_lds(cr.r1);
+        {
+            const uint32_t K = 4 * z + M - 1;                     /* M >= 1 where it matters */
+            const uint32_t dq = (K - (uint32_t) q) % L;
+            P5 rp = r1;
 #pragma unroll
-        for (int i = 1; i <= LOGL; i++) rpow[i] = p_mul(rpow[i - 1], rpow[i - 1]);
-        const int ql = (q + 1) % L;
+            for (int i = 0; i < LOGL; i++) {
+                acc = p_sel((dq >> i) & 1, p_mul(acc, rp), acc);
+                if (i + 1 < LOGL) rp = p_mul(rp, rp);
+            }
 #pragma unroll
-        for (int i = LOGL - 1; i >= 0; i--) {
-            const int sh = 1 << i;
-            const int src_lane = (lane - q) + ((ql + sh + L - 1) % L);
-            P5 o = shfl_p5<L>(acc, src_lane);
-            P5 t = p_add(p_mul(acc, rpow[i]), o);
-            acc = p_carry(t);
+            for (int o = 1; o < L; o <<= 1) {
+                P5 w;
+#pragma unroll
+                for (int i = 0; i < 5; i++) w.v[i] = __shfl_xor(acc.v[i], o);
+                acc = p_add(acc, w);
+            }
         }
-        /* in lane L-1: poly = r * (r * (vf + r^(4-delta) * W) + LEN) */
-        const uint32_t delta = 4 - v;
-        P5 rd = delta == 0 ? r4 : (delta == 1 ? p_lds(cr.r3) : (delta == 2 ? r2 : r1));
-        P5 X = p_add(p_mul(acc, rd), vf);
-        X = p_mul(p_carry(X), r1);
+        /* H1 = A r^M + sum_i C_i r^(M-1-i); tag = (H1 r + LEN) r + s */
+        P5 X = M ? p_carry(acc) : (cidaad ? p_lds(aadf) : p_from_words(aadw));
+        X = p_mul(X, r1);
         const uint32_t alen = run ? p.aad_len : 0;
         X = p_add(X, p_from_words(make_uint4(alen, 0, aead_len, 0)));
         X = p_mul(p_carry(X), r1);
@@ -789,7 +820,6 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
                 a.res[ridx] = r;
             }
         } else {
-            uint4 want = load_block(src, aead_len, aead_len + 16, aead_len + 16, 0, false);
             uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
             diff = __shfl(diff, leader);
             uint32_t nzkey = 0;

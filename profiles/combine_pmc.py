@@ -5,7 +5,11 @@ per-record figures (instructions, HBM bytes with the gfx950 FETCH_SIZE x2
 correction, effective shader clock = GRBM_GUI_ACTIVE / 8 XCDs / duration) and
 the busy fraction of the LDS array and the VALU:
     lds_busy  = SQ_LDS_IDX_ACTIVE (LDS-array cycles, all CUs) / (CUs x cycles)
-    valu_issue = SQ_INSTS_VALU x 2 cycles (wave64 on SIMD32) / (4 SIMDs x CUs x cycles)
+    valu_busy = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (4 SIMDs x CUs x cycles)
+(a wave64 integer VALU instruction holds its SIMD for 4 cycles: tools/chacha_probe.hip
+measures the ChaCha20 block, ~990 such instructions, at the same chip-wide rate
+with 1, 2, 3 or 4 waves per SIMD -- 2.0-2.3 TB/s of keystream -- i.e. the VALU,
+not latency, is saturated; SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU quad-cycles)
     python profiles/combine_pmc.py gpurun_out/prof_<tag> <kernel-substring> <records-per-dispatch> \
         [--ceiling profiles/ceiling_<config>.json] > profiles/<tag>_pmc_summary.json
 """
@@ -37,7 +41,7 @@ d = {
     "valu_insts_per_record": sq1["SQ_INSTS_VALU"] / records,
     "effective_clock_ghz": cycles / dur / 1e9,
     "valu_active_frac_of_wave_cycles": sq2["SQ_ACTIVE_INST_VALU"] / sq1["SQ_WAVE_CYCLES"],
-    "valu_issue_frac": sq1["SQ_INSTS_VALU"] * 2 / (4 * CUS * cycles),
+    "valu_busy_frac": sq2["SQ_ACTIVE_INST_VALU"] * 4 / (4 * CUS * cycles),
 }
 if "pmc_sq3" in out:
     sq3 = out["pmc_sq3"]
@@ -51,7 +55,7 @@ if "pmc_fetch" in out and "pmc_write" in out:
 out["derived"] = d
 print(json.dumps(out, indent=1))
 if ceil_path:
-    units = {"lds": d.get("lds_busy_frac", 0.0), "valu": d["valu_issue_frac"]}
+    units = {"lds": d.get("lds_busy_frac", 0.0), "valu": d["valu_busy_frac"]}
     lim = max(units, key=units.get)
     with open(ceil_path, "w") as f:
         json.dump({"limiter": lim, "limiter_busy_frac": round(units[lim], 4),
