@@ -52,6 +52,8 @@ CONFIGS = {
                 "ARIA-256-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
     "camellia128": ("CAMELLIA-128-GCM", "TLS1.2", "decrypt", 16384, 1 << 20, 1,
                     "Camellia-128-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
+    "k4": ("AES-256-GCM", "TLS1.3", "decrypt", 16383, 1 << 18, 1 << 16,
+           "64K keys x 4 records, AES-256-GCM, records round-robin over keys, 16 KiB TLS 1.3 decrypt (few records per key)"),
     "chacha16k": ("CHACHA20-POLY1305", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
                   "ChaCha20-Poly1305 decrypt, 1M x 16 KiB TLS 1.3 records, single key (the c4 ChaCha share)"),
     "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
@@ -71,6 +73,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
                     help="c2 (default) = the metric's workload; c1/c3/c4/c4s = the other BASELINE configs")
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--keys", type=int, default=0, help="override the config's key count (records round-robin over keys)")
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--align", type=int, default=128, help="record slot alignment in the arena (bytes; 128 = HBM/L2 line)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of the CPU sample")
@@ -108,12 +111,17 @@ def main():
 
     cname, tls, direction, content, n_default, nkeys, workload = CONFIGS[args.config]
     n = args.records or n_default
+    nkeys = args.keys or nkeys
     ver = M.VERSION_TLS1_3 if tls == "TLS1.3" else M.VERSION_TLS1_2
     inner = inner_len(content, tls)
     head = 8 if tls == "TLS1.2" and cname != "CHACHA20-POLY1305" else 0   # TLS 1.2 GCM explicit nonce
     taglen = 8 if cname.endswith("CCM-8") else 16
     wire = head + inner + taglen
-    stride = (wire + args.align - 1) // args.align * args.align
+    # TLS 1.2 GCM/CCM records carry an 8-byte explicit IV ahead of the
+    # ciphertext: the record buffer starts `lead` bytes into its slot so that
+    # the AEAD region, which the kernels stream, is line-aligned
+    lead = (args.align - head % args.align) % args.align if head else 0
+    stride = (lead + wire + args.align - 1) // args.align * args.align
     ciphers = {"AES-128-GCM": [M.CIPHER_AES_128_GCM], "AES-256-GCM": [M.CIPHER_AES_256_GCM],
                "AES-128-CCM": [M.CIPHER_AES_128_CCM], "AES-128-CCM-8": [M.CIPHER_AES_128_CCM_8],
                "AES-192-GCM": [M.CIPHER_AES_192_GCM], "CHACHA20-POLY1305": [M.CIPHER_CHACHA20_POLY1305],
@@ -144,8 +152,8 @@ def main():
     shard0 = sh.start
     arena = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev)
     recs = M.records(n)
-    recs["buf_off"] = np.arange(n, dtype=np.uint64) * stride
-    recs["buf_len"] = stride
+    recs["buf_off"] = np.arange(n, dtype=np.uint64) * stride + lead
+    recs["buf_len"] = stride - lead
     recs["data_offset"] = head
     recs["data_len"] = content
     # records round-robin over keys: neighbours never share a
@@ -158,7 +166,8 @@ def main():
     recs_dev = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
     res_dev = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     sample = list(range(0, n, max(1, n // max(1, args.verify))))[:args.verify]
-    pt_sample = {i: arena[i * stride + head:i * stride + head + content].cpu().numpy().copy() for i in sample}
+    pt_sample = {i: arena[i * stride + lead + head:i * stride + lead + head + content].cpu().numpy().copy()
+                 for i in sample}
 
     if direction == "decrypt":
         # produce the ciphertexts with the (separately verified) encrypt kernel
@@ -209,7 +218,7 @@ def main():
     if direction == "decrypt":
         bad += int((lens != content).sum())
         for i in sample:
-            got = out_arena[i * stride + head:i * stride + head + content].cpu().numpy()
+            got = out_arena[i * stride + lead + head:i * stride + lead + head + content].cpu().numpy()
             bad += int(not np.array_equal(got, pt_sample[i]))
     bad_t = torch.tensor([bad], dtype=torch.int64, device=dev)
     if world > 1:
@@ -230,12 +239,12 @@ def main():
             klen = M.KEYLEN[int(k["cipher"])]
             ot = O.Transform(O.TLS1_3 if ver == M.VERSION_TLS1_3 else O.TLS1_2, oc[int(k["cipher"])],
                              bytes(k["key"][:klen]), bytes(k["key"][:klen]), bytes(k["iv"]), bytes(k["iv"]))
-            buf = bytearray(stride)
+            buf = bytearray(stride - lead)
             buf[head:head + content] = pt_sample[i].tobytes()
             orec = O.Record(ctr=bytes(recs["ctr"][i]), type=23, ver=b"\x03\x03", buf=buf,
                             data_offset=head, data_len=content)
             assert ot.encrypt_buf(orec) == 0
-            got = src[i * stride:i * stride + wire].cpu().numpy().tobytes()
+            got = src[i * stride + lead:i * stride + lead + wire].cpu().numpy().tobytes()
             oracle_ok &= got == orec.data()
 
     # ---- roofline of the dominant kernel --------------------------------------
@@ -288,7 +297,7 @@ def main():
     # reported beside the device-resident value, never as it
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = end_to_end(M, kt, recs, arena, out_arena, n, stride, head, content, wire, inner, direction,
+        e2e = end_to_end(M, kt, recs, arena, out_arena, n, stride, lead, head, content, wire, inner, direction,
                          args.e2e_records)
 
     out = {
@@ -306,7 +315,8 @@ def main():
         "data": "synthetic (splitmix64 keys/nonces, uniform random payload; decrypt inputs made by the verified encrypt kernel)",
         "config": {"workload": workload, "config": args.config, "records_per_gpu": n,
                    "record_inner_bytes": inner, "record_wire_bytes": wire, "keys": nkeys,
-                   "lanes_per_record": args.lanes or "auto", "slot_align": args.align, "parallelism": f"shard{world}"},
+                   "lanes_per_record": args.lanes or "auto", "slot_align": args.align, "aead_region_offset": lead + head,
+                   "parallelism": f"shard{world}"},
         "records_per_s": round(n * world / steps_s, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -323,7 +333,7 @@ def main():
         dist.destroy_process_group()
 
 
-def end_to_end(M, kt, recs, arena, out_arena, n, stride, head, content, wire, inner, direction, e2e_records):
+def end_to_end(M, kt, recs, arena, out_arena, n, stride, lead, head, content, wire, inner, direction, e2e_records):
     """tlsrec_host_batch_* over pinned host buffers: chunked H2D -> kernels ->
     D2H on three streams (engine.hip).  Input = the first E records of the
     bench batch (ciphertexts for decrypt), output into a second pinned buffer;
@@ -349,7 +359,7 @@ def end_to_end(M, kt, recs, arena, out_arena, n, stride, head, content, wire, in
         el = time.perf_counter() - t0
         best = el if best is None else min(best, el)
     ok = bool((res["status"] == 0).all())
-    lo, hi = (head, head + content) if dec else (0, wire)
+    lo, hi = (lead + head, lead + head + content) if dec else (lead, lead + wire)
     ref = out_arena                  # the device-resident run of the same records
     for i in sorted({0, E // 2, E - 1}):
         ok &= bool(torch.equal(host_out[i * stride + lo:i * stride + hi], ref[i * stride + lo:i * stride + hi].cpu()))

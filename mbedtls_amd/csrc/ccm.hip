@@ -40,8 +40,8 @@ __device__ __forceinline__ uint32_t w4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
 
-/* ARIA: ARIA-CCM (NR = 12/14/16; S-box tables in the same 64 KiB, round
- * keys SlotState::ark) -- the CCM construction around it unchanged */
+/* ARIA: ARIA-CCM / Camellia-CCM (NR = 12/14/16 / 18/24; the S-box image,
+ * round keys SlotState::ark) -- the CCM construction around it unchanged */
 template <int NR, bool ARIA, typename RK>
 __device__ __forceinline__ uint4 blk_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
 {
@@ -54,9 +54,10 @@ __device__ __forceinline__ uint4 blk_encrypt(const uint8_t *lds, uint32_t lb, RK
 template <int NR, bool DEC, bool CID = false, bool ARIA = false>
 __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[65536];   /* T0/T1 x 32 copies at offset 0 */
+    /* T0/T1 x 32 copies (64 KiB), or the ARIA / Camellia S-box image (32 KiB) */
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ARIA ? 32768 : 65536];
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t lanebase = ARIA ? (uint32_t) (lane & 15) << 2 : (uint32_t) (lane & 31) << 2;
+    const uint32_t lanebase = (uint32_t) (lane & 31) << 2;   /* T-table / S-box image copy */
     const uint32_t lo = a.perm ? *a.lo : 0u;
     const uint32_t count = a.perm ? *a.hi - lo : (uint32_t) a.n;
     const uint64_t wg_base = (uint64_t) blockIdx.x * CCM_THREADS;

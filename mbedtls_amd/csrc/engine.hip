@@ -211,10 +211,15 @@ static int gcm_waves(void)
 }
 
 /* wave-pass GCM variant (per-wave key passes, H^L per wave in LDS) for
- * tables of many keys with very few records each (auto: < 8 per key, where
- * a workgroup-wide key pass leaves most waves idle; measured +17-20 % at 4
- * x 16 KiB per key, -45 % at 16 per key).  TLSREC_GCM_WP=1 forces it, =0
- * disables it. */
+ * tables of many keys with very few records each (auto: < 12 per key, where
+ * a workgroup-wide key pass leaves most waves idle).  Lanes per record in
+ * it: 16 (a wave's 4 records share one key pass) from 3 records per key,
+ * 64 below.  Measured, 256 K x 16 KiB AES-256-GCM decrypt (GiB/s):
+ *   records/key        1     2     4     8    16    32
+ *   wave passes L=16   90   177   415   423   429   433
+ *   wave passes L=64  212   228   244   255   259   267
+ *   workgroup passes   56   108   208   369   536   584
+ * TLSREC_GCM_WP=1 forces it, =0 disables it. */
 static int gcm_wp_env(void)
 {
     const char *e = getenv("TLSREC_GCM_WP");   /* read per batch: tests switch it */
@@ -337,7 +342,9 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.out = out;
         int nr = (int) tlsrec_cipher_nr(cipher);
         const int wpe = gcm_wp_env();
-        const bool wp = !kt->has_cid && !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && rpk < 8));
+        const bool auto_l = !(lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64);
+        if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && rpk < 12) L = (rpk >= 3 && Lfill <= 16) ? 16 : 64;
+        const bool wp = !kt->has_cid && !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && rpk < 12));
         const int waves = wp ? 8 : (kt->has_cid ? 16 : gcm_waves());
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;

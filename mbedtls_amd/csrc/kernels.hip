@@ -141,11 +141,15 @@ __device__ inline uint64_t cam_f64(uint64_t x, uint64_t k)
 {
     x ^= k;
     const uint32_t xh = (uint32_t) (x >> 32), xl = (uint32_t) x;
-    const uint32_t u = kCamSbox.sp[0][xh >> 24] ^ kCamSbox.sp[1][(xh >> 16) & 0xff] ^
-                       kCamSbox.sp[2][(xh >> 8) & 0xff] ^ kCamSbox.sp[3][xh & 0xff];
-    const uint32_t v = kCamSbox.sp[1][xl >> 24] ^ kCamSbox.sp[2][(xl >> 16) & 0xff] ^
-                       kCamSbox.sp[3][(xl >> 8) & 0xff] ^ kCamSbox.sp[0][xl & 0xff];
-    return ((uint64_t) (u ^ v) << 32) | (u ^ ((u >> 8) | (u << 24)) ^ v);
+    const uint32_t A = ((uint32_t) kCamSbox.v[0][xh >> 24] << 24) | ((uint32_t) kCamSbox.v[1][(xh >> 16) & 0xff] << 16) |
+                       ((uint32_t) kCamSbox.v[2][(xh >> 8) & 0xff] << 8) | kCamSbox.v[3][xh & 0xff];
+    const uint32_t B = ((uint32_t) kCamSbox.v[1][xl >> 24] << 24) | ((uint32_t) kCamSbox.v[2][(xl >> 16) & 0xff] << 16) |
+                       ((uint32_t) kCamSbox.v[3][(xl >> 8) & 0xff] << 8) | kCamSbox.v[0][xl & 0xff];
+    /* P-layer as in cam_f (tlsrec_device.h) */
+    const uint32_t U = A ^ ((B << 8) | (B >> 24));
+    const uint32_t V = B ^ ((U << 16) | (U >> 16));
+    const uint32_t U2 = U ^ ((V >> 8) | (V << 24));
+    return ((uint64_t) (V ^ ((U2 >> 8) | (U2 << 24))) << 32) | U2;
 }
 
 __device__ inline void cam_rol128(uint64_t hi, uint64_t lo, int n, uint64_t &oh, uint64_t &ol)
@@ -668,8 +672,12 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         }
         const uint8_t inner_type = run ? p.inner_type : 0;
         const bool tls13 = run && p.inner;   /* TLS 1.3 or DTLS 1.2 + CID inner plaintext */
-        /* a readable 16-byte address for lanes with nothing to load */
-        const uint8_t *safe = run ? src : reinterpret_cast<const uint8_t *>(a.recs);
+        /* a readable 16-byte address for slots with nothing to load, in a
+         * line the step's other lanes read anyway: the record start for the
+         * front padding of step 0, its last content bytes for the tail (the
+         * start would be a second HBM trip by then) */
+        const uint8_t *safe0 = run ? src : reinterpret_cast<const uint8_t *>(a.recs);
+        const uint8_t *safe = run ? src + (content_len >= 16 ? (content_len - 16) & ~15u : 0u) : safe0;
         /* slot (L*t + q) of step j is record block 4(L j - z) + L t + q */
         const int32_t base0 = (int32_t) q - 4 * (int32_t) z;
 
@@ -705,7 +713,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
                 const int32_t i = (int32_t) (4 * L * j) + base0 + L * t;
                 const uint32_t pos = (uint32_t) i * 16;
                 fast[t] = live && i >= 0 && pos + 16 <= content_len;
-                ct[t] = gload16(fast[t] ? src + pos : safe);
+                ct[t] = gload16(fast[t] ? src + pos : (j == 0 ? safe0 : safe));
             }
             uint4 K[4];
             keystream(j, K);

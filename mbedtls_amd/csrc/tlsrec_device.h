@@ -214,21 +214,38 @@ __constant__ const AriaSboxGen kAriaSbox{};
         y[15] = xor3(xor3(x[1], x[2], x[4]), xor3(x[5], x[8], x[10]), x[15]);                \
     } while (0)
 
-/* LDS S-box tables: SB_t[x] as a dword (value in the low byte), 16 copies
- * (copy = lane & 15) at ARIA_OFF + t*16384 + x*64 + copy*4 -- 64 KiB, the
- * region the AES T-tables use. */
+/* LDS S-box image of the LDS-table block ciphers (ARIA, Camellia): for each
+ * byte value x, 32 copies (copy = lane & 31) of one dword holding the four
+ * S-box outputs S_0[x] .. S_3[x] in its bytes 0..3, at OFF + x*128 + copy*4
+ * (32 KiB).  A lookup is ds_read_u8 at OFF + (x << 7) + (lane & 31)*4 + t:
+ * each lane of a 32-lane ds_read group owns its bank ((a/4) mod 32 = lane &
+ * 31), so reads never conflict and their timing does not depend on the key
+ * or the data. */
+template <typename GEN>
+__device__ __forceinline__ void sbox_fill_tables(uint8_t *lds, int tid, int nthreads, const GEN &g)
+{
+    for (int i = tid; i < 256 * 8; i += nthreads) {
+        const int x = i >> 3, part = i & 7;   /* part: copies 4*part .. 4*part+3 */
+        const uint32_t v = (uint32_t) g.v[0][x] | ((uint32_t) g.v[1][x] << 8) | ((uint32_t) g.v[2][x] << 16) |
+                           ((uint32_t) g.v[3][x] << 24);
+        *reinterpret_cast<uint4 *>(lds + x * 128 + part * 16) = make_uint4(v, v, v, v);
+    }
+}
+
+template <int OFF>
+__device__ __forceinline__ uint32_t sbox_lds(const uint8_t *lds, uint32_t lb, int t, uint32_t x)
+{
+    return lds[OFF + (x << 7) + lb + t];
+}
+
 __device__ __forceinline__ void aria_fill_tables(uint8_t *lds, int tid, int nthreads)
 {
-    for (int i = tid; i < 4 * 256 * 4; i += nthreads) {
-        const int t = i >> 10, x = (i >> 2) & 255, part = i & 3;   /* part: copies 4*part .. 4*part+3 */
-        const uint32_t v = kAriaSbox.v[t][x];
-        *reinterpret_cast<uint4 *>(lds + t * 16384 + x * 64 + part * 16) = make_uint4(v, v, v, v);
-    }
+    sbox_fill_tables(lds, tid, nthreads, kAriaSbox);
 }
 
 /* ARIA forward cipher (NR = 12/14/16 rounds) of one block per lane.  Words
  * are little-endian (byte i of the block = byte i%4 of word i/4); rk = the
- * NR + 1 round keys as 4 words each.  lb = (lane & 15) * 4. */
+ * NR + 1 round keys as 4 words each.  lb = (lane & 31) * 4. */
 template <int NR, int ARIA_OFF, typename RK>
 __device__ __forceinline__ uint4 aria_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
 {
@@ -245,8 +262,7 @@ __device__ __forceinline__ uint4 aria_encrypt(const uint8_t *lds, uint32_t lb, R
         for (int i = 0; i < 16; i++) {
             const uint32_t kb = (rk[4 * (r - 1) + (i >> 2)] >> (8 * (i & 3))) & 0xffu;
             const int t = odd ? (i & 3) : ((i & 3) ^ 2);
-            const uint32_t a = ((x[i] ^ kb) << 6) + lb;
-            x[i] = *reinterpret_cast<const uint32_t *>(lds + ARIA_OFF + t * 16384 + a);
+            x[i] = sbox_lds<ARIA_OFF>(lds, lb, t, x[i] ^ kb);
         }
         if (r != NR) {
             TLSREC_ARIA_A(y, x);
@@ -263,18 +279,13 @@ __device__ __forceinline__ uint4 aria_encrypt(const uint8_t *lds, uint32_t lb, R
 
 /* ---------------- Camellia (RFC 3713) ----------------------------------- */
 /* SBOX1 (RFC 3713 2.4.4); SBOX2 = SBOX1 <<< 1, SBOX3 = SBOX1 <<< 7,
- * SBOX4(x) = SBOX1(x <<< 1).  The F-function's P-layer folds into four dword
- * tables, one per S-box, SP_i[x] = SBOX_i(x) placed in the bytes of the
- * P-layer column it feeds (y1 = the top byte):
- *   SP1 = s.s.s.0, SP2 = 0.s.s.s, SP3 = s.0.s.s, SP4 = s.s.0.s.
- * For F's input halves xh = t1..t4, xl = t5..t8 (S-boxes 1234 and 2341):
- *   U = SP1[t1]^SP2[t2]^SP3[t3]^SP4[t4],  V = SP2[t5]^SP3[t6]^SP4[t7]^SP1[t8],
- *   y1..y4 = U ^ V,  y5..y8 = U ^ (U >>> 8) ^ V
- * (the right half's U-columns are the byte-neighbour sums of the left's). */
+ * SBOX4(x) = SBOX1(x <<< 1); staged as the four bytes of the S-box image
+ * (sbox_fill_tables). */
 struct CamSboxGen {
-    uint8_t s1[256];
-    uint32_t sp[4][256];
-    constexpr CamSboxGen() : s1{
+    uint8_t v[4][256];
+    constexpr CamSboxGen() : v()
+    {
+        constexpr uint8_t s1[256] = {
     112, 130,  44, 236, 179,  39, 192, 229, 228, 133,  87,  53, 234,  12, 174,  65,
      35, 239, 107, 147,  69,  25, 165,  33, 237,  14,  79,  78,  29, 101, 146, 189,
     134, 184, 175, 143, 124, 235,  31, 206,  62,  48, 220,  95,  94, 197,  11,  26,
@@ -291,58 +302,53 @@ struct CamSboxGen {
     120, 152,   6, 106, 231,  70, 113, 186, 212,  37, 171,  66, 136, 162, 141, 250,
     114,   7, 185,  85, 248, 238, 172,  10,  54,  73,  42, 104,  60,  56, 241, 164,
      64,  40, 211, 123, 187, 201,  67, 193,  21, 227, 173, 244, 119, 199, 128, 158,
-    }, sp()
-    {
+        };
         for (int x = 0; x < 256; x++) {
             const uint32_t a = s1[x];
-            const uint32_t b = ((a << 1) | (a >> 7)) & 0xffu;                      /* SBOX2 */
-            const uint32_t c = ((a << 7) | (a >> 1)) & 0xffu;                      /* SBOX3 */
-            const uint32_t d = s1[((x << 1) | (x >> 7)) & 0xff];                   /* SBOX4 */
-            sp[0][x] = (a << 24) | (a << 16) | (a << 8);
-            sp[1][x] = (b << 16) | (b << 8) | b;
-            sp[2][x] = (c << 24) | (c << 8) | c;
-            sp[3][x] = (d << 24) | (d << 16) | d;
+            v[0][x] = (uint8_t) a;
+            v[1][x] = (uint8_t) ((a << 1) | (a >> 7));                /* SBOX2 */
+            v[2][x] = (uint8_t) ((a << 7) | (a >> 1));                /* SBOX3 */
+            v[3][x] = s1[((x << 1) | (x >> 7)) & 0xff];               /* SBOX4 */
         }
     }
 };
 
 __constant__ const CamSboxGen kCamSbox{};
 
-/* LDS SP tables in the ARIA layout: SP_t[x] at t*16384 + x*64 + copy*4 */
 __device__ __forceinline__ void cam_fill_tables(uint8_t *lds, int tid, int nthreads)
 {
-    for (int i = tid; i < 4 * 256 * 4; i += nthreads) {
-        const int t = i >> 10, x = (i >> 2) & 255, part = i & 3;
-        const uint32_t v = kCamSbox.sp[t][x];
-        *reinterpret_cast<uint4 *>(lds + t * 16384 + x * 64 + part * 16) = make_uint4(v, v, v, v);
-    }
+    sbox_fill_tables(lds, tid, nthreads, kCamSbox);
 }
 
-template <int OFF>
-__device__ __forceinline__ uint32_t cam_sp(const uint8_t *lds, uint32_t lb, int t, uint32_t x)
-{
-    return *reinterpret_cast<const uint32_t *>(lds + OFF + t * 16384 + (x << 6) + lb);
-}
-
-/* F(x ^ k) on the 64-bit half (h = the high word) */
+/* F(x ^ k) on the 64-bit half (h = the high word): S-boxes 1234 / 2341 on
+ * the bytes t1..t8 of x ^ k (t1 = the top byte of h), then the P-layer on
+ * A = z1..z4, B = z5..z8 (big-endian words) as word rotations:
+ *   U = A ^ (B <<< 8),  V = B ^ (U <<< 16),  U' = U ^ (V >>> 8),
+ *   y1..y4 = V ^ (U' >>> 8),  y5..y8 = U'
+ * (each y_i the XOR of the RFC 3713 2.4.3 terms). */
 template <int OFF>
 __device__ __forceinline__ void cam_f(const uint8_t *lds, uint32_t lb, uint32_t xh, uint32_t xl, uint32_t kh,
                                       uint32_t kl, uint32_t &oh, uint32_t &ol)
 {
     xh ^= kh;
     xl ^= kl;
-    const uint32_t u = xor3(cam_sp<OFF>(lds, lb, 0, xh >> 24), cam_sp<OFF>(lds, lb, 1, (xh >> 16) & 0xffu),
-                            cam_sp<OFF>(lds, lb, 2, (xh >> 8) & 0xffu)) ^ cam_sp<OFF>(lds, lb, 3, xh & 0xffu);
-    const uint32_t v = xor3(cam_sp<OFF>(lds, lb, 1, xl >> 24), cam_sp<OFF>(lds, lb, 2, (xl >> 16) & 0xffu),
-                            cam_sp<OFF>(lds, lb, 3, (xl >> 8) & 0xffu)) ^ cam_sp<OFF>(lds, lb, 0, xl & 0xffu);
-    oh = u ^ v;
-    ol = xor3(u, __builtin_amdgcn_alignbit(u, u, 8), v);
+    const uint32_t z1 = sbox_lds<OFF>(lds, lb, 0, xh >> 24), z2 = sbox_lds<OFF>(lds, lb, 1, (xh >> 16) & 0xffu);
+    const uint32_t z3 = sbox_lds<OFF>(lds, lb, 2, (xh >> 8) & 0xffu), z4 = sbox_lds<OFF>(lds, lb, 3, xh & 0xffu);
+    const uint32_t z5 = sbox_lds<OFF>(lds, lb, 1, xl >> 24), z6 = sbox_lds<OFF>(lds, lb, 2, (xl >> 16) & 0xffu);
+    const uint32_t z7 = sbox_lds<OFF>(lds, lb, 3, (xl >> 8) & 0xffu), z8 = sbox_lds<OFF>(lds, lb, 0, xl & 0xffu);
+    const uint32_t A = (z1 << 24) | (z2 << 16) | (z3 << 8) | z4;
+    const uint32_t B = (z5 << 24) | (z6 << 16) | (z7 << 8) | z8;
+    const uint32_t U = A ^ __builtin_amdgcn_alignbit(B, B, 24);
+    const uint32_t V = B ^ __builtin_amdgcn_alignbit(U, U, 16);
+    const uint32_t U2 = U ^ __builtin_amdgcn_alignbit(V, V, 8);
+    oh = V ^ __builtin_amdgcn_alignbit(U2, U2, 8);
+    ol = U2;
 }
 
 /* Camellia forward cipher (NR = 18 / 24 rounds) of one block per lane.  Words
  * of in/out are little-endian byte quadruples of the block; rk = the 64-bit
  * subkeys in use order (kw1 kw2 | k1..k6 | ke1 ke2 | ... | kw3 kw4) as
- * (high, low) word pairs.  lb = (lane & 15) * 4. */
+ * (high, low) word pairs.  lb = (lane & 31) * 4. */
 template <int NR, int OFF, typename RK>
 __device__ __forceinline__ uint4 cam_encrypt(const uint8_t *lds, uint32_t lb, RK rk, uint4 in)
 {

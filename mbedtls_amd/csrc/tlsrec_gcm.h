@@ -114,7 +114,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     __shared__ __attribute__((aligned(16))) uint8_t lds[LY::BYTES];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane / L, q = lane % L;
-    const uint32_t lanebase = ARIA ? (uint32_t) (lane & 15) << 2 : (uint32_t) (lane & 31) << 2;
+    const uint32_t lanebase = (uint32_t) (lane & 31) << 2;   /* T-table / S-box image copy */
     uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + LY::CTL);
 
     /* This workgroup's positions: wave w owns positions base + k*W + w,
