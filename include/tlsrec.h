@@ -282,6 +282,14 @@ int tlsrec_host_batch_decrypt(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, t
 int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_batch_rec *rec,
                        tlsrec_batch_res *early, uint32_t *aead_pos, uint32_t *aead_len);
 
+/* Host-only: rank `rank`'s contiguous share of a batch of n_records split
+ * over `world` GPUs (one process per GPU): ranks differ
+ * by at most one record, every record has exactly one owner.  The key table
+ * reaches the ranks by a broadcast of rank 0's tlsrec_key_material array
+ * (ncclBroadcast over RCCL/xGMI) followed by tlsrec_keytab_load with
+ * keys_on_device = 1 -- tests/c/mgpu_shard.c shows the sequence. */
+int tlsrec_shard_bounds(uint64_t n_records, uint32_t rank, uint32_t world, uint64_t *start, uint64_t *count);
+
 /* ---- TLS 1.3 key schedule (library/ssl_tls13_keys.c) --------------------
  * HKDF-SHA256/384 on the GPU: the reference's single-shot functions with the
  * same arguments and return codes, plus a batch that derives many

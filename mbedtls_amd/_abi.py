@@ -131,6 +131,7 @@ SIGNATURES = {
     "tlsrec_host_batch_encrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, ctypes.c_uint64]),
     "tlsrec_host_batch_decrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, ctypes.c_uint64]),
     "tlsrec_frame_check": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP]),
+    "tlsrec_shard_bounds": (_INT, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP]),
     "tlsrec_device_check": (_INT, []),
     "tlsrec_tls13_hkdf_expand_label": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _VP, _SZ]),
     "tlsrec_tls13_derive_secret": (_INT, [_INT, _VP, _SZ, _VP, _SZ, _VP, _SZ, _INT, _VP, _SZ]),

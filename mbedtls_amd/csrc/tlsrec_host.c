@@ -245,3 +245,15 @@ int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_
     if (aead_len) *aead_len = p.aead_len;
     return p.status == 0;
 }
+
+/* Contiguous balanced record shard of one rank (mbedtls_amd/shard.py
+ * shard_bounds): the first n % world ranks take one
+ * extra record, so every record has exactly one owner. */
+int tlsrec_shard_bounds(uint64_t n_records, uint32_t rank, uint32_t world, uint64_t *start, uint64_t *count)
+{
+    if (world == 0 || rank >= world || !start || !count) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    const uint64_t base = n_records / world, extra = n_records % world;
+    *start = (uint64_t) rank * base + (rank < extra ? rank : extra);
+    *count = base + (rank < extra ? 1u : 0u);
+    return 0;
+}

@@ -80,3 +80,24 @@ def test_c_threads_concurrent_transforms():
     rc, out, err = _run("threads", 12, 100)
     assert rc == 0, (out, err)
     assert out["bad"] == 0
+
+
+MGPU = os.path.join(ROOT, "tests", "c", "mgpu_shard")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("records,content", [(4096, 1400), (777, 16383), (1, 0)])
+def test_c_multi_gpu_host_one_rank(records, content):
+    """tests/c/mgpu_shard.c at world 1 (one GPU per box here): rank 0's key
+    table through ncclBroadcast into tlsrec_keytab_load(keys_on_device=1),
+    tlsrec_shard_bounds, an encrypt/decrypt round trip of the shard and the
+    ncclAllReduce of status counts -- the C multi-GPU sequence of DESIGN.md
+    section 6.  World > 1 needs one GPU per rank (the driver's 8-GPU node)."""
+    assert _gpu(), "needs a GPU"
+    if not os.path.exists(MGPU):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c"), "mgpu_shard"], check=True)
+    p = subprocess.run([MGPU, "1", str(records), str(content)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, (p.stdout, p.stderr)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["pass"] is True and out["records"] == records and out["round_trip_ok"] == records
+    assert out["ranks_with_rank0_keys"] == 1 and out["shard0"] == [0, records]

@@ -1,8 +1,11 @@
 """Multi-rank sharding on CPU (gloo, world_size 2): the key table reaches
 every rank from rank 0, the record shards cover the batch exactly once, and
 per-rank processing of the shards reproduces the single-process results
-record for record.  The per-rank compute here is the oracle (CPU-only test
-box); on GPUs bench.py runs the same shard/broadcast path with the batch
+record for record.  Each rank runs the product's own host code on its shard
+-- tlsrec_shard_bounds and tlsrec_frame_check (the framing verdict of
+encrypt_buf / decrypt_buf, libtlsrec.so, no GPU needed) -- and the oracle as
+the AEAD stand-in of this CPU-only box; on GPUs bench.py and
+tests/c/mgpu_shard.c run the same shard/broadcast sequence with the batch
 kernels over RCCL."""
 import os
 import socket
@@ -39,12 +42,21 @@ def _worker(rank, world, port, q):
         keys = M.broadcast_keys(km, "cpu")
         got_km = keys.numpy().view(M.KEY_MATERIAL)
         sh = M.shard_bounds(len(recs), rank, world)
+        import ctypes
+        from mbedtls_amd import _abi
+        cs, cc = ctypes.c_uint64(), ctypes.c_uint64()
+        assert _abi.load().tlsrec_shard_bounds(len(recs), rank, world, ctypes.byref(cs), ctypes.byref(cc)) == 0
+        assert (cs.value, cc.value) == (sh.start, sh.count)
         part = B.Batch(slots, recs[sh.start:sh.stop])
+        frames = []
+        for d in part.desc:
+            go, early, pos, ln = M.frame_check(True, got_km[d["slot"]], d)
+            frames.append((go, int(early["status"]), pos, ln))
         outs, stats = part.run_oracle(True)
         res = np.zeros(len(stats), dtype=M.BATCH_RES)
         res["status"] = stats
         totals = M.reduce_status(res)
-        q.put((rank, sh.start, sh.count, got_km.tobytes(), [o.data() for o in outs], stats, totals.tolist()))
+        q.put((rank, sh.start, sh.count, got_km.tobytes(), [o.data() for o in outs], stats, totals.tolist(), frames))
     finally:
         dist.destroy_process_group()
 
@@ -64,10 +76,21 @@ def test_two_rank_shards_match_single_process():
     got.sort()
     slots, recs = _batch()
     ref_outs, ref_stats = B.Batch(slots, recs).run_oracle(True)
-    ref_km = B.Batch(slots, recs).key_materials().tobytes()
+    full = B.Batch(slots, recs)
+    ref_km = full.key_materials().tobytes()
+    kms = full.key_materials()
+    ref_frames = []
+    for d in full.desc:
+        go, early, pos, ln = M.frame_check(True, kms[d["slot"]], d)
+        ref_frames.append((go, int(early["status"]), pos, ln))
     covered = []
-    for rank, start, count, km, datas, stats, totals in got:
+    for rank, start, count, km, datas, stats, totals, frames in got:
         assert km == ref_km, f"rank {rank} key table differs from rank 0's"
+        assert frames == ref_frames[start:start + count]
+        # the framing verdict agrees with the oracle's outcome: a record the
+        # framing stops never reaches the AEAD
+        for (go, st, _, _), ost in zip(frames, stats):
+            assert go or ost == st
         covered += list(range(start, start + count))
         assert datas == [o.data() for o in ref_outs[start:start + count]]
         assert stats == ref_stats[start:start + count]
@@ -85,3 +108,20 @@ def test_shard_bounds_partition(n, world):
     assert max(counts) - min(counts) <= 1
     with pytest.raises(ValueError):
         M.shard_bounds(n, world, world)
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (5, 2), (1000, 3), (1 << 23, 8), (37, 8), (3, 16)])
+def test_c_shard_bounds_matches_python(n, world):
+    """tlsrec_shard_bounds (the C hosts' shard split, tlsrec_host.c) equals
+    mbedtls_amd.shard_bounds for every rank, and rejects bad ranks."""
+    import ctypes
+    from mbedtls_amd import _abi
+    lib = _abi.load()
+    for r in range(world):
+        s, c = ctypes.c_uint64(), ctypes.c_uint64()
+        assert lib.tlsrec_shard_bounds(n, r, world, ctypes.byref(s), ctypes.byref(c)) == 0
+        sh = M.shard_bounds(n, r, world)
+        assert (s.value, c.value) == (sh.start, sh.count)
+    s, c = ctypes.c_uint64(), ctypes.c_uint64()
+    assert lib.tlsrec_shard_bounds(n, world, world, ctypes.byref(s), ctypes.byref(c)) == M.ERR_SSL_BAD_INPUT_DATA
+    assert lib.tlsrec_shard_bounds(n, 0, 0, ctypes.byref(s), ctypes.byref(c)) == M.ERR_SSL_BAD_INPUT_DATA
