@@ -10,6 +10,7 @@
 #include <hipcub/hipcub.hpp>
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -235,9 +236,74 @@ static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t
     return (uint32_t) want;
 }
 
-/* Device scratch of one bucketed batch (stream-ordered allocation). */
+/* ---- per-stream device scratch (tlsrec_internal.h) ---- */
+struct ScratchEntry {
+    int device;
+    hipStream_t stream;
+    int kind;
+    void *mem;
+    size_t bytes;
+    pthread_mutex_t mu;
+    ScratchEntry *next;
+};
+static pthread_mutex_t g_scratch_mu = PTHREAD_MUTEX_INITIALIZER;
+static ScratchEntry *g_scratch = nullptr;
+
+extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, tlsrec_scratch_lease *lease)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    pthread_mutex_lock(&g_scratch_mu);
+    ScratchEntry *e = g_scratch;
+    while (e && !(e->device == dev && e->stream == st && e->kind == kind)) e = e->next;
+    if (!e) {
+        e = (ScratchEntry *) calloc(1, sizeof(*e));
+        if (!e) {
+            pthread_mutex_unlock(&g_scratch_mu);
+            return TLSREC_ERR_SSL_ALLOC_FAILED;
+        }
+        e->device = dev;
+        e->stream = st;
+        e->kind = kind;
+        pthread_mutex_init(&e->mu, NULL);
+        e->next = g_scratch;
+        g_scratch = e;
+    }
+    pthread_mutex_unlock(&g_scratch_mu);
+    pthread_mutex_lock(&e->mu);
+    if (e->bytes < bytes) {
+        /* grow: the stream's earlier work may still read the old buffer */
+        if (e->mem && (hipStreamSynchronize(st) != hipSuccess || hipFree(e->mem) != hipSuccess)) {
+            pthread_mutex_unlock(&e->mu);
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
+        e->mem = nullptr;
+        e->bytes = 0;
+        const size_t want = bytes + bytes / 4 + 4096;
+        if (hipMalloc(&e->mem, want) != hipSuccess) {
+            e->mem = nullptr;
+            pthread_mutex_unlock(&e->mu);
+            return TLSREC_ERR_SSL_ALLOC_FAILED;
+        }
+        e->bytes = want;
+    }
+    lease->mem = e->mem;
+    lease->entry = e;
+    return 0;
+}
+
+extern "C" void tlsrec__scratch_release(tlsrec_scratch_lease *lease)
+{
+    if (lease && lease->entry) {
+        pthread_mutex_unlock(&((ScratchEntry *) lease->entry)->mu);
+        lease->entry = nullptr;
+        lease->mem = nullptr;
+    }
+}
+
+/* Device scratch of one bucketed batch (the stream's kind-0 scratch). */
 struct BucketScratch {
-    void *mem = nullptr;
+    tlsrec_scratch_lease lease = { nullptr, nullptr };
     uint32_t *counts, *offs, *cursor, *perm;
     void *scan_tmp;
     size_t scan_bytes;
@@ -256,8 +322,9 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     const size_t al = 256;
     const size_t szk = (nk * 4 + al - 1) / al * al, szp = ((size_t) n * 4 + al - 1) / al * al;
     const size_t total = 3 * szk + szp + b.scan_bytes + al;
-    if (hipMallocAsync(&b.mem, total, st) != hipSuccess) return TLSREC_ERR_SSL_ALLOC_FAILED;
-    uint8_t *m = (uint8_t *) b.mem;
+    const int lr = tlsrec__scratch_acquire(st, 0, total, &b.lease);
+    if (lr) return lr;
+    uint8_t *m = (uint8_t *) b.lease.mem;
     b.counts = (uint32_t *) m;
     b.offs = (uint32_t *) (m + szk);
     b.cursor = (uint32_t *) (m + 2 * szk);
@@ -270,12 +337,13 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     a.n = n;
     a.capacity = kt->capacity;
     a.counts = b.counts;
+    a.offs = b.offs;
     a.cursor = b.cursor;
+    a.nk = (uint32_t) nk;
     a.perm = b.perm;
-    if (hipMemsetAsync(b.counts, 0, nk * 4, st) != hipSuccess ||
+    if (tlsrec__launch_bucket_zero(&a, st) != hipSuccess ||
         tlsrec__launch_bucket_count(&a, st) != hipSuccess ||
         hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, b.scan_bytes, b.counts, b.offs, (int) nk, st) != hipSuccess ||
-        hipMemcpyAsync(b.cursor, b.offs, nk * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         tlsrec__launch_bucket_scatter(&a, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     return 0;
@@ -300,7 +368,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     if (!identity) {
         int r = bucket(kt, recs, res, n, st, bs);
         if (r) {
-            if (bs.mem) hipFreeAsync(bs.mem, st);
+            tlsrec__scratch_release(&bs.lease);
             return r;
         }
     }
@@ -427,7 +495,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    if (bs.mem && hipFreeAsync(bs.mem, st) != hipSuccess && !rc) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    tlsrec__scratch_release(&bs.lease);
     return rc;
 }
 

@@ -392,6 +392,20 @@ __device__ __forceinline__ uint32_t bucket_claim(const BucketArgs &a, uint32_t *
     return cp ? pc : pg;
 }
 
+/* counts and cursors to zero: a kernel on the batch's stream rather than
+ * hipMemsetAsync / a device-to-device copy of the offsets, so the whole
+ * bucket pass is kernels in stream order on any HIP runtime (a C host on
+ * the system HIP 7.2 runtime saw the scatter read cursors that the
+ * offsets copy had not yet written, leaving stale perm entries) */
+__global__ __launch_bounds__(256) void tlsrec_bucket_zero_kernel(BucketArgs a)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < a.nk) {
+        a.counts[i] = 0;
+        a.cursor[i] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
 {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -410,7 +424,7 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_scatter_kernel(BucketArgs a
     uint32_t key = 0xffffffffu;
     if (i < a.n) key = bucket_key(a, a.recs[i]);
     const uint32_t pos = bucket_claim(a, a.cursor, key);
-    if (key != 0xffffffffu) a.perm[pos] = i;
+    if (key != 0xffffffffu) a.perm[a.offs[key] + pos] = i;
 }
 
 /* ======================================================================
@@ -908,6 +922,12 @@ extern "C" hipError_t tlsrec__launch_gcm(const GcmArgs *a, int dec, int lanes, i
                                          hipStream_t st)
 {
     return dec ? tlsrec__launch_gcm_dec(a, lanes, nr, waves, grid, st) : tlsrec__launch_gcm_enc(a, lanes, nr, waves, grid, st);
+}
+
+extern "C" hipError_t tlsrec__launch_bucket_zero(const BucketArgs *a, hipStream_t st)
+{
+    hipLaunchKernelGGL(tlsrec_bucket_zero_kernel, dim3((a->nk + 255) / 256), dim3(256), 0, st, *a);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t tlsrec__launch_bucket_count(const BucketArgs *a, hipStream_t st)

@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(64) kdf_job_kernel(const Job *jobs, uint32_t n
 struct DeriveArgs {
     tlsrec_tls13_secret *secrets;
     tlsrec_key_material *out;
-    const uint8_t *infos;
+    uint8_t infos[96];        /* the three encoded HkdfLabels, by value (no host staging buffer) */
     uint32_t len_upd, len_key, len_iv;
     uint32_t count, alg, cipher, key_len, update;
 };
@@ -305,13 +305,15 @@ __global__ void __launch_bounds__(64) tls13_derive_kernel(DeriveArgs a)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.count) return;
+    uint8_t infos[96];
+    for (int k = 0; k < 96; k++) infos[k] = a.infos[k];
     const uint32_t H = out_bytes(a.alg);
     uint8_t s[48];
     for (uint32_t k = 0; k < H; k++) s[k] = a.secrets[i].secret[k];
     if (a.update) {
         /* RFC 8446 7.2: secret_N+1 = HKDF-Expand-Label(secret_N, "traffic upd", "", H) */
         uint8_t nx[48];
-        hkdf_expand(a.alg, s, H, a.infos, a.len_upd, nullptr, 0, nx, H);
+        hkdf_expand(a.alg, s, H, infos, a.len_upd, nullptr, 0, nx, H);
         for (uint32_t k = 0; k < H; k++) {
             s[k] = nx[k];
             a.secrets[i].secret[k] = nx[k];
@@ -325,8 +327,8 @@ __global__ void __launch_bounds__(64) tls13_derive_kernel(DeriveArgs a)
     km.fixed_ivlen = 12;      /* TLS 1.3: fixed_ivlen = ivlen = 12, ssl_tls13_keys.c:985-998 */
     km.taglen = (uint8_t) tlsrec_cipher_taglen((int) a.cipher);
     /* ssl_tls13_make_traffic_key, ssl_tls13_keys.c:219-246 */
-    hkdf_expand(a.alg, s, H, a.infos + a.len_upd, a.len_key, nullptr, 0, km.key, a.key_len);
-    hkdf_expand(a.alg, s, H, a.infos + a.len_upd + a.len_key, a.len_iv, nullptr, 0, km.iv, 12);
+    hkdf_expand(a.alg, s, H, infos + a.len_upd, a.len_key, nullptr, 0, km.key, a.key_len);
+    hkdf_expand(a.alg, s, H, infos + a.len_upd + a.len_key, a.len_iv, nullptr, 0, km.iv, 12);
     uint4 *dst = reinterpret_cast<uint4 *>(a.out + i);
     const uint4 *src = reinterpret_cast<const uint4 *>(&km);
 #pragma unroll
@@ -668,16 +670,10 @@ extern "C" int tlsrec_tls13_keytab_derive(tlsrec_keytab *kt, uint32_t first, uin
     const size_t lu = encode_label(H, (const unsigned char *) "traffic upd", 11, nullptr, 0, infos);
     const size_t lk = encode_label(key_len, (const unsigned char *) "key", 3, nullptr, 0, infos + lu);
     const size_t lv = encode_label(12, (const unsigned char *) "iv", 2, nullptr, 0, infos + lu + lk);
-    uint8_t *d_infos = nullptr;
-    if (hipMallocAsync((void **) &d_infos, 128, st) != hipSuccess) return TLSREC_ERR_SSL_ALLOC_FAILED;
-    if (hipMemcpyAsync(d_infos, infos, lu + lk + lv, hipMemcpyHostToDevice, st) != hipSuccess) {
-        hipFreeAsync(d_infos, st);
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    }
     DeriveArgs a;
     a.secrets = secrets;
     a.out = tlsrec__keytab_stage(kt) + first;
-    a.infos = d_infos;
+    memcpy(a.infos, infos, sizeof(a.infos));
     a.len_upd = (uint32_t) lu;
     a.len_key = (uint32_t) lk;
     a.len_iv = (uint32_t) lv;
@@ -688,7 +684,6 @@ extern "C" int tlsrec_tls13_keytab_derive(tlsrec_keytab *kt, uint32_t first, uin
     a.update = key_update ? 1u : 0u;
     hipLaunchKernelGGL(tls13_derive_kernel, dim3((count + 63) / 64), dim3(64), 0, st, a);
     int r = hipGetLastError() == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    hipFreeAsync(d_infos, st);
     if (r == 0) r = tlsrec__keytab_commit_staged(kt, first, count, cipher, st);
     return r;
 }

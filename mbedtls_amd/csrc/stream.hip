@@ -381,7 +381,7 @@ using namespace tlsst;
  * ==================================================================== */
 namespace {
 struct Scratch {
-    void *mem = nullptr;
+    tlsrec_scratch_lease lease = { nullptr, nullptr };
     uint32_t *counts = nullptr, *offs = nullptr;
     HdrStop *stops = nullptr;
     void *scan_tmp = nullptr;
@@ -395,8 +395,9 @@ static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
                                          (int) n + 1, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     const size_t a = 256, sz4 = (((size_t) n + 1) * 4 + a - 1) / a * a, szs = ((size_t) n * sizeof(HdrStop) + a) / a * a;
-    if (hipMallocAsync(&sc.mem, 2 * sz4 + szs + sc.scan_bytes + a, st) != hipSuccess) return TLSREC_ERR_SSL_ALLOC_FAILED;
-    uint8_t *m = (uint8_t *) sc.mem;
+    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + sc.scan_bytes + a, &sc.lease);
+    if (lr) return lr;
+    uint8_t *m = (uint8_t *) sc.lease.mem;
     sc.counts = (uint32_t *) m;
     sc.offs = (uint32_t *) (m + sz4);
     sc.stops = (HdrStop *) (m + 2 * sz4);
@@ -449,7 +450,7 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
                            sc.counts, sc.stops, slots, cap, recs, res, sres);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    if (sc.mem && hipFreeAsync(sc.mem, st) != hipSuccess && r == 0) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    tlsrec__scratch_release(&sc.lease);
     if (r == 0 && nrecords) *nrecords = total;
     return r;
 }
@@ -506,7 +507,7 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
                            sc.offs, sc.counts, slots, cap, res, sres);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
-    if (sc.mem && hipFreeAsync(sc.mem, st) != hipSuccess && r == 0) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    tlsrec__scratch_release(&sc.lease);
     if (r == 0 && nrecords) *nrecords = total;
     return r;
 }

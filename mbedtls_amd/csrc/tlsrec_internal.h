@@ -81,9 +81,10 @@ struct BucketArgs {
     tlsrec_batch_res *res;
     uint32_t n;
     uint32_t capacity;
-    uint32_t *counts;         /* [10 * capacity + 2] records per (class, slot), then exclusive offsets */
-    uint32_t *cursor;         /* copy of the offsets, consumed by the scatter */
-    uint32_t *cp_cursor;      /* ChaCha records appended after the GCM ones */
+    uint32_t *counts;         /* [nk = 10 * capacity + 2] records per (class, slot) */
+    const uint32_t *offs;     /* [nk] their exclusive prefix sums (class start in perm) */
+    uint32_t *cursor;         /* [nk] records placed so far, from zero (the scatter) */
+    uint32_t nk;
     uint32_t *perm;           /* [n] */
 };
 
@@ -113,6 +114,22 @@ hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int 
                               hipStream_t st);
 hipError_t tlsrec__launch_chachapoly(const tlsrec::CpArgs *a, int dec, int lanes, uint32_t grid,
                                      hipStream_t st);
+/* Per-(device, stream, kind) device scratch, reused across calls (engine.hip).
+ * Work enqueued on one stream is ordered, so a stream's scratch can be
+ * reused by its next call without waiting; the lease's lock keeps two host
+ * threads from interleaving their enqueues on one stream's scratch.  (The
+ * stream-ordered allocator, hipMallocAsync / hipFreeAsync, was dropped:
+ * under the system HIP 7.2 runtime a C host saw whole batches silently
+ * skipped after a batch in the other direction -- results never written --
+ * which plain allocations do not show.)  kind: 0 the bucket pass, 1 the
+ * stream record layer (which calls the batch path inside its lease). */
+typedef struct tlsrec_scratch_lease {
+    void *mem;
+    void *entry;
+} tlsrec_scratch_lease;
+int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, tlsrec_scratch_lease *lease);
+void tlsrec__scratch_release(tlsrec_scratch_lease *lease);
+hipError_t tlsrec__launch_bucket_zero(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_count(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_t st);
 }

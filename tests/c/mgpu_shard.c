@@ -14,8 +14,8 @@
  *
  *   mgpu_shard [world] [records] [content]
  *
- * Forks `world` processes (rank r on device r % device count); the parent
- * touches no GPU.  Each rank checks that its key table equals rank 0's and
+ * Forks `world` processes (rank r on device r % device count; world 1 runs
+ * in this process); the parent touches no GPU.  Each rank checks that its key table equals rank 0's and
  * that every record of its shard round-trips (encrypt, decrypt, plaintext
  * and statuses compared).  Rank 0 prints one JSON line; exit status 0 = pass.
  */
@@ -132,6 +132,7 @@ static int run_rank(int rank, int world, ncclUniqueId id, uint64_t n, uint32_t c
         h_recs[i].type = h_res[i].type;
     }
     CK(hipMemcpy(d_recs, h_recs, count * sizeof(*d_recs), hipMemcpyHostToDevice));
+    CK(hipMemset(d_res, 0x55, count * sizeof(*d_res)));   /* every result must be written */
     CT(tlsrec_batch_decrypt(kt, d_recs, d_res, (uint32_t) count, d_arena, d_arena, 0, st));
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(h_res, d_res, count * sizeof(*h_res), hipMemcpyDeviceToHost));
@@ -153,6 +154,11 @@ static int run_rank(int rank, int world, ncclUniqueId id, uint64_t n, uint32_t c
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(tot, d_tot, sizeof(tot), hipMemcpyDeviceToHost));
     const int pass = tot[0] == n && tot[1] == n && tot[2] == n && tot[3] == (uint64_t) world;
+    if (!pass)
+        fprintf(stderr, "rank %d: shard [%llu, +%llu) encrypt ok %llu, round trip ok %llu, keys %s; first status %d len %u\n",
+                rank, (unsigned long long) start, (unsigned long long) count, (unsigned long long) enc_ok,
+                (unsigned long long) ok, keys_match ? "match" : "DIFFER", count ? h_res[0].status : 0,
+                count ? h_res[0].data_len : 0);
     if (rank == 0)
         printf("{\"world\": %d, \"records\": %llu, \"round_trip_ok\": %llu, \"encrypt_ok\": %llu, "
                "\"ranks_with_rank0_keys\": %llu, \"shard0\": [%llu, %llu], \"pass\": %s}\n",
@@ -176,6 +182,11 @@ int main(int argc, char **argv)
     const uint64_t n = argc > 2 ? strtoull(argv[2], NULL, 10) : 4096;
     const uint32_t content = argc > 3 ? (uint32_t) atoi(argv[3]) : 1400;
     if (world < 1 || world > 16 || content > 16383) return 2;
+    if (world == 1) {   /* one rank: in this process */
+        ncclUniqueId id;
+        if (ncclGetUniqueId(&id) != ncclSuccess) return 2;
+        return run_rank(0, 1, id, n, content);
+    }
     /* rank 0 makes the RCCL id and hands it to the others through a pipe:
      * the parent process never initialises the GPU */
     int fds[2];
@@ -193,8 +204,10 @@ int main(int argc, char **argv)
             } else if (read(fds[0], &id, sizeof(id)) != (ssize_t) sizeof(id)) {
                 _exit(2);
             }
+            const int rc = run_rank(r, world, id, n, content);
             fflush(stdout);
-            _exit(run_rank(r, world, id, n, content));
+            fflush(stderr);
+            _exit(rc);
         }
     }
     int fail = 0;

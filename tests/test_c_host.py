@@ -101,3 +101,19 @@ def test_c_multi_gpu_host_one_rank(records, content):
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["pass"] is True and out["records"] == records and out["round_trip_ok"] == records
     assert out["ranks_with_rank0_keys"] == 1 and out["shard0"] == [0, records]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pageable", "memset", "pinned"])
+def test_system_runtime_direction_switches(mode):
+    """Batch calls alternating encrypt / decrypt over a 256-key table on the
+    system HIP runtime (no torch in the process: what a C host links).  Every
+    call must write every result -- with the stream-ordered allocator for the
+    bucket scratch, the first call after a direction change wrote none."""
+    assert _gpu(), "needs a GPU"
+    env = dict(os.environ)
+    p = subprocess.run(["python3", os.path.join(ROOT, "tests", "sysrt_seq.py"), "64", "256", "eddeedde", mode],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["written"] == [64] * 8, out
