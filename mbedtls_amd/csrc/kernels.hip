@@ -33,7 +33,7 @@ namespace tlsrec {
 /* ======================================================================
  * Key setup
  * ==================================================================== */
-__device__ inline void aes_key_expand(const uint8_t *key, int nk, uint32_t *rk)
+__device__ inline void aes_key_expand(const uint8_t *sb, const uint8_t *key, int nk, uint32_t *rk)
 {
     const int nr = nk + 6, total = 4 * (nr + 1);
     for (int i = 0; i < nk; i++) {
@@ -45,26 +45,26 @@ __device__ inline void aes_key_expand(const uint8_t *key, int nk, uint32_t *rk)
         uint32_t t = rk[i - 1];
         if (i % nk == 0) {
             t = (t >> 8) | (t << 24);
-            t = (uint32_t) kSbox.v[t & 0xff] | ((uint32_t) kSbox.v[(t >> 8) & 0xff] << 8) |
-                ((uint32_t) kSbox.v[(t >> 16) & 0xff] << 16) | ((uint32_t) kSbox.v[t >> 24] << 24);
+            t = (uint32_t) sb[t & 0xff] | ((uint32_t) sb[(t >> 8) & 0xff] << 8) |
+                ((uint32_t) sb[(t >> 16) & 0xff] << 16) | ((uint32_t) sb[t >> 24] << 24);
             t ^= rcon;
             rcon = xtime8(rcon);
         } else if (nk > 6 && i % nk == 4) {
-            t = (uint32_t) kSbox.v[t & 0xff] | ((uint32_t) kSbox.v[(t >> 8) & 0xff] << 8) |
-                ((uint32_t) kSbox.v[(t >> 16) & 0xff] << 16) | ((uint32_t) kSbox.v[t >> 24] << 24);
+            t = (uint32_t) sb[t & 0xff] | ((uint32_t) sb[(t >> 8) & 0xff] << 8) |
+                ((uint32_t) sb[(t >> 16) & 0xff] << 16) | ((uint32_t) sb[t >> 24] << 24);
         }
         rk[i] = rk[i - nk] ^ t;
     }
 }
 
 /* byte-oriented AES (one lane; only used for H = E_K(0^128)) */
-__device__ inline void aes_encrypt_bytes(const uint32_t *rk, int nr, uint8_t st[16])
+__device__ inline void aes_encrypt_bytes(const uint8_t *sb, const uint32_t *rk, int nr, uint8_t st[16])
 {
     for (int i = 0; i < 16; i++) st[i] ^= (uint8_t) (rk[i / 4] >> (8 * (i % 4)));
     for (int r = 1; r <= nr; r++) {
         uint8_t t[16];
         for (int c = 0; c < 4; c++)
-            for (int row = 0; row < 4; row++) t[4 * c + row] = kSbox.v[st[4 * ((c + row) & 3) + row]];
+            for (int row = 0; row < 4; row++) t[4 * c + row] = sb[st[4 * ((c + row) & 3) + row]];
         if (r != nr) {
             for (int c = 0; c < 4; c++) {
                 uint32_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
@@ -81,12 +81,12 @@ __device__ inline void aes_encrypt_bytes(const uint32_t *rk, int nr, uint8_t st[
 
 /* ARIA key schedule and byte-wise block (RFC 5794 2.2, 2.3), one lane:
  * only for the round keys and H = E_K(0^128) of a slot. */
-__device__ inline void aria_round_bytes(uint8_t d[16], const uint8_t rk[16], bool odd, bool diffuse)
+__device__ inline void aria_round_bytes(const uint8_t *sb, uint8_t d[16], const uint8_t rk[16], bool odd, bool diffuse)
 {
     uint32_t x[16], y[16];
     for (int i = 0; i < 16; i++) {
         const int t = odd ? (i & 3) : ((i & 3) ^ 2);
-        x[i] = kAriaSbox.v[t][d[i] ^ rk[i]];
+        x[i] = sb[t * 256 + (d[i] ^ rk[i])];
     }
     if (diffuse) {
         TLSREC_ARIA_A(y, x);
@@ -96,7 +96,7 @@ __device__ inline void aria_round_bytes(uint8_t d[16], const uint8_t rk[16], boo
     }
 }
 
-__device__ inline int aria_key_expand(const uint8_t *key, int keylen, uint8_t ek[17][16])
+__device__ inline int aria_key_expand(const uint8_t *sb, const uint8_t *key, int keylen, uint8_t ek[17][16])
 {
     const uint8_t C[3][16] = {
         { 0x51, 0x7c, 0xc1, 0xb7, 0x27, 0x22, 0x0a, 0x94, 0xfe, 0x13, 0xab, 0xe8, 0xfa, 0x9a, 0x6e, 0xe0 },
@@ -107,13 +107,13 @@ __device__ inline int aria_key_expand(const uint8_t *key, int keylen, uint8_t ek
     uint8_t w[4][16], t[16], kr[16];
     for (int i = 0; i < 16; i++) { w[0][i] = key[i]; kr[i] = 16 + i < keylen ? key[16 + i] : 0; }
     for (int i = 0; i < 16; i++) t[i] = w[0][i];
-    aria_round_bytes(t, C[first], true, true);
+    aria_round_bytes(sb, t, C[first], true, true);
     for (int i = 0; i < 16; i++) w[1][i] = t[i] ^ kr[i];
     for (int i = 0; i < 16; i++) t[i] = w[1][i];
-    aria_round_bytes(t, C[(first + 1) % 3], false, true);
+    aria_round_bytes(sb, t, C[(first + 1) % 3], false, true);
     for (int i = 0; i < 16; i++) w[2][i] = t[i] ^ w[0][i];
     for (int i = 0; i < 16; i++) t[i] = w[2][i];
-    aria_round_bytes(t, C[(first + 2) % 3], true, true);
+    aria_round_bytes(sb, t, C[(first + 2) % 3], true, true);
     for (int i = 0; i < 16; i++) w[3][i] = t[i] ^ w[1][i];
     const int rot[5] = { 19, 31, 128 - 61, 128 - 31, 128 - 19 };   /* right rotations */
     for (int e = 0; e < nr + 1; e++) {
@@ -128,23 +128,23 @@ __device__ inline int aria_key_expand(const uint8_t *key, int keylen, uint8_t ek
     return nr;
 }
 
-__device__ inline void aria_encrypt_bytes(const uint8_t ek[17][16], int nr, uint8_t st[16])
+__device__ inline void aria_encrypt_bytes(const uint8_t *sb, const uint8_t ek[17][16], int nr, uint8_t st[16])
 {
-    for (int r = 1; r < nr; r++) aria_round_bytes(st, ek[r - 1], (r & 1) != 0, true);
-    aria_round_bytes(st, ek[nr - 1], false, false);
+    for (int r = 1; r < nr; r++) aria_round_bytes(sb, st, ek[r - 1], (r & 1) != 0, true);
+    aria_round_bytes(sb, st, ek[nr - 1], false, false);
     for (int i = 0; i < 16; i++) st[i] ^= ek[nr][i];
 }
 
 /* Camellia key schedule and 64-bit-word block (RFC 3713 2.2-2.4), one lane:
  * only for the subkeys and H = E_K(0^128) of a slot. */
-__device__ inline uint64_t cam_f64(uint64_t x, uint64_t k)
+__device__ inline uint64_t cam_f64(const uint8_t *sb, uint64_t x, uint64_t k)
 {
     x ^= k;
     const uint32_t xh = (uint32_t) (x >> 32), xl = (uint32_t) x;
-    const uint32_t A = ((uint32_t) kCamSbox.v[0][xh >> 24] << 24) | ((uint32_t) kCamSbox.v[1][(xh >> 16) & 0xff] << 16) |
-                       ((uint32_t) kCamSbox.v[2][(xh >> 8) & 0xff] << 8) | kCamSbox.v[3][xh & 0xff];
-    const uint32_t B = ((uint32_t) kCamSbox.v[1][xl >> 24] << 24) | ((uint32_t) kCamSbox.v[2][(xl >> 16) & 0xff] << 16) |
-                       ((uint32_t) kCamSbox.v[3][(xl >> 8) & 0xff] << 8) | kCamSbox.v[0][xl & 0xff];
+    const uint32_t A = ((uint32_t) sb[0 * 256 + (xh >> 24)] << 24) | ((uint32_t) sb[1 * 256 + ((xh >> 16) & 0xff)] << 16) |
+                       ((uint32_t) sb[2 * 256 + ((xh >> 8) & 0xff)] << 8) | sb[3 * 256 + (xh & 0xff)];
+    const uint32_t B = ((uint32_t) sb[1 * 256 + (xl >> 24)] << 24) | ((uint32_t) sb[2 * 256 + ((xl >> 16) & 0xff)] << 16) |
+                       ((uint32_t) sb[3 * 256 + ((xl >> 8) & 0xff)] << 8) | sb[0 * 256 + (xl & 0xff)];
     /* P-layer as in cam_f (tlsrec_device.h) */
     const uint32_t U = A ^ ((B << 8) | (B >> 24));
     const uint32_t V = B ^ ((U << 16) | (U >> 16));
@@ -161,7 +161,7 @@ __device__ inline void cam_rol128(uint64_t hi, uint64_t lo, int n, uint64_t &oh,
 }
 
 /* the 26 / 34 subkeys in use order (kw1 kw2 | k1..k6 | ke1 ke2 | ... | kw3 kw4) */
-__device__ inline int cam_key_expand(const uint8_t *key, int keylen, uint64_t sk[34])
+__device__ inline int cam_key_expand(const uint8_t *sb, const uint8_t *key, int keylen, uint64_t sk[34])
 {
     const uint64_t SIGMA[6] = { 0xA09E667F3BCC908BULL, 0xB67AE8584CAA73B2ULL, 0xC6EF372FE94F82BEULL,
                                 0x54FF53A5F1D36F1CULL, 0x10E527FADE682D1DULL, 0xB05688C2B3E6C1FDULL };
@@ -171,17 +171,17 @@ __device__ inline int cam_key_expand(const uint8_t *key, int keylen, uint64_t sk
     /* src: 0 KL, 1 KR, 2 KA, 3 KB as (hi, lo) */
     uint64_t src[4][2] = { { w[0], w[1] }, { w[2], w[3] }, { 0, 0 }, { 0, 0 } };
     uint64_t d1 = w[0] ^ w[2], d2 = w[1] ^ w[3];
-    d2 ^= cam_f64(d1, SIGMA[0]);
-    d1 ^= cam_f64(d2, SIGMA[1]);
+    d2 ^= cam_f64(sb, d1, SIGMA[0]);
+    d1 ^= cam_f64(sb, d2, SIGMA[1]);
     d1 ^= w[0];
     d2 ^= w[1];
-    d2 ^= cam_f64(d1, SIGMA[2]);
-    d1 ^= cam_f64(d2, SIGMA[3]);
+    d2 ^= cam_f64(sb, d1, SIGMA[2]);
+    d1 ^= cam_f64(sb, d2, SIGMA[3]);
     src[2][0] = d1; src[2][1] = d2;
     d1 ^= w[2];
     d2 ^= w[3];
-    d2 ^= cam_f64(d1, SIGMA[4]);
-    d1 ^= cam_f64(d2, SIGMA[5]);
+    d2 ^= cam_f64(sb, d1, SIGMA[4]);
+    d1 ^= cam_f64(sb, d2, SIGMA[5]);
     src[3][0] = d1; src[3][1] = d2;
     /* (source, rotation, halves: 3 both, 1 high, 2 low), RFC 3713 2.2 */
     const uint8_t s128[14][3] = { { 0, 0, 3 }, { 2, 0, 3 }, { 0, 15, 3 }, { 2, 15, 3 }, { 2, 30, 3 },
@@ -204,15 +204,15 @@ __device__ inline int cam_key_expand(const uint8_t *key, int keylen, uint64_t sk
     return keylen == 16 ? 18 : 24;
 }
 
-__device__ inline void cam_encrypt_u64(const uint64_t sk[34], int nr, uint64_t &hi, uint64_t &lo)
+__device__ inline void cam_encrypt_u64(const uint8_t *sb, const uint64_t sk[34], int nr, uint64_t &hi, uint64_t &lo)
 {
     uint64_t d1 = hi ^ sk[0], d2 = lo ^ sk[1];
     int i = 2;
     const int groups = nr / 6;
     for (int g = 0; g < groups; g++) {
         for (int r = 0; r < 3; r++) {
-            d2 ^= cam_f64(d1, sk[i++]);
-            d1 ^= cam_f64(d2, sk[i++]);
+            d2 ^= cam_f64(sb, d1, sk[i++]);
+            d1 ^= cam_f64(sb, d2, sk[i++]);
         }
         if (g != groups - 1) {
             uint32_t x1 = (uint32_t) (d1 >> 32), x2 = (uint32_t) d1;
@@ -242,6 +242,14 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
 {
     __shared__ G128 pw[KEY_TABLES];
     __shared__ uint4 base[KEY_TABLES][128];
+    /* the key schedule is built in LDS, not in the slot: the single lane
+     * that expands it and encrypts H reads it back word by word, and each
+     * of those reads from global memory was a full round trip (64 K AES-256
+     * slots: 5.6 ms with the schedule in the slot) */
+    __shared__ uint64_t ksched[34];
+    /* the cipher's S-boxes for that lane, from LDS (a constant-memory lookup
+     * per S-box byte is a memory round trip on its dependent chain) */
+    __shared__ uint8_t sb[4 * 256];
     const uint32_t slot = first + blockIdx.x;
     if (blockIdx.x >= count) return;
     SlotState *st = &slots[slot];
@@ -253,6 +261,9 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     const bool aria = tlsrec_cipher_is_aria(km.cipher);
     const bool cam = tlsrec_cipher_is_cam(km.cipher);
     const bool gcm = tlsrec_cipher_is_gcm(km.cipher) || tlsrec_cipher_is_alt_gcm(km.cipher);
+    for (int i = tid; i < 4 * 256; i += 256)
+        sb[i] = aria ? kAriaSbox.v[i >> 8][i & 255] : (cam ? kCamSbox.v[i >> 8][i & 255] : kSbox.v[i & 255]);
+    __syncthreads();
     if (tid == 0) {
         st->km = km;
         st->km.reserved[0] = 0;   /* CID length mirror (tlsrec_recdev.h plan_key) */
@@ -260,14 +271,16 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
         st->cid_len = 0;          /* a (re)load leaves the slot without a CID */
         if (aes) {
             const int nk = (int) tlsrec_cipher_keylen(km.cipher) / 4;
-            aes_key_expand(km.key, nk, st->rk);
+            uint32_t *rk = reinterpret_cast<uint32_t *>(ksched);
+            aes_key_expand(sb, km.key, nk, rk);
             st->nr = (uint32_t) (nk + 6);
             for (int i = 0; i < 4 * (nk + 7); i++) {
                 const bool middle = i >= 4 && i < 4 * (nk + 6);
-                st->rkr[i] = middle ? __builtin_amdgcn_alignbit(st->rk[i], st->rk[i], 16) : st->rk[i];
+                st->rk[i] = rk[i];
+                st->rkr[i] = middle ? __builtin_amdgcn_alignbit(rk[i], rk[i], 16) : rk[i];
             }
             uint8_t h[16] = { 0 };
-            aes_encrypt_bytes(st->rk, nk + 6, h);
+            aes_encrypt_bytes(sb, rk, nk + 6, h);
             G128 H;
             H.hi = 0; H.lo = 0;
             for (int i = 0; i < 8; i++) { H.hi = (H.hi << 8) | h[i]; H.lo = (H.lo << 8) | h[8 + i]; }
@@ -275,15 +288,15 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
             pw[0] = H;
             for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);
         } else if (aria) {
-            uint8_t ek[17][16];
-            const int nr = aria_key_expand(km.key, (int) tlsrec_cipher_keylen(km.cipher), ek);
+            uint8_t (*ek)[16] = reinterpret_cast<uint8_t (*)[16]>(ksched);
+            const int nr = aria_key_expand(sb, km.key, (int) tlsrec_cipher_keylen(km.cipher), ek);
             for (int e = 0; e < 17; e++)
                 for (int c = 0; c < 4; c++)
                     st->ark[4 * e + c] = e <= nr ? ((uint32_t) ek[e][4 * c] | ((uint32_t) ek[e][4 * c + 1] << 8) |
                                                     ((uint32_t) ek[e][4 * c + 2] << 16) | ((uint32_t) ek[e][4 * c + 3] << 24))
                                                  : 0u;
             uint8_t h[16] = { 0 };
-            aria_encrypt_bytes(ek, nr, h);
+            aria_encrypt_bytes(sb, ek, nr, h);
             G128 H;
             H.hi = 0; H.lo = 0;
             for (int i = 0; i < 8; i++) { H.hi = (H.hi << 8) | h[i]; H.lo = (H.lo << 8) | h[8 + i]; }
@@ -292,15 +305,15 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
             for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);
         } else if (cam) {
             /* Camellia: the subkeys as (high, low) word pairs (tlsrec_device.h cam_encrypt) */
-            uint64_t sk[34];
-            const int nr = cam_key_expand(km.key, (int) tlsrec_cipher_keylen(km.cipher), sk);
+            uint64_t *sk = ksched;
+            const int nr = cam_key_expand(sb, km.key, (int) tlsrec_cipher_keylen(km.cipher), sk);
             for (int i = 0; i < 34; i++) {
                 st->ark[2 * i] = (uint32_t) (sk[i] >> 32);
                 st->ark[2 * i + 1] = (uint32_t) sk[i];
             }
             G128 H;
             H.hi = 0; H.lo = 0;
-            cam_encrypt_u64(sk, nr, H.hi, H.lo);
+            cam_encrypt_u64(sb, sk, nr, H.hi, H.lo);
             for (int i = 0; i < 8; i++) { st->h[i] = (uint8_t) (H.hi >> (56 - 8 * i)); st->h[8 + i] = (uint8_t) (H.lo >> (56 - 8 * i)); }
             pw[0] = H;
             for (int p = 1; p < KEY_TABLES; p++) pw[p] = g_mul(pw[p - 1], pw[p - 1]);

@@ -303,10 +303,12 @@ struct DeriveArgs {
 
 __global__ void __launch_bounds__(64) tls13_derive_kernel(DeriveArgs a)
 {
+    /* the encoded labels (kernel argument) staged once per workgroup */
+    __shared__ uint8_t infos[96];
+    for (int k = threadIdx.x; k < 96; k += blockDim.x) infos[k] = a.infos[k];
+    __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.count) return;
-    uint8_t infos[96];
-    for (int k = 0; k < 96; k++) infos[k] = a.infos[k];
     const uint32_t H = out_bytes(a.alg);
     uint8_t s[48];
     for (uint32_t k = 0; k < H; k++) s[k] = a.secrets[i].secret[k];
