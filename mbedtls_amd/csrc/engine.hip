@@ -92,6 +92,12 @@ extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
 
 extern "C" uint32_t tlsrec_keytab_capacity(const tlsrec_keytab *kt) { return kt ? kt->capacity : 0; }
 
+/* host mirror of a slot's cipher (0 = never loaded) */
+extern "C" int tlsrec__keytab_cipher(const tlsrec_keytab *kt, uint32_t slot)
+{
+    return kt && slot < kt->capacity ? kt->h_cipher[slot] : 0;
+}
+
 extern "C" int tlsrec_keytab_set_cid(tlsrec_keytab *kt, uint32_t slot, const unsigned char *cid, size_t cid_len,
                                      void *stream)
 {

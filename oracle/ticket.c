@@ -28,20 +28,47 @@
 #define TKT_MIN (TKT_NAME + TKT_IV + TKT_LEN + TKT_TAG)
 #define TKT_AAD (TKT_NAME + TKT_IV + TKT_LEN)
 
+/* The ticket key's AEAD: mbedtls_ssl_ticket_setup (ssl_ticket.c:188-209)
+ * takes any PSA AEAD key type -- AES, ARIA and Camellia with GCM or CCM
+ * (16-byte tag, :185), and ChaCha20-Poly1305. */
 static int tkt_cipher_ok(int c)
 {
-    return c == ORC_CIPHER_AES_128_GCM || c == ORC_CIPHER_AES_192_GCM || c == ORC_CIPHER_AES_256_GCM ||
-           c == ORC_CIPHER_AES_128_CCM || c == ORC_CIPHER_AES_192_CCM || c == ORC_CIPHER_AES_256_CCM ||
-           c == ORC_CIPHER_CHACHA20_POLY1305;
+    return (c >= ORC_CIPHER_AES_128_GCM && c <= ORC_CIPHER_AES_256_CCM) ||
+           (c >= ORC_CIPHER_ARIA_128_GCM && c <= ORC_CIPHER_CAMELLIA_256_CCM);
 }
 
 static size_t tkt_keylen(int c)
 {
     switch (c) {
-        case ORC_CIPHER_AES_128_GCM: case ORC_CIPHER_AES_128_CCM: return 16;
-        case ORC_CIPHER_AES_192_GCM: case ORC_CIPHER_AES_192_CCM: return 24;
+        case ORC_CIPHER_AES_128_GCM: case ORC_CIPHER_AES_128_CCM: case ORC_CIPHER_ARIA_128_GCM:
+        case ORC_CIPHER_ARIA_128_CCM: case ORC_CIPHER_CAMELLIA_128_GCM: case ORC_CIPHER_CAMELLIA_128_CCM:
+            return 16;
+        case ORC_CIPHER_AES_192_GCM: case ORC_CIPHER_AES_192_CCM: case ORC_CIPHER_ARIA_192_GCM:
+        case ORC_CIPHER_ARIA_192_CCM: case ORC_CIPHER_CAMELLIA_192_GCM: case ORC_CIPHER_CAMELLIA_192_CCM:
+            return 24;
         default: return 32;
     }
+}
+
+/* block cipher of the GCM / CCM code: 0 AES, 1 ARIA, 2 Camellia */
+static int tkt_bc(int c)
+{
+    return c >= ORC_CIPHER_CAMELLIA_128_GCM ? 2 : (c >= ORC_CIPHER_ARIA_128_GCM ? 1 : 0);
+}
+
+static int tkt_is_ccm(int c)
+{
+    return (c >= ORC_CIPHER_AES_128_CCM && c <= ORC_CIPHER_AES_256_CCM) ||
+           (c >= ORC_CIPHER_ARIA_128_CCM && c <= ORC_CIPHER_ARIA_256_CCM) || c >= ORC_CIPHER_CAMELLIA_128_CCM;
+}
+
+static void tkt_bc_setkey(orc_aes_ctx *a, int c, const uint8_t *key)
+{
+    const unsigned bits = (unsigned) tkt_keylen(c) * 8;
+    const int bc = tkt_bc(c);
+    if (bc == 2) orc_camellia_setkey_enc(a, key, bits);
+    else if (bc == 1) orc_aria_setkey_enc(a, key, bits);
+    else orc_aes_setkey_enc(a, key, bits);
 }
 
 static void tkt_seal(const orc_ticket_key *k, const uint8_t *aad, uint8_t *data, size_t len, uint8_t *tag)
@@ -49,13 +76,13 @@ static void tkt_seal(const orc_ticket_key *k, const uint8_t *aad, uint8_t *data,
     const uint8_t *iv = aad + TKT_NAME;
     if (k->cipher == ORC_CIPHER_CHACHA20_POLY1305) {
         orc_chachapoly_encrypt(k->key, iv, aad, TKT_AAD, data, len, data, tag);
-    } else if (k->cipher >= ORC_CIPHER_AES_128_CCM) {
+    } else if (tkt_is_ccm(k->cipher)) {
         orc_aes_ctx a;
-        orc_aes_setkey_enc(&a, k->key, (unsigned) tkt_keylen(k->cipher) * 8);
+        tkt_bc_setkey(&a, k->cipher, k->key);
         orc_ccm_encrypt(&a, iv, aad, TKT_AAD, data, len, data, tag, TKT_TAG);
     } else {
         orc_gcm_ctx g;
-        orc_gcm_setkey(&g, k->key, (unsigned) tkt_keylen(k->cipher) * 8);
+        orc_gcm_setkey_ex(&g, k->key, (unsigned) tkt_keylen(k->cipher) * 8, tkt_bc(k->cipher));
         orc_gcm_encrypt(&g, iv, aad, TKT_AAD, data, len, data, tag, TKT_TAG);
     }
 }
@@ -65,13 +92,13 @@ static int tkt_open(const orc_ticket_key *k, const uint8_t *aad, uint8_t *data, 
     const uint8_t *iv = aad + TKT_NAME;
     if (k->cipher == ORC_CIPHER_CHACHA20_POLY1305)
         return orc_chachapoly_decrypt(k->key, iv, aad, TKT_AAD, data, len, data, tag);
-    if (k->cipher >= ORC_CIPHER_AES_128_CCM) {
+    if (tkt_is_ccm(k->cipher)) {
         orc_aes_ctx a;
-        orc_aes_setkey_enc(&a, k->key, (unsigned) tkt_keylen(k->cipher) * 8);
+        tkt_bc_setkey(&a, k->cipher, k->key);
         return orc_ccm_decrypt(&a, iv, aad, TKT_AAD, data, len, data, tag, TKT_TAG);
     }
     orc_gcm_ctx g;
-    orc_gcm_setkey(&g, k->key, (unsigned) tkt_keylen(k->cipher) * 8);
+    orc_gcm_setkey_ex(&g, k->key, (unsigned) tkt_keylen(k->cipher) * 8, tkt_bc(k->cipher));
     return orc_gcm_decrypt(&g, iv, aad, TKT_AAD, data, len, data, tag, TKT_TAG);
 }
 

@@ -16,7 +16,12 @@ import oracle as O  # noqa: E402
 from tests.prng import prng_bytes  # noqa: E402
 
 KEYSETS = [(M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305), (M.CIPHER_AES_128_GCM, M.CIPHER_AES_128_CCM),
-           (M.CIPHER_AES_256_CCM, M.CIPHER_AES_192_GCM)]
+           (M.CIPHER_AES_256_CCM, M.CIPHER_AES_192_GCM),
+           # every AEAD key type of mbedtls_ssl_ticket_setup (ssl_ticket.c:188-209), incl. the
+           # kernel's LDS-image variants: ARIA only, Camellia only, ARIA + Camellia, AES + Camellia
+           (M.CIPHER_ARIA_128_GCM, M.CIPHER_ARIA_256_CCM), (M.CIPHER_CAMELLIA_256_GCM, M.CIPHER_CAMELLIA_128_CCM),
+           (M.CIPHER_ARIA_192_GCM, M.CIPHER_CAMELLIA_192_GCM), (M.CIPHER_AES_128_GCM, M.CIPHER_CAMELLIA_256_CCM)]
+KEYSET_IDS = ["gcm256-chacha", "gcm128-ccm128", "ccm256-gcm192", "aria", "camellia", "aria-camellia", "aes-camellia"]
 
 
 def _setup(ciphers, seed):
@@ -36,7 +41,7 @@ def _arena(items, space_of):
     return offs, np.zeros(max(pos, 16), dtype=np.uint8)
 
 
-@pytest.mark.parametrize("ciphers", KEYSETS, ids=["gcm256-chacha", "gcm128-ccm128", "ccm256-gcm192"])
+@pytest.mark.parametrize("ciphers", KEYSETS, ids=KEYSET_IDS)
 def test_write_parse_batch(ciphers):
     okeys, kt = _setup(ciphers, 3)
     rng = np.random.default_rng(11)

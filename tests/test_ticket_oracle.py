@@ -5,9 +5,11 @@ import pytest
 
 import oracle as O
 from tests import _openssl as S
+from tests import test_camellia_oracle as CAM
 from tests.prng import prng_bytes
 
-KEYSETS = [(O.AES_256_GCM, O.CHACHA20_POLY1305), (O.AES_128_GCM, O.AES_128_CCM), (O.AES_256_CCM, O.AES_192_GCM)]
+KEYSETS = [(O.AES_256_GCM, O.CHACHA20_POLY1305), (O.AES_128_GCM, O.AES_128_CCM), (O.AES_256_CCM, O.AES_192_GCM),
+           (O.ARIA_128_GCM, O.ARIA_256_CCM), (O.CAMELLIA_256_GCM, O.CAMELLIA_128_CCM)]
 
 
 def _keys(ciphers, seed=1):
@@ -27,6 +29,14 @@ def test_write_vs_openssl_and_parse(ciphers, n):
             ct, tag = S.seal("chacha", k, iv, t[:18], st)
         elif c in (O.AES_128_CCM, O.AES_192_CCM, O.AES_256_CCM):
             ct, tag = S.ccm_seal(k, iv, t[:18], st, 16)
+        elif c in (O.ARIA_128_GCM, O.ARIA_192_GCM, O.ARIA_256_GCM):
+            ct, tag = S.seal("aria-gcm", k, iv, t[:18], st)
+        elif c in (O.ARIA_128_CCM, O.ARIA_192_CCM, O.ARIA_256_CCM):
+            ct, tag = S.ccm_seal(k, iv, t[:18], st, 16, name="aria-ccm")
+        elif c in (O.CAMELLIA_128_GCM, O.CAMELLIA_192_GCM, O.CAMELLIA_256_GCM):
+            ct, tag = CAM.gcm_ref(k, iv, t[:18], st)     # SP 800-38D over OpenSSL Camellia-ECB
+        elif c in (O.CAMELLIA_128_CCM, O.CAMELLIA_192_CCM, O.CAMELLIA_256_CCM):
+            ct, tag = CAM.ccm_ref(k, iv, t[:18], st)     # SP 800-38C over OpenSSL Camellia
         else:
             ct, tag = S.seal("gcm", k, iv, t[:18], st)
         assert t[18:] == ct + tag
