@@ -456,6 +456,98 @@ int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_out *stre
                           tlsrec_batch_res *res, uint32_t max_records, tlsrec_stream_out_res *sres,
                           uint32_t *nrecords, void *stream);
 
+/* ---- DTLS 1.2 datagram record layer (DTLS branch) -------
+ * The datagram-transport form of the same loops: received datagrams are
+ * split at their 13-byte DTLS record headers (plus conf->cid_len CID bytes
+ * for tls12_cid records) with the DTLS checks of ssl_parse_record_header
+ * (ssl_msg.c:3561-3776: datagram holds the record, epoch, anti-replay window
+ * :3248-3306), decrypted in place by the AEAD kernels, and ssl_get_next_record's
+ * datagram rules applied per connection in arrival order (ssl_msg.c:4727-4873:
+ * unexpected records skipped, a header error or a bad MAC drops the rest of
+ * the datagram, badmac_limit, ignore_unexpected_cid) together with
+ * ssl_prepare_record_content's DTLS post-rules (explicit sequence numbers, no
+ * in_ctr step, mbedtls_ssl_dtls_replay_update).  Send writes one record per
+ * mbedtls_ssl_write, each its own datagram (mbedtls_ssl_write_record,
+ * :2648-2793: FE FD, epoch + 48-bit sequence, out_cid).  DTLS 1.2 only (the
+ * reference has no DTLS 1.3): slots must hold TLS 1.2 keys. */
+#define TLSREC_ERR_SSL_UNEXPECTED_RECORD (-0x6700)   /* ssl.h:136 */
+#define TLSREC_ERR_SSL_EARLY_MESSAGE     (-0x6480)   /* ssl.h:146 */
+#define TLSREC_ERR_SSL_CONN_EOF          (-0x7280)   /* ssl.h:46 */
+/* MBEDTLS_SSL_IN_BUFFER_LEN / OUT_BUFFER_LEN of the AEAD-only build with DTLS
+ * connection IDs (ssl_misc.h:300-392): 13 + 16 + 16 + 16 + 16384 + 32.  A
+ * longer datagram is read truncated, as f_recv into that buffer would be. */
+#define TLSREC_DTLS_MAX_DATAGRAM   16477
+#define TLSREC_DTLS_OUT_BUFFER_LEN 16477
+/* record dispositions (besides 0 = accepted and the MBEDTLS_ERR_SSL_* code
+ * that skipped or dropped the record: UNEXPECTED_RECORD / EARLY_MESSAGE
+ * (other epoch or replayed; skipped), INVALID_MAC (datagram dropped),
+ * UNEXPECTED_CID (ignored), or the connection's fatal error) */
+#define TLSREC_DTLS_DROPPED     1    /* discarded with the rest of its datagram */
+#define TLSREC_DTLS_NOT_REACHED 2    /* after the connection's fatal error */
+#define TLSREC_DTLS_ANTI_REPLAY            1   /* conf->anti_replay */
+#define TLSREC_DTLS_IGNORE_UNEXPECTED_CID  2   /* conf->ignore_unexpected_cid */
+
+/* One received datagram (one f_recv result) in the arena. */
+typedef struct tlsrec_dgram {
+    uint64_t off;
+    uint32_t len;
+    uint32_t reserved;
+} tlsrec_dgram;
+
+/* One connection's receive state (the mbedtls_ssl_context / config fields the
+ * DTLS read loop uses) and its datagrams, in arrival order.  Datagram ranges
+ * of different connections must not overlap. */
+typedef struct tlsrec_dtls_in {
+    uint64_t window_top;     /* ssl->in_window_top */
+    uint64_t window;         /* ssl->in_window */
+    uint32_t first_dgram;    /* dgrams[first_dgram .. first_dgram + ndgram) */
+    uint32_t ndgram;
+    uint32_t slot;           /* key slot of transform_in (TLS 1.2 key) */
+    uint32_t badmac_seen;    /* ssl->badmac_seen */
+    uint32_t badmac_limit;   /* conf->badmac_limit, 0 = no limit */
+    uint16_t in_epoch;       /* ssl->in_epoch */
+    uint8_t  cid_len;        /* conf->cid_len: CID length of incoming tls12_cid records */
+    uint8_t  flags;          /* TLSREC_DTLS_ANTI_REPLAY | TLSREC_DTLS_IGNORE_UNEXPECTED_CID */
+    uint8_t  nb_zero;        /* ssl->nb_zero */
+    uint8_t  reserved[7];
+} tlsrec_dtls_in;
+
+typedef struct tlsrec_dtls_in_res {
+    uint64_t window_top;     /* state afterwards */
+    uint64_t window;
+    int32_t  status;         /* 0, or the fatal error mbedtls_ssl_read returns (processing stops) */
+    uint32_t first;          /* this connection's records are recs/res/disp[first .. first+nrec) */
+    uint32_t nrec;           /* records a header walk finds in its datagrams, in order */
+    uint32_t naccepted;      /* records with disposition 0: plaintext at
+                                arena + recs[k].buf_off + res[k].data_offset, res[k].data_len, res[k].type */
+    uint32_t dgrams_done;    /* datagrams fully processed before a fatal error */
+    uint32_t invalid_dgrams; /* datagrams cut short by a header error (INVALID_RECORD) */
+    uint32_t badmac_seen;
+    uint8_t  nb_zero;
+    uint8_t  reserved[3];
+} tlsrec_dtls_in_res;
+
+/* recs / res / disp: device arrays of max_records entries.  *nrecords (host,
+ * may be NULL) = records listed over all connections.  Records skipped or
+ * dropped keep unspecified bytes (the reference discards them too). */
+int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in *conns, uint32_t nconns,
+                        const tlsrec_dgram *dgrams, uint32_t ndgrams, uint8_t *arena, tlsrec_batch_rec *recs,
+                        tlsrec_batch_res *res, int32_t *disp, uint32_t max_records, tlsrec_dtls_in_res *cres,
+                        uint32_t *nrecords, void *stream);
+
+/* Bytes of datagrams `in_len` bytes of application data become under a TLS
+ * 1.2 key with an out_cid of cid_len bytes (0 for an unsupported suite). */
+uint64_t tlsrec_dtls_out_size(int cipher, uint32_t granularity, uint32_t cid_len, uint64_t in_len,
+                              uint32_t max_frag);
+/* tlsrec_stream_out with out_ctr = epoch (2 bytes) + 48-bit sequence number;
+ * record k of a connection is one datagram: its header starts at
+ * out_arena + recs[first + k].buf_off - 13 - cid_len and it is
+ * 13 + cid_len + res[first + k].data_len bytes long. */
+int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_out *streams, uint32_t nstreams,
+                        const uint8_t *in_arena, uint8_t *out_arena, tlsrec_batch_rec *recs,
+                        tlsrec_batch_res *res, uint32_t max_records, tlsrec_stream_out_res *sres,
+                        uint32_t *nrecords, void *stream);
+
 /* ---- session tickets (library/ssl_ticket.c) ------------
  * mbedtls_ssl_ticket_write / mbedtls_ssl_ticket_parse for a batch of tickets
  * in device memory.  Ticket = key_name[4] || iv[12] || len16 || state ||

@@ -15,7 +15,10 @@ from ._abi import (CIPHER_AES_128_GCM, CIPHER_AES_256_GCM, CIPHER_CHACHA20_POLY1
                    ERR_SSL_BAD_INPUT_DATA, ERR_SSL_BUFFER_TOO_SMALL, ERR_SSL_FEATURE_UNAVAILABLE,
                    ERR_SSL_HW_ACCEL_FAILED, ERR_SSL_INTERNAL_ERROR, ERR_SSL_INVALID_MAC,
                    ERR_SSL_INVALID_RECORD, ERR_SSL_UNEXPECTED_CID, MSG_APPLICATION_DATA, MSG_CID,
-                   CID_LEN_MAX, VERSION_TLS1_2, VERSION_TLS1_3,
+                   CID_LEN_MAX, VERSION_TLS1_2, VERSION_TLS1_3, ERR_SSL_COUNTER_WRAPPING,
+                   ERR_SSL_UNEXPECTED_RECORD, ERR_SSL_EARLY_MESSAGE, ERR_SSL_CONN_EOF, DTLS_MAX_DATAGRAM,
+                   DTLS_OUT_BUFFER_LEN, DTLS_DROPPED, DTLS_NOT_REACHED, DTLS_ANTI_REPLAY,
+                   DTLS_IGNORE_UNEXPECTED_CID,
                    BATCH_REC, BATCH_RES, KEY_MATERIAL, load)
 from .batch import (KeyTable, batch_decrypt, batch_encrypt, frame_check, host_batch, key_material,  # noqa: F401
                     records, results, seq_bytes)

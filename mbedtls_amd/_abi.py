@@ -26,6 +26,13 @@ ERR_SSL_INTERNAL_ERROR = -0x6C00
 ERR_SSL_UNEXPECTED_CID = -0x6000
 ERR_SSL_COUNTER_WRAPPING = -0x6B80
 ERR_SSL_SESSION_TICKET_EXPIRED = -0x6D80
+ERR_SSL_UNEXPECTED_RECORD = -0x6700
+ERR_SSL_EARLY_MESSAGE = -0x6480
+ERR_SSL_CONN_EOF = -0x7280
+DTLS_MAX_DATAGRAM = 16477
+DTLS_OUT_BUFFER_LEN = 16477
+DTLS_DROPPED, DTLS_NOT_REACHED = 1, 2
+DTLS_ANTI_REPLAY, DTLS_IGNORE_UNEXPECTED_CID = 1, 2
 MAX_IN_RECORD = 16421
 OUT_BUF_SPACE = 16416
 
@@ -75,6 +82,14 @@ assert TICKET.itemsize == 16 and TICKET_RES.itemsize == 16
 STREAM_READ_REQ = np.dtype([("out_off", "<u8"), ("out_cap", "<u4"), ("reserved", "<u4")])
 STREAM_READ_RES = np.dtype([("copied", "<u4"), ("records", "<u4"), ("left", "<u4"), ("reserved", "<u4")])
 assert STREAM_READ_REQ.itemsize == 16 and STREAM_READ_RES.itemsize == 16
+DGRAM = np.dtype([("off", "<u8"), ("len", "<u4"), ("reserved", "<u4")])
+DTLS_IN = np.dtype([("window_top", "<u8"), ("window", "<u8"), ("first_dgram", "<u4"), ("ndgram", "<u4"),
+                    ("slot", "<u4"), ("badmac_seen", "<u4"), ("badmac_limit", "<u4"), ("in_epoch", "<u2"),
+                    ("cid_len", "u1"), ("flags", "u1"), ("nb_zero", "u1"), ("reserved", "u1", 7)])
+DTLS_IN_RES = np.dtype([("window_top", "<u8"), ("window", "<u8"), ("status", "<i4"), ("first", "<u4"),
+                        ("nrec", "<u4"), ("naccepted", "<u4"), ("dgrams_done", "<u4"), ("invalid_dgrams", "<u4"),
+                        ("badmac_seen", "<u4"), ("nb_zero", "u1"), ("reserved", "u1", 3)])
+assert DGRAM.itemsize == 16 and DTLS_IN.itemsize == 48 and DTLS_IN_RES.itemsize == 48
 assert STREAM_IN.itemsize == 32 and STREAM_IN_RES.itemsize == 32
 assert STREAM_OUT.itemsize == 40 and STREAM_OUT_RES.itemsize == 32
 assert KEY_MATERIAL.itemsize == 64 and BATCH_REC.itemsize == 40 and BATCH_RES.itemsize == 16
@@ -146,6 +161,9 @@ SIGNATURES = {
     "tlsrec_stream_read": (_INT, [_VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "tlsrec_stream_out_size": (ctypes.c_uint64, [_INT, _INT, _U32, ctypes.c_uint64, _U32]),
     "tlsrec_stream_encrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
+    "tlsrec_dtls_decrypt": (_INT, [_VP, _VP, _U32, _VP, _U32, _VP, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
+    "tlsrec_dtls_out_size": (ctypes.c_uint64, [_INT, _U32, _U32, ctypes.c_uint64, _U32]),
+    "tlsrec_dtls_encrypt": (_INT, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     "tlsrec_version_string": (ctypes.c_char_p, []),
 }
 

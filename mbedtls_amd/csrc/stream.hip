@@ -163,6 +163,7 @@ __global__ void in_finish_kernel(const tlsrec_stream_in *s, uint32_t n, const ui
             res[first + k] = r;
         } else {
             if (r.status) { st = r.status; break; }
+            if (r.type < 20 || r.type > 23) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; }   /* type re-check :3914-3917 */
             if (r.data_len == 0) {                /* :3888-3906 */
                 if (minor == 3 && r.type != TLSREC_MSG_APPLICATION_DATA) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; }
                 if (++nbz > 3) { st = TLSREC_ERR_SSL_INVALID_MAC; break; }
@@ -372,6 +373,383 @@ __global__ void __launch_bounds__(256) read_kernel(const tlsrec_stream_in_res *s
     }
 }
 
+/* ---------------- DTLS 1.2 (datagram transport) ------------------------ */
+/* How a datagram's header walk ended (ssl_get_next_record / fetch_input). */
+enum DgStop : int32_t {
+    DG_END = 0,        /* every byte belongs to a record */
+    DG_INVALID = 1,    /* a header error: INVALID_RECORD, rest of the datagram dropped (:4790-4797) */
+    DG_TRAILING = 2,   /* 1..12 bytes after a record: fetch_input's INTERNAL_ERROR (:1921-1926) */
+    DG_EOF = 3         /* an empty datagram: f_recv returned 0, CONN_EOF (:1968-1970) */
+};
+
+struct DtlsHdr {
+    uint32_t pos, data_offset, data_len, cid_len;
+};
+
+/* mbedtls_ssl_read_version, datagram transport (ssl_msg.c:6215-6228) */
+__device__ __forceinline__ uint32_t read_version_dtls(uint32_t a, uint32_t b)
+{
+    const uint32_t w = (a << 8) | b;
+    return (uint16_t) ~(w - (w == 0xfeffu ? 0x0202u : 0x0201u));
+}
+
+__device__ __forceinline__ uint32_t dgram_len(const tlsrec_dgram &d)
+{
+    return d.len < TLSREC_DTLS_MAX_DATAGRAM ? d.len : (uint32_t) TLSREC_DTLS_MAX_DATAGRAM;   /* f_recv truncates */
+}
+
+/* The records of one datagram, walked with the header checks of
+ * ssl_parse_record_header that decide where a record ends (:3591-3753; type
+ * :3529-3539 or a tls12_cid header of conf->cid_len bytes :3616-3649, version
+ * <= TLS 1.2, data_len != 0, the datagram holds the record); f(h, header) per
+ * record. */
+template <typename F>
+__device__ int32_t dtls_walk(const uint8_t *b, uint32_t len, uint32_t cid_conf, F f)
+{
+    if (len == 0) return DG_EOF;
+    uint32_t pos = 0;
+    while (pos < len) {
+        const uint32_t rem = len - pos;
+        if (rem < 13) return pos == 0 ? DG_INVALID : DG_TRAILING;
+        const uint8_t *h = b + pos;
+        const uint32_t type = h[0];
+        uint32_t lo = 11, cid = 0;
+        if (cid_conf != 0 && type == TLSREC_MSG_CID) {
+            lo += cid_conf;
+            if (rem < lo + 2) return DG_INVALID;
+            cid = cid_conf;
+        } else if (type < 20 || type > 23) {
+            return DG_INVALID;
+        }
+        if (read_version_dtls(h[1], h[2]) > 0x0303u) return DG_INVALID;     /* max_tls_version, ssl_tls.c:5514-5517 */
+        const uint32_t dlen = ((uint32_t) h[lo] << 8) | h[lo + 1];
+        if (dlen == 0) return DG_INVALID;
+        if (rem < lo + 2 + dlen) return DG_INVALID;
+        const DtlsHdr d = { pos, lo + 2, dlen, cid };
+        f(d, h);
+        pos += lo + 2 + dlen;
+    }
+    return DG_END;
+}
+
+/* the anti-replay window (mbedtls_ssl_dtls_replay_check / _update, ssl_msg.c:3248-3306) */
+struct ReplayWindow {
+    uint64_t top, bits;
+    bool on;
+
+    __device__ __forceinline__ static uint64_t seq48(const uint8_t *ctr)
+    {
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 2; k < 8; k++) v = (v << 8) | ctr[k];
+        return v;
+    }
+    __device__ __forceinline__ bool fresh(const uint8_t *ctr) const
+    {
+        const uint64_t s = seq48(ctr);
+        if (!on || s > top) return true;
+        const uint64_t bit = top - s;
+        return bit < 64 && !((bits >> bit) & 1);
+    }
+    __device__ __forceinline__ void update(const uint8_t *ctr)
+    {
+        if (!on) return;
+        const uint64_t s = seq48(ctr);
+        if (s > top) {
+            const uint64_t shift = s - top;
+            bits = shift >= 64 ? 1 : ((bits << shift) | 1);
+            top = s;
+        } else if (top - s < 64) {
+            bits |= (uint64_t) 1 << (top - s);
+        }
+    }
+};
+
+__device__ __forceinline__ bool dtls_conn_ok(const tlsrec_dtls_in &c, uint32_t ndg, const SlotState *slots,
+                                             uint32_t cap)
+{
+    return slot_minor(slots, cap, c.slot) == 3 && c.first_dgram <= ndg && c.ndgram <= ndg - c.first_dgram &&
+           c.cid_len <= TLSREC_CID_LEN_MAX;
+}
+
+__global__ void dtls_count_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
+                                  const uint8_t *arena, const SlotState *slots, uint32_t cap, uint32_t *counts)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        counts[n] = 0;
+        return;
+    }
+    const tlsrec_dtls_in ci = c[i];
+    uint32_t cnt = 0;
+    if (dtls_conn_ok(ci, ndg, slots, cap))
+        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++)
+            dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &, const uint8_t *) { cnt++; });
+    counts[i] = cnt;
+}
+
+/* One descriptor per record.  A record is decrypted when its epoch matches
+ * and the window the connection arrived with does not reject it: the window
+ * only ever gains records, so every record the in-order pass will accept is
+ * among them (replayed copies of a record that then fails its MAC included). */
+__global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
+                                 const uint8_t *arena, const uint32_t *offs, const SlotState *slots, uint32_t cap,
+                                 tlsrec_batch_rec *recs)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tlsrec_dtls_in ci = c[i];
+    if (!dtls_conn_ok(ci, ndg, slots, cap)) return;
+    const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
+    uint32_t k = offs[i];
+    for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++) {
+        const uint64_t base = dg[d].off;
+        dtls_walk(arena + base, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &h, const uint8_t *p) {
+            tlsrec_batch_rec r;
+            memset(&r, 0, sizeof(r));
+            r.buf_off = base + h.pos;                  /* rec->buf = the header (:3715-3716) */
+            r.buf_len = h.data_offset + h.data_len;
+            r.data_offset = h.data_offset;
+            r.data_len = h.data_len;
+            memcpy(r.ctr, p + 3, 8);                   /* explicit epoch + sequence number (:3683-3687) */
+            r.type = p[0];
+            r.ver[0] = p[1];
+            r.ver[1] = p[2];
+            r.cid_len = (uint8_t) h.cid_len;
+            r.cid_off[0] = 11;                         /* the CID follows the sequence number */
+            const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
+            r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
+            recs[k++] = r;
+        });
+    }
+}
+
+/* ssl_get_next_record over each connection's datagrams in arrival order, on
+ * the decrypt results (one lane per connection). */
+__global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
+                                   const uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
+                                   const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
+                                   const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tlsrec_dtls_in ci = c[i];
+    ReplayWindow w = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
+    const bool ignore_cid = (ci.flags & TLSREC_DTLS_IGNORE_UNEXPECTED_CID) != 0;
+    uint32_t nbz = ci.nb_zero, bms = ci.badmac_seen, nacc = 0, done = 0, inval = 0;
+    const uint32_t first = offs[i];
+    uint32_t k = first;
+    int32_t st = 0;
+    if (!dtls_conn_ok(ci, ndg, slots, cap)) {
+        st = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    } else {
+        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++) {
+            bool dropped = false;
+            const int32_t stop = dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len,
+                                           [&](const DtlsHdr &, const uint8_t *p) {
+                const uint32_t kk = k++;
+                if (st) { disp[kk] = TLSREC_DTLS_NOT_REACHED; return; }
+                if (dropped) { disp[kk] = TLSREC_DTLS_DROPPED; return; }
+                const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
+                if (epoch != ci.in_epoch) {            /* :3755-3768, skipped after the handshake (:4727-4800) */
+                    disp[kk] = epoch == (uint32_t) ci.in_epoch + 1 ? TLSREC_ERR_SSL_EARLY_MESSAGE
+                                                                   : TLSREC_ERR_SSL_UNEXPECTED_RECORD;
+                    return;
+                }
+                if (!w.fresh(p + 3)) { disp[kk] = TLSREC_ERR_SSL_UNEXPECTED_RECORD; return; }   /* :3769-3776 */
+                if (recs[kk].slot == NO_SLOT) {        /* not decrypted: impossible, the window only grows */
+                    st = TLSREC_ERR_SSL_INTERNAL_ERROR;
+                    disp[kk] = st;
+                    return;
+                }
+                const tlsrec_batch_res r = res[kk];
+                int32_t e = r.status;                  /* ssl_prepare_record_content (:3810-4017) */
+                if (e == TLSREC_ERR_SSL_UNEXPECTED_CID && ignore_cid) { disp[kk] = e; return; }   /* :3872-3879 */
+                if (e == 0) {
+                    if (r.type < 20 || r.type > 23) {  /* :3914-3917 */
+                        e = TLSREC_ERR_SSL_INVALID_RECORD;
+                    } else if (r.data_len == 0) {      /* :3920-3941 */
+                        if (r.type != TLSREC_MSG_APPLICATION_DATA) e = TLSREC_ERR_SSL_INVALID_RECORD;
+                        else if (++nbz > 3) e = TLSREC_ERR_SSL_INVALID_MAC;
+                    } else {
+                        nbz = 0;
+                    }
+                }
+                if (e == 0) {
+                    w.update(p + 3);                   /* mbedtls_ssl_dtls_replay_update (:4003-4007) */
+                    if (r.data_len > 16384) e = TLSREC_ERR_SSL_INVALID_RECORD;   /* :4011-4014 */
+                }
+                disp[kk] = e;
+                if (e == TLSREC_ERR_SSL_INVALID_MAC) { /* :4837-4873 */
+                    if (ci.badmac_limit != 0 && ++bms >= ci.badmac_limit) st = e;
+                    else dropped = true;
+                } else if (e) {
+                    st = e;
+                } else {
+                    nacc++;
+                }
+            });
+            if (!st && !dropped) {
+                if (stop == DG_INVALID) inval++;
+                else if (stop == DG_TRAILING) st = TLSREC_ERR_SSL_INTERNAL_ERROR;
+                else if (stop == DG_EOF) st = TLSREC_ERR_SSL_CONN_EOF;
+            }
+            if (!st) done++;
+        }
+    }
+    tlsrec_dtls_in_res o;
+    memset(&o, 0, sizeof(o));
+    o.window_top = w.top;
+    o.window = w.bits;
+    o.status = st;
+    o.first = first;
+    o.nrec = counts[i];
+    o.naccepted = nacc;
+    o.dgrams_done = done;
+    o.invalid_dgrams = inval;
+    o.badmac_seen = bms;
+    o.nb_zero = (uint8_t) nbz;
+    cres[i] = o;
+}
+
+/* send: one record per datagram */
+__device__ __forceinline__ uint32_t dtls_cid_of(const SlotState *slots, uint32_t slot) { return slots[slot].cid_len; }
+
+/* protected length of an n-byte record under a TLS 1.2 key (DTLSInnerPlaintext with a CID, :874-897) */
+__device__ __forceinline__ uint32_t dtls_body(const OutShape &o, uint32_t cid, uint32_t n)
+{
+    if (cid) {
+        const uint32_t inner = n + 1;
+        return o.head + inner + (o.gran - inner % o.gran) % o.gran + o.tag;
+    }
+    return o.head + n + o.tag;
+}
+
+__global__ void dtls_out_count_kernel(const tlsrec_stream_out *s, uint32_t n, const SlotState *slots, uint32_t cap,
+                                      uint32_t *counts)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        counts[n] = 0;
+        return;
+    }
+    const uint32_t f = frag_of(s[i]);
+    const OutShape sh = out_shape(slots, cap, s[i].slot);
+    counts[i] = (sh.ok && !sh.tls13) ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
+}
+
+__device__ __forceinline__ void dtls_seq(uint8_t ctr[8], const uint8_t base[8], uint64_t k)
+{
+    const uint64_t s = (ReplayWindow::seq48(base) + k) & 0xFFFFFFFFFFFFull;
+    ctr[0] = base[0];
+    ctr[1] = base[1];
+#pragma unroll
+    for (int b = 7; b >= 2; b--) ctr[b] = (uint8_t) (s >> (8 * (7 - b)));
+}
+
+/* One wave per record: the DTLS header (type after encryption, FE FD, epoch +
+ * sequence, out_cid, protected length; mbedtls_ssl_write_record :2669-2727),
+ * the descriptor, and the plaintext copied behind the header. */
+__global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream_out *s, uint32_t n,
+                                                             const uint32_t *offs, uint32_t total,
+                                                             const SlotState *slots, uint32_t cap, const uint8_t *in,
+                                                             uint8_t *out, tlsrec_batch_rec *recs)
+{
+    const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= total) return;
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (offs[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t i = lo;
+    const tlsrec_stream_out si = s[i];
+    const uint32_t k = j - offs[i];
+    const uint32_t f = frag_of(si);
+    const OutShape sh = out_shape(slots, cap, si.slot);
+    const uint32_t cid = dtls_cid_of(slots, si.slot), hdr = 13 + cid;
+    const uint64_t src_off = (uint64_t) k * f;
+    const uint64_t left = (uint64_t) si.in_len - src_off;
+    const uint32_t len = left < f ? (uint32_t) left : f;
+    const uint64_t pos = si.out_off + (uint64_t) k * (hdr + dtls_body(sh, cid, f));
+    const uint8_t *src = in + si.in_off + src_off;
+    uint8_t *dst = out + pos + hdr + sh.head;
+    const uint32_t nv = len / 16;
+    for (uint32_t v = lane; v < nv; v += 64) {
+        uint4 w;
+        __builtin_memcpy(&w, src + 16 * v, 16);
+        __builtin_memcpy(dst + 16 * v, &w, 16);
+    }
+    for (uint32_t b = nv * 16 + lane; b < len; b += 64) dst[b] = src[b];
+    if (lane == 0) {
+        const uint32_t body = dtls_body(sh, cid, len);
+        uint8_t *h = out + pos;
+        tlsrec_batch_rec d;
+        memset(&d, 0, sizeof(d));
+        dtls_seq(d.ctr, si.out_ctr, k);
+        h[0] = cid ? (uint8_t) TLSREC_MSG_CID : si.type;     /* the type encrypt_buf leaves (:2727) */
+        h[1] = 0xfe;                                          /* mbedtls_ssl_write_version, DTLS 1.2 */
+        h[2] = 0xfd;
+        memcpy(h + 3, d.ctr, 8);
+        memcpy(h + 11, slots[si.slot].cid, cid);              /* out_cid (:2712-2714) */
+        h[11 + cid] = (uint8_t) (body >> 8);
+        h[12 + cid] = (uint8_t) body;
+        d.buf_off = pos + hdr;                                /* rec.buf = out_iv */
+        d.buf_len = TLSREC_DTLS_OUT_BUFFER_LEN - hdr;         /* out_buf_len - (out_iv - out_buf) */
+        d.data_offset = sh.head;
+        d.data_len = len;
+        d.slot = si.slot;
+        d.type = si.type;
+        d.ver[0] = 0xfe;
+        d.ver[1] = 0xfd;
+        recs[j] = d;
+    }
+}
+
+__global__ void dtls_out_finish_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs,
+                                       const uint32_t *counts, const SlotState *slots, uint32_t cap,
+                                       const tlsrec_batch_res *res, tlsrec_stream_out_res *sres)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tlsrec_stream_out si = s[i];
+    const OutShape sh = out_shape(slots, cap, si.slot);
+    int32_t st = (sh.ok && !sh.tls13) || si.in_len == 0 ? 0 : TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    const uint32_t cid = sh.ok ? dtls_cid_of(slots, si.slot) : 0, f = frag_of(si);
+    uint8_t ctr[8];
+    memcpy(ctr, si.out_ctr, 8);
+    uint32_t nrec = 0, olen = 0;
+    const uint32_t first = offs[i], cnt = counts[i];
+    for (uint32_t k = 0; k < cnt && st == 0; k++) {
+        const tlsrec_batch_res &r = res[first + k];
+        if (r.status) { st = r.status; break; }
+        const uint64_t left = (uint64_t) si.in_len - (uint64_t) k * f;
+        const uint32_t len = left < f ? (uint32_t) left : f;
+        if (r.data_offset != 0 || r.data_len != dtls_body(sh, cid, len)) {          /* :2697-2700 */
+            st = TLSREC_ERR_SSL_INTERNAL_ERROR;
+            break;
+        }
+        olen += 13 + cid + r.data_len;
+        nrec++;
+        int b;                                                 /* :2741-2756, ep_len = 2 */
+        for (b = 8; b > 2; b--)
+            if (++ctr[b - 1] != 0) break;
+        if (b == 2) st = TLSREC_ERR_SSL_COUNTER_WRAPPING;
+    }
+    tlsrec_stream_out_res o;
+    memset(&o, 0, sizeof(o));
+    o.status = st;
+    o.first = first;
+    o.nrec = nrec;
+    o.out_len = olen;
+    memcpy(o.out_ctr, ctr, 8);
+    o.nparsed = cnt;
+    sres[i] = o;
+}
+
 } /* namespace tlsst */
 
 using namespace tlsst;
@@ -521,4 +899,98 @@ extern "C" int tlsrec_stream_read(const tlsrec_stream_in_res *sres, uint32_t nst
     hipLaunchKernelGGL(read_kernel, dim3(nstreams), dim3(256), 0, (hipStream_t) stream, sres, nstreams, recs, res,
                        arena, req, out_arena, rres);
     return hipGetLastError() == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+}
+
+/* ---------------- DTLS host side ---------------------------------------- */
+extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in *conns, uint32_t nconns,
+                                   const tlsrec_dgram *dgrams, uint32_t ndgrams, uint8_t *arena,
+                                   tlsrec_batch_rec *recs, tlsrec_batch_res *res, int32_t *disp,
+                                   uint32_t max_records, tlsrec_dtls_in_res *cres, uint32_t *nrecords, void *stream)
+{
+    if (nrecords) *nrecords = 0;
+    if (!kt || (nconns && (!conns || !cres || (ndgrams && (!dgrams || !arena))))) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (nconns == 0) return 0;
+    hipStream_t st = (hipStream_t) stream;
+    const SlotState *slots = tlsrec__keytab_slots(kt);
+    const uint32_t cap = tlsrec_keytab_capacity(kt);
+    Scratch sc;
+    int r = scratch_alloc(sc, nconns, st);
+    uint32_t total = 0;
+    if (r == 0) {
+        hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                           ndgrams, (const uint8_t *) arena, slots, cap, sc.counts);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
+    if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (r == 0 && total) {
+        hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                           ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) r = tlsrec_batch_decrypt(kt, recs, res, total, arena, arena, 0, stream);
+    }
+    if (r == 0) {
+        hipLaunchKernelGGL(dtls_finish_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                           ndgrams, (const uint8_t *) arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    tlsrec__scratch_release(&sc.lease);
+    if (r == 0 && nrecords) *nrecords = total;
+    return r;
+}
+
+extern "C" uint64_t tlsrec_dtls_out_size(int cipher, uint32_t granularity, uint32_t cid_len, uint64_t in_len,
+                                         uint32_t max_frag)
+{
+    if (tlsrec_cipher_keylen(cipher) == 0 || cid_len > TLSREC_CID_LEN_MAX) return 0;
+    const uint64_t tag = tlsrec_cipher_taglen(cipher);
+    const uint64_t f = max_frag ? max_frag : 16384;
+    const uint64_t g = granularity ? granularity : 16;
+    const uint64_t head = cipher != TLSREC_CIPHER_CHACHA20_POLY1305 ? 8 : 0;
+    auto body = [&](uint64_t n) -> uint64_t {
+        if (cid_len) {
+            const uint64_t inner = n + 1;
+            return head + inner + (g - inner % g) % g + tag;
+        }
+        return head + n + tag;
+    };
+    const uint64_t full = in_len / f, rest = in_len % f;
+    return full * (13 + cid_len + body(f)) + (rest ? 13 + cid_len + body(rest) : 0);
+}
+
+extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_out *streams, uint32_t nstreams,
+                                   const uint8_t *in_arena, uint8_t *out_arena, tlsrec_batch_rec *recs,
+                                   tlsrec_batch_res *res, uint32_t max_records, tlsrec_stream_out_res *sres,
+                                   uint32_t *nrecords, void *stream)
+{
+    if (nrecords) *nrecords = 0;
+    if (!kt || (nstreams && (!streams || !in_arena || !out_arena || !sres))) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (nstreams == 0) return 0;
+    hipStream_t st = (hipStream_t) stream;
+    const SlotState *slots = tlsrec__keytab_slots(kt);
+    const uint32_t cap = tlsrec_keytab_capacity(kt);
+    Scratch sc;
+    int r = scratch_alloc(sc, nstreams, st);
+    uint32_t total = 0;
+    if (r == 0) {
+        hipLaunchKernelGGL(dtls_out_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
+                           slots, cap, sc.counts);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
+    if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (r == 0 && total) {
+        hipLaunchKernelGGL(dtls_out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
+                           total, slots, cap, in_arena, out_arena, recs);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0) r = tlsrec_batch_encrypt(kt, recs, res, total, out_arena, out_arena, 0, stream);
+    }
+    if (r == 0) {
+        hipLaunchKernelGGL(dtls_out_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
+                           sc.offs, sc.counts, slots, cap, res, sres);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    }
+    tlsrec__scratch_release(&sc.lease);
+    if (r == 0 && nrecords) *nrecords = total;
+    return r;
 }

@@ -466,6 +466,94 @@ def stream_encrypt(t: "Transform", pt: bytes, rtype: int = 23, out_ctr: bytes = 
     return r, out.raw[:olen.value], nrec.value, bytes(ctr)
 
 
+# ---- DTLS 1.2 datagram record loops (oracle/dtls.c) ------------------------------
+ERR_UNEXPECTED_RECORD = -0x6700
+ERR_EARLY_MESSAGE = -0x6480
+ERR_CONN_EOF = -0x7280
+DTLS_MAX_DATAGRAM = 16477
+DTLS_DROPPED, DTLS_NOT_REACHED = 1, 2
+
+
+class DtlsState(ctypes.Structure):
+    """The mbedtls_ssl_context / config fields of the DTLS read loop."""
+    _fields_ = [("window_top", ctypes.c_uint64), ("window", ctypes.c_uint64), ("badmac_seen", ctypes.c_uint32),
+                ("badmac_limit", ctypes.c_uint32), ("in_epoch", ctypes.c_uint16), ("cid_len", ctypes.c_uint8),
+                ("anti_replay", ctypes.c_uint8), ("ignore_unexpected_cid", ctypes.c_uint8),
+                ("nb_zero", ctypes.c_uint8)]
+
+
+class _DtlsRec(ctypes.Structure):
+    _fields_ = [("dgram", ctypes.c_uint32), ("off", ctypes.c_uint32), ("data_offset", ctypes.c_uint32),
+                ("data_len", ctypes.c_uint32), ("disp", ctypes.c_int32), ("type", ctypes.c_uint8)]
+
+
+class _DtlsRes(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("nrec", ctypes.c_uint32), ("naccepted", ctypes.c_uint32),
+                ("dgrams_done", ctypes.c_uint32), ("invalid_dgrams", ctypes.c_uint32)]
+
+
+def dtls_replay_check(st: DtlsState, ctr: bytes) -> int:
+    f = lib().orc_dtls_replay_check
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    f.restype = ctypes.c_int
+    return f(ctypes.byref(st), bytes(ctr))
+
+
+def dtls_replay_update(st: DtlsState, ctr: bytes) -> None:
+    f = lib().orc_dtls_replay_update
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    f.restype = None
+    f(ctypes.byref(st), bytes(ctr))
+
+
+def dtls_decrypt(t: "Transform", st: DtlsState, datagrams):
+    """One connection's datagrams (list of bytes), in arrival order.  `st` is
+    updated in place.  Returns (res dict, [(dgram, off, data_offset,
+    data_len, disp, type)], [datagram bytes after])."""
+    offs, pos = [], 0
+    for d in datagrams:
+        offs.append(pos)
+        pos += len(d)
+    buf = ctypes.create_string_buffer(b"".join(datagrams), max(1, pos))
+    cap = pos // 13 + 1
+    recs = (_DtlsRec * cap)()
+    res = _DtlsRes()
+    doff = (ctypes.c_uint64 * max(1, len(datagrams)))(*offs)
+    dlen = (ctypes.c_uint32 * max(1, len(datagrams)))(*[len(d) for d in datagrams])
+    f = lib().orc_dtls_decrypt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _S,
+                  ctypes.c_void_p, _S, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    f(t._mem, ctypes.byref(st), buf, doff, dlen, len(datagrams), recs, cap, ctypes.byref(res))
+    out = [(r.dgram, r.off, r.data_offset, r.data_len, r.disp, r.type) for r in recs[:res.nrec]]
+    raw = buf.raw
+    return ({"status": res.status, "nrec": res.nrec, "naccepted": res.naccepted, "dgrams_done": res.dgrams_done,
+             "invalid_dgrams": res.invalid_dgrams}, out,
+            [raw[o:o + len(d)] for o, d in zip(offs, datagrams)])
+
+
+def dtls_record_wire(t: "Transform", n: int) -> int:
+    f = lib().orc_dtls_record_wire
+    f.argtypes = [ctypes.c_void_p, _S]
+    f.restype = _S
+    return f(t._mem, n)
+
+
+def dtls_encrypt(t: "Transform", pt: bytes, rtype: int = 23, out_ctr: bytes = bytes(8), max_frag: int = 16384):
+    """Returns (status, datagrams back to back, records, out_ctr after)."""
+    cap = sum(dtls_record_wire(t, min(max_frag, len(pt) - o)) for o in range(0, len(pt), max_frag)) + 16
+    out = ctypes.create_string_buffer(cap)
+    ctr = (ctypes.c_uint8 * 8)(*out_ctr)
+    olen = _S()
+    nrec = ctypes.c_uint32()
+    f = lib().orc_dtls_encrypt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, _S, ctypes.c_uint8, ctypes.c_void_p, _S, ctypes.c_void_p, _S,
+                  ctypes.c_void_p, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    r = f(t._mem, bytes(pt), len(pt), rtype, ctr, max_frag, out, cap, ctypes.byref(olen), ctypes.byref(nrec))
+    return r, out.raw[:olen.value], nrec.value, bytes(ctr)
+
+
 # ---- session tickets (oracle/ticket.c) -------------------------------------------
 ERR_SESSION_TICKET_EXPIRED = -0x6D80
 

@@ -275,6 +275,54 @@ int orc_stream_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, ui
                        size_t max_frag, size_t out_buf_space, uint8_t *out, size_t out_cap, size_t *out_len,
                        uint32_t *nrec);
 
+/* ---- DTLS 1.2 datagram record loops (oracle/dtls.c) ---------------------- */
+#define ORC_ERR_SSL_UNEXPECTED_RECORD (-0x6700)  /* ssl.h:136 */
+#define ORC_ERR_SSL_EARLY_MESSAGE     (-0x6480)  /* ssl.h:146 */
+#define ORC_ERR_SSL_CONN_EOF          (-0x7280)  /* ssl.h:46 */
+/* MBEDTLS_SSL_IN_BUFFER_LEN / OUT_BUFFER_LEN of the AEAD-only build with DTLS
+ * connection IDs (ssl_misc.h:300-392): 13 + (16 IV + 16 tag + 16 CID
+ * padding + 16384) + 32 CID; in_hdr = in_buf for DTLS (ssl_msg.c:5264-5266) */
+#define ORC_DTLS_MAX_DATAGRAM   16477
+#define ORC_DTLS_OUT_BUFFER_LEN 16477
+/* record dispositions besides 0 (accepted) and the MBEDTLS_ERR_SSL_* code that
+ * skipped or dropped the record */
+#define ORC_DTLS_DROPPED     1   /* discarded with the rest of its datagram */
+#define ORC_DTLS_NOT_REACHED 2   /* after the connection's fatal error */
+
+/* the mbedtls_ssl_context / config fields the DTLS read loop uses */
+typedef struct {
+    uint64_t window_top, window;      /* in_window_top / in_window (anti-replay) */
+    uint32_t badmac_seen, badmac_limit;
+    uint16_t in_epoch;
+    uint8_t cid_len;                  /* conf->cid_len: CID length of incoming tls12_cid records */
+    uint8_t anti_replay;              /* conf->anti_replay */
+    uint8_t ignore_unexpected_cid;    /* conf->ignore_unexpected_cid */
+    uint8_t nb_zero;
+} orc_dtls_state;
+
+typedef struct {
+    uint32_t dgram, off;              /* datagram index, header offset in it */
+    uint32_t data_offset, data_len;   /* rec fields after processing (offset from the header) */
+    int32_t disp;
+    uint8_t type;
+} orc_dtls_rec;
+
+typedef struct {
+    int32_t status;                   /* the fatal error mbedtls_ssl_read returns, 0 = none */
+    uint32_t nrec;                    /* records listed (every record a header walk finds) */
+    uint32_t naccepted;
+    uint32_t dgrams_done;             /* datagrams processed before a fatal error */
+    uint32_t invalid_dgrams;          /* datagrams cut short by a header error */
+} orc_dtls_res;
+
+int orc_dtls_replay_check(const orc_dtls_state *st, const uint8_t ctr[8]);
+void orc_dtls_replay_update(orc_dtls_state *st, const uint8_t ctr[8]);
+int orc_dtls_decrypt(const orc_transform *t, orc_dtls_state *st, uint8_t *buf, const uint64_t *doff,
+                     const uint32_t *dlen, size_t nd, orc_dtls_rec *out, size_t max_out, orc_dtls_res *res);
+size_t orc_dtls_record_wire(const orc_transform *t, size_t n);
+int orc_dtls_encrypt(const orc_transform *t, const uint8_t *pt, size_t len, uint8_t type, uint8_t out_ctr[8],
+                     size_t max_frag, uint8_t *out, size_t out_cap, size_t *out_len, uint32_t *nrec);
+
 /* ---- session tickets (oracle/ticket.c) ----------------------------------- */
 #define ORC_ERR_SSL_SESSION_TICKET_EXPIRED (-0x6D80)   /* ssl.h:111 */
 typedef struct {

@@ -80,6 +80,12 @@ int orc_stream_decrypt(const orc_transform *t, uint8_t *buf, size_t len, const u
                 res->status = r;
                 break;
             }
+            /* the content type may change in decryption (TLS 1.3 / CID inner
+             * plaintext): re-checked, fatal this time (ssl_msg.c:3914-3917) */
+            if (rec.type != 20 && rec.type != 21 && rec.type != 22 && rec.type != 23) {
+                res->status = ORC_ERR_SSL_INVALID_RECORD;
+                break;
+            }
             if (rec.data_len == 0) {
                 if (t->tls_version == ORC_VERSION_TLS1_2 && rec.type != 23) {
                     res->status = ORC_ERR_SSL_INVALID_RECORD;

@@ -161,6 +161,17 @@ def _empty_record(t, ctr):
     return bytes([23, 3, 3]) + rec.data_len.to_bytes(2, "big") + rec.data()
 
 
+def _typed_record(t, ctr, typ):
+    """a record whose (TLS 1.3: inner) content type is `typ`; after
+    decryption ssl_prepare_record_content re-checks it (ssl_msg.c:3914-3917)"""
+    buf = bytearray(128)
+    head = 8 if (t.tls_version == O.TLS1_2 and t.cipher != O.CHACHA20_POLY1305) else 0
+    buf[head:head + 5] = b"hello"
+    rec = O.Record(ctr=ctr.to_bytes(8, "big"), type=typ, ver=b"\x03\x03", buf=buf, data_offset=head, data_len=5)
+    assert t.encrypt_buf(rec) == 0 and rec.data_offset == 0
+    return bytes([rec.type, 3, 3]) + rec.data_len.to_bytes(2, "big") + rec.data()
+
+
 def test_stop_conditions_match_oracle():
     slots = [(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, prng_bytes(1, 32), prng_bytes(2, 12), 0),
              (M.CIPHER_AES_128_GCM, M.VERSION_TLS1_2, prng_bytes(3, 16), prng_bytes(4, 12), 0),
@@ -180,7 +191,8 @@ def test_stop_conditions_match_oracle():
                   (slot, bytes([20, 3, 3, 0, 1, 1]) + w, 0, 0),                           # CCS first
                   (slot, b"".join(_empty_record(t, k) for k in range(4)), 0, 0),          # 4 empty
                   (slot, b"".join(_empty_record(t, k) for k in range(2)), 0, 2),          # nb_zero carried
-                  (slot, _empty_record(t, (1 << 64) - 1), (1 << 64) - 1, 0)]              # ctr wrap
+                  (slot, _empty_record(t, (1 << 64) - 1), (1 << 64) - 1, 0),              # ctr wrap
+                  (slot, _typed_record(t, 0, 24) + w, 0, 0)]                              # inner type 24
     a, recs, res, sres, offs = c.decrypt(conns)
     for i, (slot, data, ctr, nbz) in enumerate(conns):
         want, wrecs, _ = O.stream_decrypt(c.ot[slot], data, ctr.to_bytes(8, "big"), nbz)
