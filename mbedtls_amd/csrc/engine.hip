@@ -55,7 +55,7 @@ extern "C" const char *tlsrec_version_string(void)
 {
     return "tlsrec 0.2 gfx950: aes-128/192/256-gcm(L=4/8/16/64, T-tables in LDS, GHASH 4-bit position tables) "
            "aes-ccm/ccm_8(lane per record) chacha20-poly1305(L=1/2/4/8, 26-bit limbs) "
-           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer aria-128/192/256-gcm/ccm camellia-128/192/256-gcm/ccm dtls1.2-cid";
+           "tls13-key-schedule(hkdf-sha256/384) stream-record-layer aria-128/192/256-gcm/ccm camellia-128/192/256-gcm/ccm dtls1.2-cid dtls1.2-datagram-record-layer(anti-replay) session-tickets";
 }
 
 extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
@@ -233,6 +233,13 @@ static int gcm_wp_env(void)
     return e ? atoi(e) : -1;
 }
 
+/* lanes per GCM record when the caller passes 0 (auto): measurement override */
+static uint32_t gcm_lanes_env(void)
+{
+    const char *e = getenv("TLSREC_GCM_LANES");
+    return e ? (uint32_t) atoi(e) : 0u;
+}
+
 static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t target_wgs)
 {
     uint64_t want = (n + (uint64_t) waves_per_wg * target_wgs - 1) / ((uint64_t) waves_per_wg * target_wgs);
@@ -382,6 +389,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     int rc = 0;
     static const int gcm_ciphers[3] = { TLSREC_CIPHER_AES_128_GCM, TLSREC_CIPHER_AES_256_GCM,
                                         TLSREC_CIPHER_AES_192_GCM };
+    const uint32_t lanes_in = lanes;
+    if (!lanes) lanes = gcm_lanes_env();
     for (int ci = 0; ci < 3 && !rc; ci++) {
         const int cipher = gcm_ciphers[ci];     /* bucket class ci: keys [ci * cap, (ci + 1) * cap) */
         if (!(cmask & (1u << cipher))) continue;
@@ -481,7 +490,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         /* 2 lanes per record, more when the batch would not fill the chip
          * (cu x 8 resident waves: 2 per SIMD) */
         const uint64_t rpwave = (uint64_t) n / ((uint64_t) cu * 8);
-        int L = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8) ? (int) lanes
+        int L = (lanes_in == 1 || lanes_in == 2 || lanes_in == 4 || lanes_in == 8) ? (int) lanes_in
                 : (rpwave >= 32 ? 2 : (rpwave >= 16 ? 4 : 8));
         if (kt->has_cid) L = 2;     /* the CID variant: one configuration */
         CpArgs a;

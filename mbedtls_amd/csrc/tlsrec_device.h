@@ -49,7 +49,7 @@ struct SboxGen {
 
 __constant__ const SboxGen kSbox{};
 
-__device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff; }
+__device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ (0x1bu & (0u - ((s >> 7) & 1u)))) & 0xff; }
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t rotr16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
@@ -648,10 +648,11 @@ struct G128 { uint64_t hi, lo; };
 
 __device__ __forceinline__ G128 g_shr1(G128 v)
 {
-    uint64_t lsb = v.lo & 1;
+    /* masks, not branches: H is secret and a one-lane branch is timed by exec */
+    const uint64_t lsb = 0 - (v.lo & 1);
     G128 r;
     r.lo = (v.lo >> 1) | (v.hi << 63);
-    r.hi = (v.hi >> 1) ^ (lsb ? 0xE100000000000000ULL : 0);
+    r.hi = (v.hi >> 1) ^ (lsb & 0xE100000000000000ULL);
     return r;
 }
 
@@ -659,8 +660,10 @@ __device__ inline G128 g_mul(G128 x, G128 y)
 {
     G128 z = { 0, 0 }, v = y;
     for (int i = 0; i < 128; i++) {
-        uint64_t bit = (i < 64) ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
-        if (bit) { z.hi ^= v.hi; z.lo ^= v.lo; }
+        const uint64_t bit = (i < 64) ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
+        const uint64_t m = 0 - bit;
+        z.hi ^= v.hi & m;
+        z.lo ^= v.lo & m;
         v = g_shr1(v);
     }
     return z;

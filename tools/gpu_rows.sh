@@ -19,6 +19,9 @@ done &&
 row stream16 300 python3 tools/bench_stream.py --conns 65536 --recs 16 && cat $O/stream16.json &&
 row stream4 300 python3 tools/bench_stream.py --conns 65536 --recs 4 && cat $O/stream4.json &&
 row stream_cp 300 python3 tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3 && cat $O/stream_cp.json &&
+row dtls_small 300 python3 tools/bench_dtls.py && cat $O/dtls_small.json &&
+row dtls_cp 300 python3 tools/bench_dtls.py --cipher 3 && cat $O/dtls_cp.json &&
+row dtls16k 300 python3 tools/bench_dtls.py --content 16384 --recs 4 --cipher 2 && cat $O/dtls16k.json &&
 row keysched 300 python3 tools/bench_keysched.py && cat $O/keysched.json &&
 : > $O/latency.jsonl &&
 for a in "2 1.3 16383" "2 1.3 1400" "3 1.3 1400" "1 1.2 1400" "2 1.3 100"; do
