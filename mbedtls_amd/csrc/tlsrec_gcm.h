@@ -87,14 +87,17 @@ __device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, cons
     return f;
 }
 
-/* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0 */
+/* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0.
+ * Only lanes q < SH multiply (the others' values are never read again), so a
+ * level's table reads shrink with it: L - 1 lane-multiplies per record instead
+ * of L log2 L (the shuffle runs on every lane: its sources must be active). */
 template <int SH>
-__device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane)
+__device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane, int q)
 {
     if constexpr (SH >= 1) {
         uint4 o = shfl4(Y, (lane + SH) & 63);
-        Y = xor4(gmul<Log2<SH>::v>(lds, Y), o);
-        return gtree<SH / 2>(lds, Y, lane);
+        if (q < SH) Y = xor4(gmul<Log2<SH>::v>(lds, Y), o);
+        return gtree<SH / 2>(lds, Y, lane, q);
     } else {
         return Y;
     }
@@ -196,11 +199,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 tlsrec_plan p;
                 make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
                 nonce_words<DEC>(p, d, a.in, nw);
+                /* only this pass's records: with many keys of few records
+                 * each, most of a wave's 64 positions belong to other passes
+                 * (masked lanes issue no table reads) */
+                if constexpr (ARIA)
+                    ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+                else
+                    ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
             }
-            if constexpr (ARIA)
-                ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
-            else
-                ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
             reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
         }
         /* lanes of this wave read other lanes' E(J0): the wave's own LDS
@@ -244,10 +250,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
              * only the step with cc == 0 reads it. */
             uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + wave * 64 + lane;
-            {
-                const uint4 aadh = gmul<0>(gp, jb.aadw);
-                *fold = m ? aadh : jb.aadw;
-            }
+            if (jb.run && (uint32_t) q == z % L)      /* the lane that holds block 0 (cc == 0) */
+                *fold = m ? gmul<0>(gp, jb.aadw) : jb.aadw;
             /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
              * does not depend on step j's keystream, so its table reads share
              * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
@@ -354,10 +358,12 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
             }
             /* tree: sum_q Y_q H^(L-q) */
-            Y = gtree<L / 2>(gp, Y, lane);
-            Y = gmul<0>(gp, Y);                                      /* T */
-            uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
-            Y = gmul<0>(gp, xor4(Y, lenw));                          /* GHASH */
+            Y = gtree<L / 2>(gp, Y, lane, q);
+            if (q == 0) {                                            /* the group leader's sum */
+                Y = gmul<0>(gp, Y);                                  /* T */
+                uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
+                Y = gmul<0>(gp, xor4(Y, lenw));                      /* GHASH */
+            }
             if (!jb.run) continue;
             const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
             const uint4 tag = xor4(Y, ej0);
