@@ -364,8 +364,12 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
 
 /* only_cipher: launch only that cipher's kernel (the single-record engine,
  * which knows the record's slot on the host); 0 = every cipher loaded. */
+/* avg_bytes: mean record size when the caller knows it (the stream / DTLS
+ * layers and the host pipeline do; 0 = unknown) -- it decides the GCM launch
+ * for many keys with little work each (below). */
 static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
-                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec, uint32_t only_cipher = 0)
+                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec, uint32_t only_cipher = 0,
+                 uint32_t avg_bytes = 0)
 {
     if (!kt || (!recs && n) || (!res && n)) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (n == 0) return 0;
@@ -426,8 +430,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         int nr = (int) tlsrec_cipher_nr(cipher);
         const int wpe = gcm_wp_env();
         const bool auto_l = !(lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64);
-        if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && rpk < 12) L = (rpk >= 3 && Lfill <= 16) ? 16 : 64;
-        const bool wp = !kt->has_cid && !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && rpk < 12));
+        /* wave passes (each wave stages only its key's H^L table, no
+         * workgroup barriers) for few records per key, or -- when the record
+         * size is known -- for keys with under 64 KiB of records each (same-box
+         * measurements: 16 x 1.4 KiB per key 198 -> 313 GiB/s, DTLS 125 -> 231;
+         * 16 x 16 KiB and 64 x 1.4 KiB per key stay faster with key passes) */
+        const bool light = rpk < 12 || (avg_bytes != 0 && rpk < 48 && (uint64_t) rpk * avg_bytes < 65536u);
+        if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && light) L = (rpk >= 3 && Lfill <= 16) ? 16 : 64;
+        const bool wp = !kt->has_cid && !identity && (L == 16 || L == 64) && nr != 12 && (wpe == 1 || (wpe != 0 && light));
         const int waves = wp ? 8 : (kt->has_cid ? 16 : gcm_waves());
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
@@ -526,6 +536,13 @@ extern "C" int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_
                                     uint32_t lanes_per_record, void *stream)
 {
     return batch(kt, recs, res, n, in_arena, out_arena, lanes_per_record, stream, 1);
+}
+
+extern "C" int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                   uint32_t n, const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec,
+                                   uint32_t avg_bytes)
+{
+    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, dec, 0, avg_bytes);
 }
 
 
@@ -671,7 +688,8 @@ static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_ba
         /* the descriptors' buf_off are offsets into the host arena: shift the
          * device arena base so that base + buf_off lands in the slot */
         uint8_t *dev = (uint8_t *) ((uintptr_t) p->slot[k] - (uintptr_t) C.base);
-        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, zc ? zc : dev, lanes, p->cmp, dec);
+        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, zc ? zc : dev, lanes, p->cmp, dec, 0,
+                   (uint32_t) (C.span / (C.count ? C.count : 1)));
         if (rc) break;
         e = hipEventRecord(p->ev_cmp[k], p->cmp);
         if (zc) {

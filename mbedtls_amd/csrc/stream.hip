@@ -67,6 +67,14 @@ __device__ __forceinline__ uint32_t slot_minor(const SlotState *slots, uint32_t 
     return k.cipher ? k.tls_minor : 0;
 }
 
+/* add v to *sum: a wave-wide sum, one atomic per wave */
+__device__ __forceinline__ void wave_add_bytes(unsigned long long *sum, unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(sum, v);
+}
+
 /* ---------------- receive ---------------------------------------------- */
 struct HdrStop {
     int32_t status;           /* header error that stopped the walk, 0 = out of bytes */
@@ -97,19 +105,20 @@ __device__ HdrStop walk_in(const uint8_t *base, uint32_t len, F f)
 }
 
 __global__ void in_count_kernel(const tlsrec_stream_in *s, uint32_t n, const uint8_t *arena, uint32_t *counts,
-                                HdrStop *stops)
+                                HdrStop *stops, unsigned long long *bytes)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {                       /* scan sentinel: offs[n] = total */
+    unsigned long long b = 0;
+    if (i < n) {
+        uint32_t c = 0;
+        const HdrStop st = walk_in(arena + s[i].off, s[i].len,
+                                   [&](uint32_t, uint32_t, uint32_t, uint8_t, uint8_t, uint32_t dlen) { c++; b += dlen; });
+        counts[i] = c;
+        stops[i] = st;
+    } else if (i == n) {                /* scan sentinel: offs[n] = total */
         counts[n] = 0;
-        return;
     }
-    uint32_t c = 0;
-    const HdrStop st = walk_in(arena + s[i].off, s[i].len,
-                               [&](uint32_t, uint32_t, uint32_t, uint8_t, uint8_t, uint32_t) { c++; });
-    counts[i] = c;
-    stops[i] = st;
+    wave_add_bytes(bytes, b);
 }
 
 __global__ void in_emit_kernel(const tlsrec_stream_in *s, uint32_t n, const uint8_t *arena, const uint32_t *offs,
@@ -223,16 +232,19 @@ __device__ __forceinline__ uint32_t out_body(const OutShape &o, uint32_t n)
 __device__ __forceinline__ uint32_t frag_of(const tlsrec_stream_out &s) { return s.max_frag ? s.max_frag : 16384u; }
 
 __global__ void out_count_kernel(const tlsrec_stream_out *s, uint32_t n, const SlotState *slots, uint32_t cap,
-                                 uint32_t *counts)
+                                 uint32_t *counts, unsigned long long *bytes)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {
+    unsigned long long b = 0;
+    if (i < n) {
+        const uint32_t f = frag_of(s[i]);
+        const bool ok = out_shape(slots, cap, s[i].slot).ok;
+        counts[i] = ok ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
+        b = ok ? s[i].in_len : 0;
+    } else if (i == n) {
         counts[n] = 0;
-        return;
     }
-    const uint32_t f = frag_of(s[i]);
-    counts[i] = out_shape(slots, cap, s[i].slot).ok ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
+    wave_add_bytes(bytes, b);
 }
 
 /* One wave per record (4 per workgroup): header, descriptor, and the
@@ -473,20 +485,25 @@ __device__ __forceinline__ bool dtls_conn_ok(const tlsrec_dtls_in &c, uint32_t n
 }
 
 __global__ void dtls_count_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
-                                  const uint8_t *arena, const SlotState *slots, uint32_t cap, uint32_t *counts)
+                                  const uint8_t *arena, const SlotState *slots, uint32_t cap, uint32_t *counts,
+                                  unsigned long long *bytes)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {
+    unsigned long long b = 0;
+    if (i < n) {
+        const tlsrec_dtls_in ci = c[i];
+        uint32_t cnt = 0;
+        if (dtls_conn_ok(ci, ndg, slots, cap))
+            for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++)
+                dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &h, const uint8_t *) {
+                    cnt++;
+                    b += h.data_len;
+                });
+        counts[i] = cnt;
+    } else if (i == n) {
         counts[n] = 0;
-        return;
     }
-    const tlsrec_dtls_in ci = c[i];
-    uint32_t cnt = 0;
-    if (dtls_conn_ok(ci, ndg, slots, cap))
-        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++)
-            dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &, const uint8_t *) { cnt++; });
-    counts[i] = cnt;
+    wave_add_bytes(bytes, b);
 }
 
 /* One descriptor per record.  A record is decrypted when its epoch matches
@@ -627,17 +644,20 @@ __device__ __forceinline__ uint32_t dtls_body(const OutShape &o, uint32_t cid, u
 }
 
 __global__ void dtls_out_count_kernel(const tlsrec_stream_out *s, uint32_t n, const SlotState *slots, uint32_t cap,
-                                      uint32_t *counts)
+                                      uint32_t *counts, unsigned long long *bytes)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {
+    unsigned long long b = 0;
+    if (i < n) {
+        const uint32_t f = frag_of(s[i]);
+        const OutShape sh = out_shape(slots, cap, s[i].slot);
+        const bool ok = sh.ok && !sh.tls13;
+        counts[i] = ok ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
+        b = ok ? s[i].in_len : 0;
+    } else if (i == n) {
         counts[n] = 0;
-        return;
     }
-    const uint32_t f = frag_of(s[i]);
-    const OutShape sh = out_shape(slots, cap, s[i].slot);
-    counts[i] = (sh.ok && !sh.tls13) ? (uint32_t) (((uint64_t) s[i].in_len + f - 1) / f) : 0u;
+    wave_add_bytes(bytes, b);
 }
 
 __device__ __forceinline__ void dtls_seq(uint8_t ctr[8], const uint8_t base[8], uint64_t k)
@@ -762,6 +782,7 @@ struct Scratch {
     tlsrec_scratch_lease lease = { nullptr, nullptr };
     uint32_t *counts = nullptr, *offs = nullptr;
     HdrStop *stops = nullptr;
+    unsigned long long *bytes = nullptr;   /* record bytes of the batch (its mean size steers the GCM launch) */
     void *scan_tmp = nullptr;
     size_t scan_bytes = 0;
 };
@@ -773,24 +794,29 @@ static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
                                          (int) n + 1, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     const size_t a = 256, sz4 = (((size_t) n + 1) * 4 + a - 1) / a * a, szs = ((size_t) n * sizeof(HdrStop) + a) / a * a;
-    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + sc.scan_bytes + a, &sc.lease);
+    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + a + sc.scan_bytes + a, &sc.lease);
     if (lr) return lr;
     uint8_t *m = (uint8_t *) sc.lease.mem;
     sc.counts = (uint32_t *) m;
     sc.offs = (uint32_t *) (m + sz4);
     sc.stops = (HdrStop *) (m + 2 * sz4);
-    sc.scan_tmp = m + 2 * sz4 + szs;
-    return 0;
+    sc.bytes = (unsigned long long *) (m + 2 * sz4 + szs);
+    sc.scan_tmp = m + 2 * sz4 + szs + a;
+    return hipMemsetAsync(sc.bytes, 0, sizeof(unsigned long long), st) == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
 }
 
-/* exclusive scan of counts[0..n] -> offs; returns offs[n] (the total) on the host */
-static int scan_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total)
+/* exclusive scan of counts[0..n] -> offs; returns offs[n] (the total) on the
+ * host, and the mean record size of the batch (0 if unknown) */
+static int scan_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total, uint32_t *avg_bytes = nullptr)
 {
+    unsigned long long bytes = 0;
     if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, sc.scan_bytes, sc.counts, sc.offs, (int) n + 1, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&bytes, sc.bytes, sizeof(bytes), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (avg_bytes) *avg_bytes = *total ? (uint32_t) (bytes / *total) : 0u;
     return 0;
 }
 
@@ -809,11 +835,12 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
     int r = scratch_alloc(sc, nstreams, st);
-    uint32_t total = 0;
+    uint32_t total = 0, avg = 0;
     if (r == 0) {
         hipLaunchKernelGGL(in_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
-                           (const uint8_t *) arena, sc.counts, sc.stops);
-        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                           (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total, &avg)
+                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
@@ -821,7 +848,7 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
         hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
                            (const uint8_t *) arena, sc.offs, slots, cap, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) r = tlsrec_batch_decrypt(kt, recs, res, total, arena, arena, 0, stream);
+        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }
     if (r == 0) {
         hipLaunchKernelGGL(in_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams, sc.offs,
@@ -866,11 +893,12 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
     int r = scratch_alloc(sc, nstreams, st);
-    uint32_t total = 0;
+    uint32_t total = 0, avg = 0;
     if (r == 0) {
         hipLaunchKernelGGL(out_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
-                           slots, cap, sc.counts);
-        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                           slots, cap, sc.counts, sc.bytes);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total, &avg)
+                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
@@ -878,7 +906,7 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
         hipLaunchKernelGGL(out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
                            total, slots, cap, in_arena, out_arena, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) r = tlsrec_batch_encrypt(kt, recs, res, total, out_arena, out_arena, 0, stream);
+        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
     }
     if (r == 0) {
         hipLaunchKernelGGL(out_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
@@ -915,11 +943,12 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
     int r = scratch_alloc(sc, nconns, st);
-    uint32_t total = 0;
+    uint32_t total = 0, avg = 0;
     if (r == 0) {
         hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                           ndgrams, (const uint8_t *) arena, slots, cap, sc.counts);
-        r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                           ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total, &avg)
+                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
@@ -927,7 +956,7 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
         hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
                            ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) r = tlsrec_batch_decrypt(kt, recs, res, total, arena, arena, 0, stream);
+        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }
     if (r == 0) {
         hipLaunchKernelGGL(dtls_finish_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
@@ -971,11 +1000,12 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
     int r = scratch_alloc(sc, nstreams, st);
-    uint32_t total = 0;
+    uint32_t total = 0, avg = 0;
     if (r == 0) {
         hipLaunchKernelGGL(dtls_out_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
-                           slots, cap, sc.counts);
-        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                           slots, cap, sc.counts, sc.bytes);
+        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total, &avg)
+                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
@@ -983,7 +1013,7 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
         hipLaunchKernelGGL(dtls_out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
                            total, slots, cap, in_arena, out_arena, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) r = tlsrec_batch_encrypt(kt, recs, res, total, out_arena, out_arena, 0, stream);
+        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
     }
     if (r == 0) {
         hipLaunchKernelGGL(dtls_out_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,

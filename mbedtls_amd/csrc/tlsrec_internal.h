@@ -129,6 +129,10 @@ typedef struct tlsrec_scratch_lease {
 } tlsrec_scratch_lease;
 int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, tlsrec_scratch_lease *lease);
 void tlsrec__scratch_release(tlsrec_scratch_lease *lease);
+/* tlsrec_batch_encrypt (dec = 0) / _decrypt (dec = 1) with auto lanes, for a
+ * caller that knows the batch's mean record size (the stream / DTLS layers) */
+int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
+                        const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec, uint32_t avg_bytes);
 hipError_t tlsrec__launch_bucket_zero(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_count(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_t st);
