@@ -247,6 +247,18 @@ __global__ void out_count_kernel(const tlsrec_stream_out *s, uint32_t n, const S
     wave_add_bytes(bytes, b);
 }
 
+/* records of connection i are [offs[i], offs[i] + counts[i]): park i in
+ * their descriptors' slot field for the frame kernels (one load per record
+ * instead of a binary search over offs) */
+__global__ void __launch_bounds__(256) out_map_kernel(uint32_t n, const uint32_t *offs, const uint32_t *counts,
+                                                      tlsrec_batch_rec *recs)
+{
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);   /* one wave per connection */
+    if (i >= n) return;
+    const uint32_t f = offs[i], c = counts[i];
+    for (uint32_t k = threadIdx.x & 63; k < c; k += 64) recs[f + k].slot = i;
+}
+
 /* One wave per record (4 per workgroup): header, descriptor, and the
  * plaintext copied into the record's slot of the output stream with 16-byte
  * accesses at any byte alignment (unaligned-access mode, see kernels.hip). */
@@ -256,14 +268,7 @@ __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out 
 {
     const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= total) return;
-    /* connection of record j: the last i with offs[i] <= j */
-    uint32_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (offs[mid] <= j) lo = mid;
-        else hi = mid;
-    }
-    const uint32_t i = lo;
+    const uint32_t i = recs[j].slot;              /* connection of record j (out_map_kernel) */
     const tlsrec_stream_out si = s[i];
     const uint32_t k = j - offs[i];
     const uint32_t f = frag_of(si);
@@ -679,13 +684,7 @@ __global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream
 {
     const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= total) return;
-    uint32_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (offs[mid] <= j) lo = mid;
-        else hi = mid;
-    }
-    const uint32_t i = lo;
+    const uint32_t i = recs[j].slot;              /* connection of record j (out_map_kernel) */
     const tlsrec_stream_out si = s[i];
     const uint32_t k = j - offs[i];
     const uint32_t f = frag_of(si);
@@ -903,6 +902,8 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
+        hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs, sc.counts,
+                           recs);
         hipLaunchKernelGGL(out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
                            total, slots, cap, in_arena, out_arena, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
@@ -1010,6 +1011,8 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
+        hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs, sc.counts,
+                           recs);
         hipLaunchKernelGGL(dtls_out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
                            total, slots, cap, in_arena, out_arena, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
