@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of the CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (pinned H2D/D2H) leg")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the process group even at WORLD_SIZE=1 (rehearses the RCCL path on one GPU)")
     ap.add_argument("--e2e-records", type=int, default=0, help="records of the end-to-end leg (0 = ~2 GiB worth)")
     ap.add_argument("--verify", type=int, default=64, help="records spot-checked against the oracle")
     return ap.parse_args()
@@ -105,7 +107,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.dist
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
@@ -190,7 +193,7 @@ def main():
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
@@ -201,13 +204,13 @@ def main():
         run()
         b.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
 
@@ -221,7 +224,7 @@ def main():
             got = out_arena[i * stride + lead + head:i * stride + lead + head + content].cpu().numpy()
             bad += int(not np.array_equal(got, pt_sample[i]))
     bad_t = torch.tensor([bad], dtype=torch.int64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(bad_t)
     bad = int(bad_t.item())
 
@@ -329,7 +332,7 @@ def main():
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
