@@ -782,10 +782,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
             const uint32_t h = wave_min(run ? (cfull + z) / L : 0);
             jh = h > 1 ? h : 0;
         }
-        const uint32_t jl = jh ? 1u : Jmax;
-        uint32_t j = 0;
-        for (; j < jl; j++) general(j);
-        for (; j < jh; j++) {
+        auto body = [&](uint32_t j, bool fold) {
             const uint32_t pos0 = (uint32_t) ((int32_t) (4 * L * j) + base0) * 16;
             uint4 c[4];
 #pragma unroll
@@ -804,12 +801,28 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
             const P5 x3 = p_from_words(c[3]);
 #pragma unroll
             for (int i = 0; i < 5; i++) dd.v[i] = x3.v[i];
+            P5 x0 = p_from_words(c[0]);
+            /* step 0 without front padding: slot 0 (lane q = 0, t = 0) is C_0,
+             * which takes the AAD as A*r (limbs stay < 2^27: the D5 sum holds) */
+            if (fold && q == 0) x0 = p_add(x0, p_mul(p_from_words(aadw), p_lds(cr.r1)));
             p_mac(dd, acc, p_lds(cr.rl[3]));
-            p_mac(dd, p_from_words(c[0]), p_lds(cr.rl[2]));
+            p_mac(dd, x0, p_lds(cr.rl[2]));
             p_mac(dd, p_from_words(c[1]), p_lds(cr.rl[1]));
             p_mac(dd, p_from_words(c[2]), p_lds(cr.rl[0]));
             acc = p_reduce(dd);
+        };
+        /* step 0 takes the body when no record of the wave has front padding
+         * (whole steps, e.g. 1 408-B TLS 1.3 records at L = 2) and the AAD is
+         * one block; otherwise the general step */
+        const bool body0 = jh != 0 && !CID && wave_max(z) == 0;
+        const uint32_t jl = jh ? 1u : Jmax;
+        uint32_t j = 0;
+        if (body0) {
+            body(0, true);
+            j = 1;
         }
+        for (; j < jl; j++) general(j);
+        for (; j < jh; j++) body(j, false);
         for (; j < Jmax; j++) general(j);
 
         /* sum_q acc_q r^(d_q), d_q = blocks from the end of lane q's chain to
