@@ -28,6 +28,8 @@ struct tlsrec_keytab {
     int cu;                   /* compute units of the device (launch sizing), read once at create */
     SlotState *d_slots;
     uint4 *d_ghtab;
+    uint8_t *d_cipher;        /* each slot's cipher, one byte (the bucket pass reads it per record:
+                                 an L2-resident array instead of a line of the 1 KiB slot) */
     tlsrec_key_material *d_stage;
     uint8_t *h_cipher;        /* host mirror of each slot's cipher */
     uint32_t cipher_mask;     /* 1 << TLSREC_CIPHER_* of every loaded slot */
@@ -78,11 +80,13 @@ extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
     if (!kt->h_cipher ||
         hipMalloc((void **) &kt->d_slots, sizeof(SlotState) * (size_t) capacity) != hipSuccess ||
         hipMalloc((void **) &kt->d_ghtab, sizeof(uint4) * (size_t) KEY_TABLE_WORDS * capacity) != hipSuccess ||
+        hipMalloc((void **) &kt->d_cipher, (size_t) capacity) != hipSuccess ||
         hipMalloc((void **) &kt->d_stage, sizeof(tlsrec_key_material) * (size_t) capacity) != hipSuccess) {
         tlsrec_keytab_free(kt);
         return TLSREC_ERR_SSL_ALLOC_FAILED;
     }
-    if (hipMemset(kt->d_slots, 0, sizeof(SlotState) * (size_t) capacity) != hipSuccess) {
+    if (hipMemset(kt->d_slots, 0, sizeof(SlotState) * (size_t) capacity) != hipSuccess ||
+        hipMemset(kt->d_cipher, 0, (size_t) capacity) != hipSuccess) {
         tlsrec_keytab_free(kt);
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
@@ -132,6 +136,7 @@ extern "C" void tlsrec_keytab_free(tlsrec_keytab *kt)
     }
     hipFree(kt->d_slots);
     hipFree(kt->d_ghtab);
+    hipFree(kt->d_cipher);
     hipFree(kt->d_stage);
     free(kt->h_cipher);
     free(kt);
@@ -185,7 +190,7 @@ extern "C" int tlsrec_keytab_load(tlsrec_keytab *kt, uint32_t first, uint32_t co
         if (hipStreamSynchronize(st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         src = kt->d_stage + first;
     }
-    return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, src, first, count, st));
+    return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, kt->d_cipher, src, first, count, st));
 }
 
 /* Device-side producers of key material (keysched.hip) write into the
@@ -203,7 +208,7 @@ extern "C" int tlsrec__keytab_commit_staged(tlsrec_keytab *kt, uint32_t first, u
         kt->h_cipher[first + i] = (uint8_t) cipher;
     }
     kt->cipher_mask |= 1u << cipher;
-    return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, kt->d_stage + first, first, count, st));
+    return hip_ok(tlsrec__launch_keysetup(kt->d_slots, kt->d_ghtab, kt->d_cipher, kt->d_stage + first, first, count, st));
 }
 
 /* waves per GCM workgroup: 16 (default) or 8; TLSREC_GCM_WAVES overrides */
@@ -345,6 +350,7 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     b.scan_tmp = m + 3 * szk + szp;
     BucketArgs a;
     a.slots = kt->d_slots;
+    a.cipher_of = kt->d_cipher;
     a.recs = recs;
     a.res = res;
     a.n = n;
@@ -833,6 +839,7 @@ extern "C" void tlsrec__engine_slot_free(int slot)
         /* zeroize (ssl_msg.c:6084-6099); the slot's cipher stays recorded in the
          * table's mask, so a later batch of this page may launch one kernel more */
         hipMemsetAsync(kt->d_slots + i, 0, sizeof(SlotState), g_load);
+        hipMemsetAsync(kt->d_cipher + i, 0, 1, g_load);
         hipMemsetAsync(kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS, 0, sizeof(uint4) * KEY_TABLE_WORDS, g_load);
         hipStreamSynchronize(g_load);
         kt->h_cipher[i] = 0;

@@ -236,7 +236,7 @@ __device__ inline void cam_encrypt_u64(const uint8_t *sb, const uint64_t sk[34],
 }
 
 /* One 256-thread workgroup per slot. */
-__global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab,
+__global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab, uint8_t *cipher_of,
                                                              const tlsrec_key_material *keys,
                                                              uint32_t first, uint32_t count)
 {
@@ -266,6 +266,7 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     __syncthreads();
     if (tid == 0) {
         st->km = km;
+        cipher_of[slot] = km.cipher;
         st->km.reserved[0] = 0;   /* CID length mirror (tlsrec_recdev.h plan_key) */
         st->nr = 0;
         st->cid_len = 0;          /* a (re)load leaves the slot without a CID */
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
 __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec_batch_rec &d)
 {
     if (d.slot >= a.capacity) return 0xffffffffu;
-    const int c = a.slots[d.slot].km.cipher;
+    const int c = a.cipher_of[d.slot];
     switch (c) {
         case TLSREC_CIPHER_AES_128_GCM: return d.slot;
         case TLSREC_CIPHER_AES_256_GCM: return a.capacity + d.slot;
@@ -931,11 +932,13 @@ hipError_t tlsrec__launch_gcm_alt_enc(const GcmArgs *a, int nr, int cid, uint32_
 hipError_t tlsrec__launch_gcm_alt_dec(const GcmArgs *a, int nr, int cid, uint32_t grid, hipStream_t st);
 }
 
-extern "C" hipError_t tlsrec__launch_keysetup(SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
-                                              uint32_t first, uint32_t count, hipStream_t st)
+extern "C" hipError_t tlsrec__launch_keysetup(SlotState *slots, uint4 *ghtab, uint8_t *cipher_of,
+                                              const tlsrec_key_material *keys, uint32_t first, uint32_t count,
+                                              hipStream_t st)
 {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(tlsrec_keysetup_kernel, dim3(count), dim3(256), 0, st, slots, ghtab, keys, first, count);
+    hipLaunchKernelGGL(tlsrec_keysetup_kernel, dim3(count), dim3(256), 0, st, slots, ghtab, cipher_of, keys, first,
+                       count);
     return hipGetLastError();
 }
 

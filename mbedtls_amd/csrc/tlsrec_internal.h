@@ -77,6 +77,7 @@ struct CpArgs {
  * ChaCha20-Poly1305 class; no usable slot: BAD_INPUT_DATA. */
 struct BucketArgs {
     const SlotState *slots;
+    const uint8_t *cipher_of; /* [capacity] each slot's cipher (0 = none) */
     const tlsrec_batch_rec *recs;
     tlsrec_batch_res *res;
     uint32_t n;
@@ -107,7 +108,8 @@ struct CcmArgs {
 
 extern "C" {
 hipError_t tlsrec__launch_ccm(const tlsrec::CcmArgs *a, int dec, uint32_t nr_mask, hipStream_t st);
-hipError_t tlsrec__launch_keysetup(tlsrec::SlotState *slots, uint4 *ghtab, const tlsrec_key_material *keys,
+hipError_t tlsrec__launch_keysetup(tlsrec::SlotState *slots, uint4 *ghtab, uint8_t *cipher_of,
+                                   const tlsrec_key_material *keys,
                                    uint32_t first, uint32_t count, hipStream_t st);
 hipError_t tlsrec__launch_gcm_aria(const tlsrec::GcmArgs *a, int dec, int nr, int cid, uint32_t grid, hipStream_t st);
 hipError_t tlsrec__launch_gcm(const tlsrec::GcmArgs *a, int dec, int lanes, int nr, int waves, uint32_t grid,

@@ -264,3 +264,31 @@ def test_stream_read_matches_oracle():
             assert o2[outs[k]:outs[k] + len(out)].tobytes() == out
             assert a2[offs[k]:offs[k] + len(data)].tobytes() == after
     c.close()
+
+
+@pytest.mark.parametrize("cipher", [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM])
+def test_many_keys_small_records_wave_passes(cipher):
+    """640 connections x 16 records of 1 400 B: under 64 KiB of records per
+    key, so the stream layer's record-size hint sends the GCM kernels into
+    wave passes at 16 lanes (engine.hip `light`); every record stream and
+    plaintext checked against the oracle."""
+    kl = M.KEYLEN[cipher]
+    slots = [(cipher, M.VERSION_TLS1_3, prng_bytes(9000 + i, kl), prng_bytes(19000 + i, 12), 0) for i in range(640)]
+    c = Conns(slots)
+    jobs = [(i, prng_bytes(29000 + i, 16 * 1400), i * 7919, 1400, 23) for i in range(640)]
+    got = c.encrypt(jobs)
+    for (slot, pt, ctr, frag, typ), (r, out) in zip(jobs, got):
+        st, want, nrec, ctr2 = O.stream_encrypt(c.ot[slot], pt, typ, ctr.to_bytes(8, "big"), frag)
+        assert (int(r["status"]), int(r["nrec"]), out, bytes(r["out_ctr"])) == (st, nrec, want, ctr2), slot
+    conns = [(slot, out, ctr, 0) for (slot, _, ctr, _, _), (_, out) in zip(jobs, got)]
+    a, recs, res, sres, offs = c.decrypt(conns)
+    for i, (slot, data, ctr, nbz) in enumerate(conns):
+        g = sres[i]
+        assert (int(g["status"]), int(g["nrec"])) == (0, 16), i
+        f = int(g["first"])
+        pt = jobs[i][1]
+        for k in range(16):
+            o = int(recs[f + k]["buf_off"]) + int(res[f + k]["data_offset"])
+            assert int(res[f + k]["data_len"]) == 1400
+            assert a[o:o + 1400].tobytes() == pt[1400 * k:1400 * (k + 1)], (i, k)
+    c.close()

@@ -21,6 +21,7 @@ for round in 1 2; do
     one $lib k4 python3 bench.py --config k4 --no-cpu --no-e2e --steps 5 || exit 1
     one $lib c4s python3 bench.py --config c4s --no-cpu --no-e2e --steps 5 || exit 1
     one $lib dtls1400 python3 tools/bench_dtls.py --steps 3 || exit 1
+    one $lib streamcp python3 tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3 --steps 3 || exit 1
   done
 done
 cat $O
