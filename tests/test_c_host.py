@@ -117,3 +117,25 @@ def test_system_runtime_direction_switches(mode):
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["written"] == [64] * 8, out
+
+
+DTLS = os.path.join(ROOT, "tests", "c", "dtls_host")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("conns,dgrams,content,cipher", [(64, 8, 1200, 1), (300, 3, 16384, 2), (17, 40, 100, 3),
+                                                          (32, 6, 1400, 8)])
+def test_c_dtls_host(conns, dgrams, content, cipher):
+    """tests/c/dtls_host.c: a C program (gcc, include/tlsrec.h + the HIP
+    runtime API) sends datagrams with tlsrec_dtls_encrypt and receives them,
+    plus a replay and a bad-MAC datagram per connection, with
+    tlsrec_dtls_decrypt -- every plaintext, disposition and window checked."""
+    assert _gpu(), "needs a GPU"
+    if not os.path.exists(DTLS):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c"), "dtls_host"], check=True)
+    p = subprocess.run([DTLS, str(conns), str(dgrams), str(content), str(cipher)], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, (p.stdout, p.stderr)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["pass"] is True and out["accepted"] == conns * dgrams == out["plaintext_ok"]
+    assert out["replays_skipped"] == conns and out["bad_mac_dropped"] == conns
