@@ -238,6 +238,15 @@ static int gcm_wp_env(void)
     return e ? atoi(e) : -1;
 }
 
+/* 8-lane GCM kernel with the 5-bit GHASH Horner table (gmul5: 104 instead of
+ * 128 LDS cycles per multiply); TLSREC_GCM_G5=0 selects the 4-bit table
+ * (read per batch: tests and A/B runs switch it) */
+static uint32_t gcm_g5(void)
+{
+    const char *e = getenv("TLSREC_GCM_G5");
+    return (e && atoi(e) == 0) ? 0u : 1u;
+}
+
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */
 static uint32_t gcm_lanes_env(void)
 {
@@ -448,6 +457,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
+        a.g5 = gcm_g5();
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
@@ -476,6 +486,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.rpw = pick_rpw(n, (uint32_t) ARIA_GCM_WAVES, 8u, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) c;
+        a.g5 = 0;
         const uint64_t per_wg = (uint64_t) ARIA_GCM_WAVES * a.rpw;
         const uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_alt_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)

@@ -339,6 +339,22 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
             if ((nib >> (3 - i)) & 1) acc = xor4(acc, base[p][4 * k + i]);
         out[e] = acc;
     }
+    /* H^8 again as G5 tables (tlsrec_device.h gmul5): window k, entry n =
+     * sum of P x^j over the set bits of n, j = the GCM bit index of the word
+     * bit the index bit comes from; lo halves then hi halves */
+    uint2 *g5 = reinterpret_cast<uint2 *>(out + KEY_G5_OFF);
+    for (int e = tid; e < KEY_G5_WORDS; e += 256) {
+        const int k = e >> 5, n = e & 31;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < g5_bits(k); i++)
+            if ((n >> i) & 1) {
+                const int t = g5_bit(k, i);
+                const int j = 8 * (4 * g5_word(k, i) + t / 8) + (7 - t % 8);
+                acc = xor4(acc, base[KEY_G5_POWER][j]);
+            }
+        g5[k * 32 + n] = make_uint2(acc.x, acc.y);                 /* lo halves at k * 256 B */
+        g5[G5_HI / 8 + k * 32 + n] = make_uint2(acc.z, acc.w);    /* hi halves at G5_HI + k * 256 B */
+    }
 }
 
 /* The GCM record kernel lives in tlsrec_gcm.h (instantiated by gcm_*.hip). */

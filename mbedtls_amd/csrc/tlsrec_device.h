@@ -463,6 +463,111 @@ __device__ __forceinline__ void gmul_word(const uint8_t *lds, uint32_t wd, int d
     }
 }
 
+/* ---------------- GHASH with 5-bit position tables (G5) ------------------ *
+ * ds_read_b64 serves 32 lanes per LDS cycle over all 64 banks, so a 256-byte
+ * image of 32 eight-byte entries is conflict-free for any index: a 5-bit
+ * window read as two 8-byte halves costs the LDS what one 4-bit window's
+ * ds_read_b128 costs.  26 windows cover the 128 bits (24 of 5 bits, 2 of 4
+ * that straddle a word boundary): 104 LDS cycles per multiply instead of 128.
+ * Windows take contiguous bits of the little-endian block words; the lo
+ * halves (8 B) of window k's 32 entries sit at k*256, the hi halves at
+ * G5_HI + k*256 -- more than ds_read2_b64's offset range apart, so the two
+ * reads of a window stay ds_read_b64 (the fused ds_read2_b64 takes 8 LDS
+ * cycles over 32 banks and would conflict).  Entry n of window
+ * k = sum over set bits i of n of P * x^j(bit i), j the GCM bit index of that
+ * word bit (tlsrec_keysetup_kernel writes the tables). */
+constexpr int G5_HI = 26 * 256;
+struct G5Win { uint8_t d, s, cross; };
+__host__ __device__ constexpr G5Win g5_win(int k)
+{
+    return k < 6 ? G5Win{ 0, (uint8_t) (5 * k), 0 }
+         : k == 6 ? G5Win{ 0, 30, 1 }
+         : k < 13 ? G5Win{ 1, (uint8_t) (2 + 5 * (k - 7)), 0 }
+         : k < 19 ? G5Win{ 2, (uint8_t) (5 * (k - 13)), 0 }
+         : k == 19 ? G5Win{ 2, 30, 1 }
+         : G5Win{ 3, (uint8_t) (2 + 5 * (k - 20)), 0 };
+}
+/* word / bit of bit i (0 = LSB) of window k's index */
+__host__ __device__ constexpr int g5_word(int k, int i) { return g5_win(k).cross && i >= 2 ? g5_win(k).d + 1 : g5_win(k).d; }
+__host__ __device__ constexpr int g5_bit(int k, int i)
+{
+    return g5_win(k).cross ? (i < 2 ? 30 + i : i - 2) : g5_win(k).s + i;
+}
+__host__ __device__ constexpr int g5_bits(int k) { return g5_win(k).cross ? 4 : 5; }
+
+/* byte offset (index * 8) of window k's entry for the block words w */
+template <int K>
+__device__ __forceinline__ uint32_t g5_addr(const uint32_t (&w)[4])
+{
+    constexpr G5Win W = g5_win(K);
+    if constexpr (W.cross)
+        return __builtin_amdgcn_alignbit(w[W.d + 1], w[W.d], 27) & 0x78u;
+    else if constexpr (W.s >= 3)
+        return (w[W.d] >> (W.s - 3)) & 0xF8u;
+    else
+        return (w[W.d] << (3 - W.s)) & 0xF8u;
+}
+
+/* the hi-half address as a register the compiler cannot relate to the lo
+ * one: otherwise it fuses the pair into ds_read2st64_b64 (8 LDS cycles over
+ * 32 banks, conflicting) */
+__device__ __forceinline__ uint32_t g5_hi(uint32_t a)
+{
+    uint32_t h;
+    asm("v_mov_b32 %0, %1" : "=v"(h) : "v"(a));
+    return h;
+}
+
+/* acc ^= the products of windows K0 .. K0+NK-1 (table at lds) */
+template <int K0, int NK>
+__device__ __forceinline__ void gmul5_part(const uint8_t *lds, const uint32_t (&w)[4], uint4 &acc)
+{
+    if constexpr (NK >= 2) {
+        const uint32_t a0 = g5_addr<K0>(w), a1 = g5_addr<K0 + 1>(w);
+        const uint2 l0 = *reinterpret_cast<const uint2 *>(lds + a0 + K0 * 256);
+        const uint2 h0 = *reinterpret_cast<const uint2 *>(lds + g5_hi(a0) + G5_HI + K0 * 256);
+        const uint2 l1 = *reinterpret_cast<const uint2 *>(lds + a1 + (K0 + 1) * 256);
+        const uint2 h1 = *reinterpret_cast<const uint2 *>(lds + g5_hi(a1) + G5_HI + (K0 + 1) * 256);
+        acc.x = xor3(acc.x, l0.x, l1.x);
+        acc.y = xor3(acc.y, l0.y, l1.y);
+        acc.z = xor3(acc.z, h0.x, h1.x);
+        acc.w = xor3(acc.w, h0.y, h1.y);
+        gmul5_part<K0 + 2, NK - 2>(lds, w, acc);
+    } else if constexpr (NK == 1) {
+        const uint32_t a0 = g5_addr<K0>(w);
+        const uint2 l0 = *reinterpret_cast<const uint2 *>(lds + a0 + K0 * 256);
+        const uint2 h0 = *reinterpret_cast<const uint2 *>(lds + g5_hi(a0) + G5_HI + K0 * 256);
+        acc.x ^= l0.x;
+        acc.y ^= l0.y;
+        acc.z ^= h0.x;
+        acc.w ^= h0.y;
+    }
+}
+
+/* phase g (0..7) of a G5 multiply: windows [3g + min(g, 2), ...): 4,4,3,3,3,3,3,3 */
+template <int G>
+__device__ __forceinline__ void gmul5_phase(const uint8_t *lds, const uint32_t (&w)[4], uint4 &acc)
+{
+    constexpr int K0 = G < 2 ? 4 * G : 8 + 3 * (G - 2);
+    constexpr int NK = G < 2 ? 4 : 3;
+    gmul5_part<K0, NK>(lds, w, acc);
+}
+
+/* y * P with P's G5 table at lds (whole multiply, four phases of 6-7 windows) */
+__device__ __forceinline__ uint4 gmul5(const uint8_t *lds, uint4 y)
+{
+    const uint32_t w[4] = { y.x, y.y, y.z, y.w };
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    gmul5_part<0, 7>(lds, w, acc);
+    asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w) : : "memory");
+    gmul5_part<7, 6>(lds, w, acc);
+    asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w) : : "memory");
+    gmul5_part<13, 7>(lds, w, acc);
+    asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w) : : "memory");
+    gmul5_part<20, 6>(lds, w, acc);
+    return acc;
+}
+
 /* AES middle round r on (s0..s3), rotated round keys (see aes_encrypt). */
 template <int AES_OFF, typename RK>
 __device__ __forceinline__ void aes_round(const uint8_t *lds, uint32_t lb, RK rk, int r,
@@ -523,7 +628,7 @@ __device__ __forceinline__ CtrCache ctr_cache(const uint8_t *lds, uint32_t lb, R
  * asm statements are the phase boundaries: they re-define the AES state, the
  * accumulator and the source words still to be read, so no read moves into an
  * earlier phase (bounded reads in flight and VGPRs, no memory clobber). */
-template <int NR, int AES_OFF, int PI, int R0 = 2, int RS = 1, typename RK>
+template <int NR, int AES_OFF, int PI, int R0 = 2, int RS = 1, bool G5 = false, typename RK>
 __device__ __forceinline__ void aes_ghash(const uint8_t *lds, const uint8_t *gh, uint32_t lb, RK rk,
                                           const CtrCache &cc, uint32_t ctrw, uint4 y, uint4 &ks, uint4 &prod)
 {
@@ -549,13 +654,34 @@ __device__ __forceinline__ void aes_ghash(const uint8_t *lds, const uint8_t *gh,
         if (r > 2) aes_round<AES_OFF>(lds, lb, rk, r, s0, s1, s2, s3);
         const int g = (r - R0) / RS;
         if (r >= R0 && (r - R0) % RS == 0 && g < 8) {
-            gmul_word<PI, 2>(gh, w[g >> 1], g >> 1, acc, 2 * (g & 1));
-            asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(acc.x), "+v"(acc.y), "+v"(acc.z),
-                         "+v"(acc.w));
-            /* the words still to be read enter the next phase through the barrier */
-            if (g < 2) asm volatile("" : "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
-            else if (g < 4) asm volatile("" : "+v"(w[2]), "+v"(w[3]));
-            else if (g < 6) asm volatile("" : "+v"(w[3]));
+            if constexpr (G5) {
+                /* G5 phases read windows across word boundaries: every word
+                 * still read enters the next phase through the barrier */
+                switch (g) {
+                    case 0: gmul5_phase<0>(gh, w, acc); break;
+                    case 1: gmul5_phase<1>(gh, w, acc); break;
+                    case 2: gmul5_phase<2>(gh, w, acc); break;
+                    case 3: gmul5_phase<3>(gh, w, acc); break;
+                    case 4: gmul5_phase<4>(gh, w, acc); break;
+                    case 5: gmul5_phase<5>(gh, w, acc); break;
+                    case 6: gmul5_phase<6>(gh, w, acc); break;
+                    default: gmul5_phase<7>(gh, w, acc); break;
+                }
+                asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(acc.x), "+v"(acc.y), "+v"(acc.z),
+                             "+v"(acc.w));
+                if (g < 2) asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+                else if (g < 4) asm volatile("" : "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+                else if (g < 6) asm volatile("" : "+v"(w[2]), "+v"(w[3]));
+                else asm volatile("" : "+v"(w[3]));
+            } else {
+                gmul_word<PI, 2>(gh, w[g >> 1], g >> 1, acc, 2 * (g & 1));
+                asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(acc.x), "+v"(acc.y), "+v"(acc.z),
+                             "+v"(acc.w));
+                /* the words still to be read enter the next phase through the barrier */
+                if (g < 2) asm volatile("" : "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+                else if (g < 4) asm volatile("" : "+v"(w[2]), "+v"(w[3]));
+                else if (g < 6) asm volatile("" : "+v"(w[3]));
+            }
         }
     }
     uint32_t o[4];

@@ -27,15 +27,19 @@ namespace tlsrec {
 /* WP (wave passes): each wave keeps only its current key's H^L table in its
  * own 8 KiB of LDS; the once-per-record multiplies (AAD fold, tree, final)
  * read the key's tables in global memory. */
-template <int L, int W, bool WP = false>
+/* G5: the Horner table H^L is the 13 KiB 5-bit form (gmul5) after the tree's
+ * 4-bit tables H^1 .. H^(L/2). */
+template <int L, int W, bool WP = false, bool G5 = false>
 struct GcmLds {
-    static constexpr int NT = WP ? W : Log2<L>::v + 1;  /* GHASH tables H^1 .. H^L, or one H^L per wave */
+    static constexpr int NT = WP ? W : Log2<L>::v + (G5 ? 0 : 1);  /* 4-bit GHASH tables, or one H^L per wave */
     static constexpr int GH = 0;
-    static constexpr int AES = NT * 8192;               /* T0/T1 x 32 copies */
+    static constexpr int HG5 = NT * 8192;               /* G5 Horner table */
+    static constexpr int AES = HG5 + (G5 ? KEY_G5_WORDS * 16 : 0);   /* T0/T1 x 32 copies */
     static constexpr int EJ0 = AES + 65536;             /* W waves x 64 x 16 B */
     static constexpr int FOLD = EJ0 + W * 64 * 16;      /* W waves x 64 x 16 B: AAD fold */
     static constexpr int CTL = FOLD + W * 64 * 16;
     static constexpr int BYTES = CTL + 16;
+    static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 
 /* Per-record state that the AEAD loop reads (kept small: it lives in
@@ -105,10 +109,12 @@ __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane, in
 
 /* ARIA: the block cipher is ARIA (NR = 12/14/16 rounds, S-box tables in the
  * T-table LDS region, round keys SlotState::ark) -- GCM around it unchanged */
-template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false, bool ARIA = false>
+template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false, bool ARIA = false,
+          bool G5 = false>
 __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 {
-    using LY = GcmLds<L, W, WP>;
+    static_assert(!G5 || (L == 1 << KEY_G5_POWER && !WP && !CID && !ARIA && B == 1), "G5: the 8-lane 16-wave kernel");
+    using LY = GcmLds<L, W, WP, G5>;
     constexpr int NTHR = W * 64;
     constexpr int LOGL = Log2<L>::v;
     constexpr int R = 64 / L;
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 
     /* Horner multiplier table H^L (hor) and the per-record tables H^1..H^(L/2) (gp) */
     constexpr int HPI = WP ? 0 : LOGL;                   /* H^L table index from hor */
-    const uint8_t *hor = WP ? lds + LY::GH + wave * 8192 : lds + LY::GH;
+    const uint8_t *hor = WP ? lds + LY::GH + wave * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
     for (int iter = 0;; iter++) {
         uint32_t s;
         if constexpr (WP) {
@@ -179,6 +185,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
                 uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
                 for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
+                if constexpr (G5) {
+                    uint4 *d5 = reinterpret_cast<uint4 *>(lds + LY::HG5);
+                    for (int i = tid; i < KEY_G5_WORDS; i += NTHR) d5[i] = src[KEY_G5_OFF + i];
+                }
             }
             __syncthreads();
         }
@@ -279,13 +289,16 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 auto crypt = [&](int32_t cc, uint4 y, uint4 &ks, uint4 &Zn) {
                     const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
                     if constexpr (CACHED) {
-                        aes_ghash<NR, LY::AES, HPI>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
+                        aes_ghash<NR, LY::AES, HPI, 2, 1, G5>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
                     } else {
                         if constexpr (ARIA)
                             ks = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
                         else
                             ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
-                        Zn = gmul<HPI>(hor, y);
+                        if constexpr (G5)
+                            Zn = gmul5(hor, y);
+                        else
+                            Zn = gmul<HPI>(hor, y);
                     }
                 };
                 auto general = [&](uint32_t j) {
@@ -456,10 +469,18 @@ template <int L, int NR, bool DEC, int W>
 static hipError_t launch_gcm_t(const GcmArgs &a, uint32_t grid, hipStream_t st)
 {
     /* 16 waves x 1 block per lane, or 8 waves x 2 independent blocks per lane */
-    if constexpr (W == 8)
+    if constexpr (W == 8) {
         hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 8, 2>), dim3(grid), dim3(8 * 64), 0, st, a);
-    else
+    } else if constexpr (L == 1 << KEY_G5_POWER) {
+        /* 8 lanes: the Horner multiplier H^8 from the 5-bit (G5) table */
+        if (a.g5)
+            hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 16, 1, false, false, false, true>), dim3(grid),
+                               dim3(16 * 64), 0, st, a);
+        else
+            hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 16, 1>), dim3(grid), dim3(16 * 64), 0, st, a);
+    } else {
         hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 16, 1>), dim3(grid), dim3(16 * 64), 0, st, a);
+    }
     return hipGetLastError();
 }
 

@@ -11,8 +11,13 @@
 
 namespace tlsrec {
 
-constexpr int KEY_TABLES = 7;                       /* H^1, H^2, ..., H^64 */
-constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512;   /* uint4 entries per slot (56 KiB) */
+constexpr int KEY_TABLES = 7;                       /* H^1, H^2, ..., H^64 (4-bit position tables) */
+/* plus H^8 as 5-bit position tables read in 8-byte halves (gmul5 in
+ * tlsrec_device.h): 26 windows x 512 B, the 8-lane Horner multiplier */
+constexpr int KEY_G5_POWER = 3;                     /* H^(2^3) */
+constexpr int KEY_G5_WORDS = 26 * 32;               /* uint4 entries (13 KiB) */
+constexpr int KEY_G5_OFF = KEY_TABLES * 512;        /* uint4 offset of the G5 table in a slot */
+constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512 + KEY_G5_WORDS;   /* uint4 entries per slot (69 KiB) */
 
 constexpr int GCM_WAVES = 16;                       /* default waves per workgroup (one WG per CU) */
 constexpr int CP_THREADS = 256;
@@ -56,6 +61,7 @@ struct GcmArgs {
     uint32_t rpw;             /* records per wavefront chunk (<= 64) */
     uint32_t capacity;
     uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM / _192_GCM */
+    uint32_t g5;              /* host-side launch choice: 5-bit GHASH Horner table (8-lane, 16-wave kernel) */
 };
 
 struct CpArgs {

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Fresh-build check on one box: the -m gpu suite, smoke, then one default bench line.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.txt 2>&1 || { echo "gpu tests failed"; tail -20 gpurun_out/gpu_tests.txt; exit 1; }
+tail -2 gpurun_out/gpu_tests.txt
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.txt 2>&1 || { echo "smoke failed"; tail -5 gpurun_out/smoke.txt; exit 1; }
+timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { echo "bench failed"; tail -5 gpurun_out/bench_default.err; exit 1; }
+cat gpurun_out/bench_default.json
