@@ -285,6 +285,7 @@ def main():
                    "ceiling_GBps": round(achieved / busy, 1) if busy > 0 else None,
                    "ceiling_frac_of_hbm": round(achieved / busy / HBM_PEAK_GBS, 4) if busy > 0 else None,
                    "clock_ghz": cj.get("effective_clock_ghz"), "units": cj.get("units"),
+                   "valu_x4": cj.get("valu_x4"), "valu_model": cj.get("valu_model"),
                    "source": f"profiles/ceiling_{args.config}.json ({cj.get('source', '?')})"}
 
     steps_s = wall / args.steps

@@ -6,6 +6,10 @@ correction, effective shader clock = GRBM_GUI_ACTIVE / 8 XCDs / duration) and
 the busy fraction of the LDS array and the VALU:
     lds_busy  = SQ_LDS_IDX_ACTIVE (LDS-array cycles, all CUs) / (CUs x cycles)
     valu_busy = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (4 SIMDs x CUs x cycles)
+    [--valu-ticks T: the kernel's hot-loop mean issue cost per VALU instruction
+     (tools/valu_mix.py over the per-class costs of tools/rate_probe.hip); the
+     ceiling file then charges T instead of 4 cycles per instruction and keeps
+     the 4-cycle figure as valu_x4]
 (a wave64 integer VALU instruction holds its SIMD for 4 cycles: tools/chacha_probe.hip
 measures the ChaCha20 block, ~990 such instructions, at the same chip-wide rate
 with 1, 2, 3 or 4 waves per SIMD -- 2.0-2.3 TB/s of keystream -- i.e. the VALU,
@@ -23,6 +27,11 @@ from summarize_pmc import summarize  # noqa: E402
 CUS = 256
 args = sys.argv[1:]
 ceil_path = None
+valu_ticks = None
+if "--valu-ticks" in args:
+    k = args.index("--valu-ticks")
+    valu_ticks = float(args[k + 1])
+    del args[k:k + 2]
 if "--ceiling" in args:
     k = args.index("--ceiling")
     ceil_path = args[k + 1]
@@ -55,11 +64,16 @@ if "pmc_fetch" in out and "pmc_write" in out:
 out["derived"] = d
 print(json.dumps(out, indent=1))
 if ceil_path:
-    units = {"lds": d.get("lds_busy_frac", 0.0), "valu": d["valu_busy_frac"]}
+    valu = d["valu_busy_frac"] * (valu_ticks / 4 if valu_ticks else 1.0)
+    units = {"lds": d.get("lds_busy_frac", 0.0), "valu": valu}
     lim = max(units, key=units.get)
+    extra = {}
+    if valu_ticks:
+        extra = {"valu_x4": round(d["valu_busy_frac"], 4),
+                 "valu_model": f"SQ_ACTIVE_INST_VALU x {valu_ticks} cycles (hot-loop mix, tools/valu_mix.py)"}
     with open(ceil_path, "w") as f:
         json.dump({"limiter": lim, "limiter_busy_frac": round(units[lim], 4),
-                   "units": {k: round(v, 4) for k, v in units.items()},
+                   "units": {k: round(v, 4) for k, v in units.items()}, **extra,
                    "effective_clock_ghz": round(d["effective_clock_ghz"], 3),
                    "lds_bank_conflict_frac": round(d.get("lds_bank_conflict_frac", 0.0), 5),
                    "source": os.path.basename(os.path.normpath(root)) + " (rocprofv3 --pmc, " + kern + ")"}, f, indent=1)
