@@ -172,9 +172,12 @@ def main():
     pt_sample = {i: arena[i * stride + lead + head:i * stride + lead + head + content].cpu().numpy().copy()
                  for i in sample}
 
+    # the caller's record size as the launch hint of tlsrec_batch_*_sized
+    # (lanes auto); an explicit --lanes takes the unhinted call
+    hint = 0 if args.lanes else wire
     if direction == "decrypt":
         # produce the ciphertexts with the (separately verified) encrypt kernel
-        M.batch_encrypt(kt, recs_dev, res_dev, n, arena, arena, lanes=args.lanes)
+        M.batch_encrypt(kt, recs_dev, res_dev, n, arena, arena, lanes=args.lanes, mean_bytes=hint)
         torch.cuda.synchronize()
         enc_status = res_dev.view(torch.int32)[0::4]
         assert int((enc_status != 0).sum()) == 0, "encrypt of the synthetic batch failed"
@@ -183,11 +186,13 @@ def main():
         dec["data_len"] = wire
         in_recs = torch.from_numpy(dec.view(np.uint8).copy()).to(dev)
         in_arena, out_arena = arena, torch.empty_like(arena)
-        run = lambda: M.batch_decrypt(kt, in_recs, res_dev, n, in_arena, out_arena, lanes=args.lanes)  # noqa: E731
+        run = lambda: M.batch_decrypt(kt, in_recs, res_dev, n, in_arena, out_arena, lanes=args.lanes,  # noqa: E731
+                                      mean_bytes=hint)
     else:
         in_recs = recs_dev
         in_arena, out_arena = arena, torch.empty_like(arena)
-        run = lambda: M.batch_encrypt(kt, in_recs, res_dev, n, in_arena, out_arena, lanes=args.lanes)  # noqa: E731
+        run = lambda: M.batch_encrypt(kt, in_recs, res_dev, n, in_arena, out_arena, lanes=args.lanes,  # noqa: E731
+                                      mean_bytes=hint)
 
     # ---- warmup, then K timed steps -----------------------------------------
     for _ in range(args.warmup):

@@ -251,6 +251,19 @@ int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
                          tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
                          uint8_t *out_arena, uint32_t lanes_per_record, void *stream);
 
+/* The same with the caller's mean record size (buf_len bytes, 0 = unknown)
+ * as a launch hint: the host cannot read device-resident descriptors without
+ * a sync, and with many keys of small records (<= 4 KiB, 12..127 per key)
+ * the GCM kernels then take per-wave key passes at 4 lanes per record (the
+ * stream / DTLS layers and the host pipeline pass the size themselves).
+ * Results are identical with any hint; lanes are chosen automatically. */
+int tlsrec_batch_encrypt_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
+                               tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
+                               uint8_t *out_arena, uint32_t mean_record_bytes, void *stream);
+int tlsrec_batch_decrypt_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
+                               tlsrec_batch_res *res, uint32_t n, const uint8_t *in_arena,
+                               uint8_t *out_arena, uint32_t mean_record_bytes, void *stream);
+
 /* Records in HOST memory (the socket-buffer boundary of ssl_msg.c:2058 /
  * :1855): the same per-record semantics as tlsrec_batch_*, with `recs` /
  * `res` host arrays and buf_off offsets into the host arenas in_arena /

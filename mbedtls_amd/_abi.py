@@ -143,6 +143,8 @@ SIGNATURES = {
     "tlsrec_keytab_free": (None, [_VP]),
     "tlsrec_batch_encrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
     "tlsrec_batch_decrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
+    "tlsrec_batch_encrypt_sized": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
+    "tlsrec_batch_decrypt_sized": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, _VP]),
     "tlsrec_host_batch_encrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, ctypes.c_uint64]),
     "tlsrec_host_batch_decrypt": (_INT, [_VP, _VP, _VP, _U32, _VP, _VP, _U32, ctypes.c_uint64]),
     "tlsrec_frame_check": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP]),

@@ -96,22 +96,31 @@ class KeyTable:
             pass
 
 
-def batch_encrypt(kt: KeyTable, recs, res, n: int, in_arena, out_arena=None, lanes: int = 0,
-                  stream=None) -> None:
+def _batch(name: str, kt: KeyTable, recs, res, n: int, in_arena, out_arena, lanes: int, stream,
+           mean_bytes: int) -> None:
+    """tlsrec_batch_<dir> (lanes: 0 = auto), or tlsrec_batch_<dir>_sized when
+    the caller passes its mean record size (then lanes are auto)."""
     out_arena = in_arena if out_arena is None else out_arena
-    r = _abi.load().tlsrec_batch_encrypt(kt.handle, _ptr(recs), _ptr(res), n, _ptr(in_arena),
-                                         _ptr(out_arena), lanes, _stream(stream))
+    lib = _abi.load()
+    if mean_bytes:
+        if lanes:
+            raise ValueError("mean_bytes is a hint for the automatic lane choice: pass lanes=0")
+        fn, arg = getattr(lib, name + "_sized"), mean_bytes
+    else:
+        fn, arg = getattr(lib, name), lanes
+    r = fn(kt.handle, _ptr(recs), _ptr(res), n, _ptr(in_arena), _ptr(out_arena), arg, _stream(stream))
     if r != 0:
-        raise RuntimeError(f"tlsrec_batch_encrypt failed: {r:#x}")
+        raise RuntimeError(f"{name} failed: {r:#x}")
+
+
+def batch_encrypt(kt: KeyTable, recs, res, n: int, in_arena, out_arena=None, lanes: int = 0,
+                  stream=None, mean_bytes: int = 0) -> None:
+    _batch("tlsrec_batch_encrypt", kt, recs, res, n, in_arena, out_arena, lanes, stream, mean_bytes)
 
 
 def batch_decrypt(kt: KeyTable, recs, res, n: int, in_arena, out_arena=None, lanes: int = 0,
-                  stream=None) -> None:
-    out_arena = in_arena if out_arena is None else out_arena
-    r = _abi.load().tlsrec_batch_decrypt(kt.handle, _ptr(recs), _ptr(res), n, _ptr(in_arena),
-                                         _ptr(out_arena), lanes, _stream(stream))
-    if r != 0:
-        raise RuntimeError(f"tlsrec_batch_decrypt failed: {r:#x}")
+                  stream=None, mean_bytes: int = 0) -> None:
+    _batch("tlsrec_batch_decrypt", kt, recs, res, n, in_arena, out_arena, lanes, stream, mean_bytes)
 
 
 def host_batch(decrypt: bool, kt: KeyTable, recs, res, n: int, in_arena, out_arena=None, lanes: int = 0,

@@ -496,7 +496,7 @@ static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t gr
         return hipErrorInvalidValue;
     }
     if (waves == -8) {   /* wave-pass variant (engine: many keys, few records each) */
-        if constexpr (L == 16 || L == 64) {
+        if constexpr (L == 4 || L == 16 || L == 64) {
             if (nr == 10) return launch_gcm_wp<L, 10, DEC>(a, grid, st);
             if (nr == 14) return launch_gcm_wp<L, 14, DEC>(a, grid, st);
         }
