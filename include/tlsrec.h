@@ -254,7 +254,7 @@ int tlsrec_batch_decrypt(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,
 /* The same with the caller's mean record size (buf_len bytes, 0 = unknown)
  * as a launch hint: the host cannot read device-resident descriptors without
  * a sync, and with many keys of small records (<= 4 KiB, 12..127 per key)
- * the GCM kernels then take per-wave key passes at 4 lanes per record (the
+ * the GCM kernels then take per-wave key passes at 2 or 4 lanes per record (the
  * stream / DTLS layers and the host pipeline pass the size themselves).
  * Results are identical with any hint; lanes are chosen automatically. */
 int tlsrec_batch_encrypt_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs,

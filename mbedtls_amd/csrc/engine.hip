@@ -427,9 +427,9 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
          * 536 GiB/s) */
         const uint64_t rpwave = (uint64_t) n / ((uint64_t) cu * GCM_WAVES);
         const int Lfill = rpwave >= 8 ? 8 : (rpwave >= 2 ? 16 : 64);
-        int L = (lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
+        int L = (lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
                 : (nl <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
-        if (!(lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) && Lfill > L) L = Lfill;
+        if (!(lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) && Lfill > L) L = Lfill;
         if (kt->has_cid) L = 8;     /* the CID variant: one configuration */
         GcmArgs a;
         a.slots = kt->d_slots;
@@ -444,7 +444,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.out = out;
         int nr = (int) tlsrec_cipher_nr(cipher);
         const int wpe = gcm_wp_env();
-        const bool auto_l = !(lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64);
+        const bool auto_l = !(lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64);
         /* wave passes (each wave stages only its key's H^L table, no
          * workgroup barriers) for few records per key, or -- when the record
          * size is known -- for keys with under 64 KiB of records each (same-box
@@ -458,14 +458,20 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
          *   64 K keys x 16, DTLS AES-128-GCM   receive 232 -> 390, send 212 -> 328 GiB/s
          *   64 K keys x 16, stream AES-256-GCM receive 198 -> 335, send 200 -> 294
          *   16 K keys x 64, stream AES-256-GCM receive 317 -> 357, send 282 -> 324
-         *   c4s (64 K keys x 64, GCM + ChaCha)  486 -> 541 */
-        const bool small4 = avg_bytes != 0 && avg_bytes <= 4096 && rpk >= 12 && rpk < 128 &&
-                            (uint64_t) n >= (uint64_t) cu * 8 * 16;
-        const bool light = rpk < 12 || (avg_bytes != 0 && rpk < 48 && (uint64_t) rpk * avg_bytes < 65536u) || small4;
+         *   c4s (64 K keys x 64, GCM + ChaCha)  486 -> 541
+         * and 2 lanes (32 records per round, the tree only H^1) from 48 records
+         * per key: 16 K keys x 64 stream receive 353 -> 375, send 319 -> 332,
+         * c4s 536 -> 549 (at 16 per key 2 lanes idle half the wave: 388 -> 254). */
+        const bool small = avg_bytes != 0 && avg_bytes <= 4096 && rpk >= 12 && rpk < 128;
+        const bool small2 = small && rpk >= 48 && (uint64_t) n >= (uint64_t) cu * 8 * 32;
+        const bool small4 = small && !small2 && (uint64_t) n >= (uint64_t) cu * 8 * 16;
+        const bool light = rpk < 12 || (avg_bytes != 0 && rpk < 48 && (uint64_t) rpk * avg_bytes < 65536u) ||
+                           small2 || small4;
         if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && light)
-            L = small4 ? 4 : ((rpk >= 3 && Lfill <= 16) ? 16 : 64);
-        const bool wp = !kt->has_cid && !identity && (L == 4 || L == 16 || L == 64) && nr != 12 &&
+            L = small2 ? 2 : (small4 ? 4 : ((rpk >= 3 && Lfill <= 16) ? 16 : 64));
+        const bool wp = !kt->has_cid && !identity && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
                         (wpe == 1 || (wpe != 0 && light));
+        if (L == 2 && !wp) L = 4;     /* 2 lanes: wave passes only */
         const int waves = wp ? 8 : (kt->has_cid ? 16 : gcm_waves());
         a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;

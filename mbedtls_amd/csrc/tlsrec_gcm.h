@@ -512,6 +512,11 @@ template <bool DEC>
 hipError_t gcm_dispatch(const GcmArgs &a, int lanes, int nr, int waves, uint32_t grid, hipStream_t st)
 {
     switch (lanes) {
+        case 2:   /* wave passes only */
+            if (waves != -8) return hipErrorInvalidValue;
+            if (nr == 10) return launch_gcm_wp<2, 10, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_wp<2, 14, DEC>(a, grid, st);
+            return hipErrorInvalidValue;
         case 4: return launch_gcm_nr<4, DEC>(a, nr, waves, grid, st);
         case 8: return launch_gcm_nr<8, DEC>(a, nr, waves, grid, st);
         case 16: return launch_gcm_nr<16, DEC>(a, nr, waves, grid, st);

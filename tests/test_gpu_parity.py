@@ -256,7 +256,7 @@ def test_many_keys_all_ciphers_round_robin(lanes):
         assert not bad, "; ".join(bad[:5])
 
 
-@pytest.mark.parametrize("lanes", [4, 16, 64])
+@pytest.mark.parametrize("lanes", [2, 4, 16, 64])
 def test_gcm_wave_pass(lanes, monkeypatch):
     """Wave-pass GCM variant (TLSREC_GCM_WP=1: per-wave key passes, H^L per
     wave in LDS, per-record tables from HBM): 200 keys of GCM-128/192/256 and
@@ -284,12 +284,13 @@ def test_gcm_wave_pass(lanes, monkeypatch):
 @pytest.mark.parametrize("per_key", [16, 64])
 def test_gcm_sized_small_records(per_key):
     """tlsrec_batch_*_sized with a small mean record size: many keys of
-    12..127 small records each (>= 32 K records, the chip-fill bound) send the
-    GCM kernels into 4-lane wave passes (engine.hip `small4`); AES-128/256-GCM
-    and ChaCha20-Poly1305 keys, records round-robin over keys, lengths around
+    12..127 small records each send the GCM kernels into wave passes at 4
+    lanes (16 per key, 36 K records: engine.hip `small4`) or 2 lanes (64 per
+    key, 64 K records, the chip-fill bound of `small2`); AES-128/256-GCM and
+    ChaCha20-Poly1305 keys, records round-robin over keys, lengths around
     1.4 KiB incl. ragged ones and tampered records -- bit-exact vs the oracle
     in both directions."""
-    nkeys = 36864 // per_key
+    nkeys = (36864 if per_key < 48 else 65536) // per_key
     slots = B.random_slots(4242 + per_key, [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305],
                            [M.VERSION_TLS1_3, M.VERSION_TLS1_2], nkeys)
     n = nkeys * per_key
