@@ -56,6 +56,10 @@ CONFIGS = {
            "64K keys x 4 records, AES-256-GCM, records round-robin over keys, 16 KiB TLS 1.3 decrypt (few records per key)"),
     "chacha16k": ("CHACHA20-POLY1305", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
                   "ChaCha20-Poly1305 decrypt, 1M x 16 KiB TLS 1.3 records, single key (the c4 ChaCha share)"),
+    "c3d": ("CHACHA20-POLY1305", "TLS1.3", "decrypt", 1400, 1 << 20, 1,
+            "ChaCha20-Poly1305 decrypt, 1M x 1.4 KiB TLS 1.3 records, single key (c3 received)"),
+    "chacha16ke": ("CHACHA20-POLY1305", "TLS1.3", "encrypt", 16383, 1 << 20, 1,
+                   "ChaCha20-Poly1305 encrypt, 1M x 16 KiB TLS 1.3 records, single key (chacha16k sent)"),
     "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
             "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 1.4 KiB TLS 1.3 decrypt"),
 }
