@@ -54,6 +54,8 @@ CONFIGS = {
                     "Camellia-128-GCM decrypt, 1M x 16 KiB TLS 1.2 records, single key (8(f)-2)"),
     "k4": ("AES-256-GCM", "TLS1.3", "decrypt", 16383, 1 << 18, 1 << 16,
            "64K keys x 4 records, AES-256-GCM, records round-robin over keys, 16 KiB TLS 1.3 decrypt (few records per key)"),
+    "k4e": ("AES-256-GCM", "TLS1.3", "encrypt", 16383, 1 << 18, 1 << 16,
+            "64K keys x 4 records, AES-256-GCM, records round-robin over keys, 16 KiB TLS 1.3 encrypt (k4 sent)"),
     "chacha16k": ("CHACHA20-POLY1305", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
                   "ChaCha20-Poly1305 decrypt, 1M x 16 KiB TLS 1.3 records, single key (the c4 ChaCha share)"),
     "c3d": ("CHACHA20-POLY1305", "TLS1.3", "decrypt", 1400, 1 << 20, 1,
