@@ -1,0 +1,98 @@
+/*
+ * tlsrec_clmul.h -- GF(2^128) multiply of two variable elements in the GCM
+ * convention (SP 800-38D 6.3) on 32-bit integer arithmetic, no tables: a
+ * carry-less 32x32 -> 64 product from four integer multiplies per bit class
+ * ("holes" every fourth bit keep the integer carries out of the bits that are
+ * read), Karatsuba 128 = 2 x 64 = 4 x 32 (nine 32-bit products), and the
+ * reduction by x^128 + x^7 + x^2 + x + 1.
+ *
+ * Host and device: the kernels use it where a power of H is needed whose
+ * position table is not in LDS; gcc builds it for the CPU test
+ * (tests/c/clmul_check.c against the oracle's bitwise orc_gf128_mul).
+ * Blocks are the 16-byte GCM strings as four little-endian words (the
+ * kernels' uint4 layout).
+ */
+#ifndef TLSREC_CLMUL_H
+#define TLSREC_CLMUL_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define TLSREC_CLMUL_FN __host__ __device__ __forceinline__
+#else
+#define TLSREC_CLMUL_FN static inline
+#endif
+
+/* carry-less 32 x 32 -> 64: bit class c of x (bits = c mod 4) times bit
+ * class d of y lands on class c + d; at most 8 terms meet at a bit, so their
+ * integer sum stays below 16 and never carries into the next bit of the
+ * same class */
+TLSREC_CLMUL_FN uint64_t tlsrec_clmul32(uint32_t x, uint32_t y)
+{
+    const uint64_t x0 = x & 0x11111111u, x1 = x & 0x22222222u, x2 = x & 0x44444444u, x3 = x & 0x88888888u;
+    const uint64_t y0 = y & 0x11111111u, y1 = y & 0x22222222u, y2 = y & 0x44444444u, y3 = y & 0x88888888u;
+    const uint64_t z0 = (x0 * y0) ^ (x1 * y3) ^ (x2 * y2) ^ (x3 * y1);
+    const uint64_t z1 = (x0 * y1) ^ (x1 * y0) ^ (x2 * y3) ^ (x3 * y2);
+    const uint64_t z2 = (x0 * y2) ^ (x1 * y1) ^ (x2 * y0) ^ (x3 * y3);
+    const uint64_t z3 = (x0 * y3) ^ (x1 * y2) ^ (x2 * y1) ^ (x3 * y0);
+    return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) | (z2 & 0x4444444444444444ull) |
+           (z3 & 0x8888888888888888ull);
+}
+
+/* GCM bytes (little-endian word of bytes 4k..4k+3) <-> polynomial word k
+ * (bit j = coefficient of x^(32k+j)): reverse the bits of each byte */
+TLSREC_CLMUL_FN uint32_t tlsrec_brev8x4(uint32_t w)
+{
+    w = ((w >> 1) & 0x55555555u) | ((w & 0x55555555u) << 1);
+    w = ((w >> 2) & 0x33333333u) | ((w & 0x33333333u) << 2);
+    w = ((w >> 4) & 0x0F0F0F0Fu) | ((w & 0x0F0F0F0Fu) << 4);
+    return w;
+}
+
+/* 64 x 64 -> 128 (Karatsuba over 32-bit halves); a, b: 2 words, r: 4 words */
+TLSREC_CLMUL_FN void tlsrec_clmul64(const uint32_t a[2], const uint32_t b[2], uint32_t r[4])
+{
+    const uint64_t lo = tlsrec_clmul32(a[0], b[0]);
+    const uint64_t hi = tlsrec_clmul32(a[1], b[1]);
+    const uint64_t mid = tlsrec_clmul32(a[0] ^ a[1], b[0] ^ b[1]) ^ lo ^ hi;
+    r[0] = (uint32_t) lo;
+    r[1] = (uint32_t) (lo >> 32) ^ (uint32_t) mid;
+    r[2] = (uint32_t) hi ^ (uint32_t) (mid >> 32);
+    r[3] = (uint32_t) (hi >> 32);
+}
+
+/* x * y in GF(2^128), GCM strings as little-endian words */
+TLSREC_CLMUL_FN void tlsrec_gf128_mul(const uint32_t x[4], const uint32_t y[4], uint32_t out[4])
+{
+    uint32_t a[4], b[4];
+    for (int i = 0; i < 4; i++) {
+        a[i] = tlsrec_brev8x4(x[i]);
+        b[i] = tlsrec_brev8x4(y[i]);
+    }
+    /* 128 x 128 -> 256, Karatsuba over 64-bit halves */
+    uint32_t l[4], h[4], m[4];
+    tlsrec_clmul64(a, b, l);
+    tlsrec_clmul64(a + 2, b + 2, h);
+    const uint32_t as[2] = { a[0] ^ a[2], a[1] ^ a[3] }, bs[2] = { b[0] ^ b[2], b[1] ^ b[3] };
+    tlsrec_clmul64(as, bs, m);
+    uint32_t c[8];
+    for (int i = 0; i < 4; i++) {
+        m[i] ^= l[i] ^ h[i];
+        c[i] = l[i];
+        c[4 + i] = h[i];
+    }
+    for (int i = 0; i < 4; i++) c[2 + i] ^= m[i];
+    /* reduce: x^128 = x^7 + x^2 + x + 1; H = c[4..7] (degree <= 126) */
+    uint32_t r[4];
+    for (int i = 0; i < 4; i++) {
+        const uint32_t hp = i ? c[3 + i] : 0u;       /* word below, for the carries of the shifts */
+        r[i] = c[i] ^ c[4 + i] ^ (c[4 + i] << 1) ^ (hp >> 31) ^ (c[4 + i] << 2) ^ (hp >> 30) ^ (c[4 + i] << 7) ^
+               (hp >> 25);
+    }
+    /* the bits the shifts moved past x^127, folded once more (degree < 14) */
+    const uint32_t o = (c[7] >> 31) ^ (c[7] >> 30) ^ (c[7] >> 25);
+    r[0] ^= o ^ (o << 1) ^ (o << 2) ^ (o << 7);
+    for (int i = 0; i < 4; i++) out[i] = tlsrec_brev8x4(r[i]);
+}
+
+#endif /* TLSREC_CLMUL_H */

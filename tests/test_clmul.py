@@ -1,0 +1,48 @@
+"""CPU test of the table-free GF(2^128) multiply (mbedtls_amd/csrc/tlsrec_clmul.h):
+tests/c/libclmul_check.so (gcc) against the oracle's bitwise orc_gf128_mul
+(the GCM multiply of SP 800-38D 6.3) on random and edge operands, the
+identity element and commutativity."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from tests.prng import prng_bytes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tests", "c", "libclmul_check.so")
+
+
+@pytest.fixture(scope="module")
+def libs():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c"), "libclmul_check.so"], check=True)
+    c = ctypes.CDLL(LIB)
+    import oracle as O
+    return c, O
+
+
+def _mul(lib, fn, x, y):
+    if fn == "orc_gf128_mul":
+        return lib.gf128_mul(x, y)
+    out = ctypes.create_string_buffer(16)
+    getattr(lib, fn)(x, y, out)
+    return out.raw
+
+
+def test_clmul_vs_oracle(libs):
+    c, o = libs
+    edge = [bytes(16), b"\x80" + bytes(15), bytes(15) + b"\x01", b"\xff" * 16, b"\x01" + bytes(15)]
+    vals = edge + [prng_bytes(9100 + i, 16) for i in range(400)]
+    for i, x in enumerate(vals):
+        y = vals[(7 * i + 3) % len(vals)]
+        assert _mul(c, "clmul_check_mul", x, y) == _mul(o, "orc_gf128_mul", x, y), (x.hex(), y.hex())
+
+
+def test_clmul_identity_and_commutes(libs):
+    c, _ = libs
+    one = b"\x80" + bytes(15)          # the GCM string of the polynomial 1
+    for i in range(50):
+        x, y = prng_bytes(9600 + i, 16), prng_bytes(9700 + i, 16)
+        assert _mul(c, "clmul_check_mul", x, one) == x
+        assert _mul(c, "clmul_check_mul", x, y) == _mul(c, "clmul_check_mul", y, x)
