@@ -247,6 +247,16 @@ static uint32_t gcm_g5(void)
     return (e && atoi(e) == 0) ? 0u : 1u;
 }
 
+/* 16-lane wave passes: the lane tree by table-free multiplies (tlsrec_clmul.h)
+ * instead of the key's H^8 / H^4 / H^2 / H^1 tables from HBM (24 KiB more per
+ * key pass).  Same-box: k4 455 -> 461 GiB/s, stream 4 x 16 KiB per key
+ * receive 424/429 -> 432/432.  TLSREC_GCM_TREEMUL=0 selects the tables. */
+static uint32_t gcm_tm(void)
+{
+    const char *e = getenv("TLSREC_GCM_TREEMUL");
+    return (e && atoi(e) == 0) ? 0u : 1u;
+}
+
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */
 static uint32_t gcm_lanes_env(void)
 {
@@ -477,6 +487,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         a.g5 = gcm_g5();
+        a.tm = gcm_tm();
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
@@ -506,6 +517,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.capacity = cap;
         a.cipher = (uint32_t) c;
         a.g5 = 0;
+        a.tm = 0;
         const uint64_t per_wg = (uint64_t) ARIA_GCM_WAVES * a.rpw;
         const uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_alt_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)

@@ -14,6 +14,7 @@
 #include <type_traits>
 
 #include "tlsrec.h"
+#include "tlsrec_clmul.h"
 #include "tlsrec_device.h"
 #include "tlsrec_frame.h"
 #include "tlsrec_internal.h"
@@ -89,6 +90,30 @@ __device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, cons
     if (p.aad_len > 32) f = xor4(gmul<0>(gp, f), cid_aad_block<2, 0>(p, d, cid));
     if (p.aad_len > 48) f = xor4(gmul<0>(gp, f), cid_aad_block<3, 0>(p, d, cid));
     return f;
+}
+
+/* The lane tree with table-free multiplies (tlsrec_clmul.h) by the powers
+ * P[k] = H^(2^k) held as values: for the wave passes, whose per-record tables
+ * otherwise come from HBM (a key's H^8, H^4, H^2 tables, 24 KiB, for 4
+ * records of 16 KiB at L = 16). */
+__device__ __forceinline__ uint4 gf_mul_v(uint4 x, uint4 p)
+{
+    const uint32_t a[4] = { x.x, x.y, x.z, x.w }, b[4] = { p.x, p.y, p.z, p.w };
+    uint32_t r[4];
+    tlsrec_gf128_mul(a, b, r);
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+template <int SH>
+__device__ __forceinline__ uint4 gtree_v(const uint4 (&P)[4], uint4 Y, int lane, int q)
+{
+    if constexpr (SH >= 1) {
+        uint4 o = shfl4(Y, (lane + SH) & 63);
+        if (q < SH) Y = xor4(gf_mul_v(Y, P[Log2<SH>::v]), o);
+        return gtree_v<SH / 2>(P, Y, lane, q);
+    } else {
+        return Y;
+    }
 }
 
 /* lanes q < SH: Y_q = Y_q * H^SH ^ Y_(q+SH); leaves sum_q Y_q H^(2SH-1-q) in q = 0.
@@ -371,7 +396,20 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
             }
             /* tree: sum_q Y_q H^(L-q) */
-            Y = gtree<L / 2>(gp, Y, lane, q);
+            if constexpr (WP && L == 16) {
+                if (a.tm) {
+                    const SlotState &ss = a.slots[s];
+                    const uint4 P[4] = { *reinterpret_cast<const uint4 *>(ss.h),
+                                         make_uint4(ss.hpow[0][0], ss.hpow[0][1], ss.hpow[0][2], ss.hpow[0][3]),
+                                         make_uint4(ss.hpow[1][0], ss.hpow[1][1], ss.hpow[1][2], ss.hpow[1][3]),
+                                         make_uint4(ss.hpow[2][0], ss.hpow[2][1], ss.hpow[2][2], ss.hpow[2][3]) };
+                    Y = gtree_v<L / 2>(P, Y, lane, q);
+                } else {
+                    Y = gtree<L / 2>(gp, Y, lane, q);
+                }
+            } else {
+                Y = gtree<L / 2>(gp, Y, lane, q);
+            }
             if (q == 0) {                                            /* the group leader's sum */
                 Y = gmul<0>(gp, Y);                                  /* T */
                 uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
