@@ -27,7 +27,8 @@ namespace tlsrec {
  * ==================================================================== */
 /* WP (wave passes): each wave keeps only its current key's H^L table in its
  * own 8 KiB of LDS; the once-per-record multiplies (AAD fold, tree, final)
- * read the key's tables in global memory. */
+ * read the key's tables in global memory -- except the 16-lane tree, which
+ * multiplies by H^8 .. H^1 held as values (gtree_v, GcmArgs::tm). */
 /* G5: the Horner table H^L is the 13 KiB 5-bit form (gmul5) after the tree's
  * 4-bit tables H^1 .. H^(L/2). */
 template <int L, int W, bool WP = false, bool G5 = false>
