@@ -573,6 +573,13 @@ __device__ __forceinline__ uint32_t ks_slot(uint32_t c, uint32_t g)
     return 4u * c + ((g + (c >> 1)) & 3u);
 }
 
+/* the half-size exchange row (two slots per lane): lanes c .. c+7 of a
+ * ds_write_b128 group land on 8 distinct 16-byte bank quads */
+__device__ __forceinline__ uint32_t ks_half(uint32_t c, uint32_t g)
+{
+    return 2u * c + ((g + (c >> 2)) & 1u);
+}
+
 /*
  * ChaCha20-Poly1305 record kernel (RFC 8439 2.8 around the framing plan).
  *
@@ -599,7 +606,12 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
     constexpr int R = 64 / L;
     constexpr int LOGL = Log2<L>::v;
     __shared__ CpRec crec[CP_WAVES][64];
-    __shared__ uint4 kst[CP_WAVES][256];                  /* keystream exchange, 4 KiB per wave */
+    /* keystream exchange: 4 KiB per wave, or (L <= 2) 2 KiB in two phases --
+     * a lane's reads then need only half its block's slots at a time, and the
+     * workgroup's 50 KiB of LDS let three workgroups (12 waves, the VGPR bound)
+     * share a CU instead of two */
+    constexpr bool SPLIT = L <= 2;
+    __shared__ uint4 kst[CP_WAVES][SPLIT ? 128 : 256];
     __shared__ uint32_t cidf[CP_WAVES][CID ? 64 : 1][5];   /* CID: AAD blocks Horner-folded */
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane / L, q = lane % L;
@@ -661,9 +673,17 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
     uint32_t kw[4], kr[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-        kw[t] = ks_slot((uint32_t) lane, (uint32_t) t);
         const uint32_t u = (uint32_t) (L * t + q);
-        kr[t] = ks_slot((uint32_t) (lane - q) + u / 4, u % 4);
+        if constexpr (SPLIT) {
+            /* slot t of a lane's block goes out in phase t >> 1; the slot a
+             * lane reads for t, u % 4 of lane (lane - q + u / 4), comes in
+             * phase (u % 4) >> 1: t even / odd at L = 2, t < 2 / >= 2 at L = 1 */
+            kw[t] = ks_half((uint32_t) lane, (uint32_t) t & 1u);
+            kr[t] = ks_half((uint32_t) (lane - q) + u / 4, (u % 4) & 1u);
+        } else {
+            kw[t] = ks_slot((uint32_t) lane, (uint32_t) t);
+            kr[t] = ks_slot((uint32_t) (lane - q) + u / 4, u % 4);
+        }
     }
 
     for (uint32_t rr = 0; rr < a.rpw; rr += R) {
@@ -741,13 +761,27 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
             uint32_t ks[16];
             chacha_block_kn(cr.key, L * j - z + (uint32_t) q + 1u, ks);
             asm volatile("" ::: "memory");   /* after the previous step's reads */
+            if constexpr (SPLIT) {
 #pragma unroll
-            for (int t = 0; t < 4; t++)
-                krow[kw[t]] = make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]);
-            /* other lanes' writes: same wave, in-order LDS queue */
-            asm volatile("" ::: "memory");
+                for (int ph = 0; ph < 2; ph++) {
 #pragma unroll
-            for (int t = 0; t < 4; t++) K[t] = krow[kr[t]];
+                    for (int t = 2 * ph; t < 2 * ph + 2; t++)
+                        krow[kw[t]] = make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]);
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+                        if ((L == 1 ? t >> 1 : t & 1) == ph) K[t] = krow[kr[t]];   /* ((L t + q) % 4) >> 1 */
+                    asm volatile("" ::: "memory");   /* phase 1 writes after phase 0 reads (in-order queue) */
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    krow[kw[t]] = make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3]);
+                /* other lanes' writes: same wave, in-order LDS queue */
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int t = 0; t < 4; t++) K[t] = krow[kr[t]];
+            }
         };
 
         /* general step: any step (front padding, the AAD fold at block 0,
