@@ -253,8 +253,9 @@ static uint32_t gcm_g5(void)
  * receive 424/429 -> 432/432.  TLSREC_GCM_TREEMUL=0 selects the tables. */
 static uint32_t gcm_tm(void)
 {
+    /* bit 0: 16-lane wave passes (default on); bit 1: 2- and 4-lane ones */
     const char *e = getenv("TLSREC_GCM_TREEMUL");
-    return (e && atoi(e) == 0) ? 0u : 1u;
+    return e ? (uint32_t) atoi(e) & 3u : 1u;
 }
 
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */

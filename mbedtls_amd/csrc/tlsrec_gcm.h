@@ -397,8 +397,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
             }
             /* tree: sum_q Y_q H^(L-q) */
-            if constexpr (WP && L == 16) {
-                if (a.tm) {
+            if constexpr (WP && (L == 16 || L == 4 || L == 2)) {
+                if (a.tm & (L == 16 ? 1u : 2u)) {
                     const SlotState &ss = a.slots[s];
                     const uint4 P[4] = { *reinterpret_cast<const uint4 *>(ss.h),
                                          make_uint4(ss.hpow[0][0], ss.hpow[0][1], ss.hpow[0][2], ss.hpow[0][3]),
