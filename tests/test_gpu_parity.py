@@ -263,6 +263,20 @@ def test_gcm_wave_pass(lanes, monkeypatch):
     ChaCha, both TLS versions, ragged lengths incl. the edge list, tampered
     records -- bit-exact vs the oracle in both directions."""
     monkeypatch.setenv("TLSREC_GCM_WP", "1")
+    _wave_pass_case(lanes)
+
+
+@pytest.mark.parametrize("lanes,tm", [(16, "0"), (4, "3"), (2, "3")])
+def test_gcm_wave_pass_lane_tree(lanes, tm, monkeypatch):
+    """The wave passes' lane tree both ways: from the key's HBM tables at 16
+    lanes (TLSREC_GCM_TREEMUL=0; table-free is the default there) and by
+    table-free multiplies at 4 and 2 lanes (=3; tables are the default)."""
+    monkeypatch.setenv("TLSREC_GCM_WP", "1")
+    monkeypatch.setenv("TLSREC_GCM_TREEMUL", tm)
+    _wave_pass_case(lanes)
+
+
+def _wave_pass_case(lanes):
     nkeys = 200
     slots = B.random_slots(777 + lanes, [M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_AES_192_GCM,
                                          M.CIPHER_CHACHA20_POLY1305],
