@@ -400,7 +400,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             if constexpr (WP && (L == 16 || L == 4 || L == 2)) {
                 if (a.tm & (L == 16 ? 1u : 2u)) {
                     const SlotState &ss = a.slots[s];
-                    const uint4 P[4] = { *reinterpret_cast<const uint4 *>(ss.h),
+                    uint4 h1;
+                    __builtin_memcpy(&h1, ss.h, 16);                 /* H: bytes at a 4-byte-aligned offset */
+                    const uint4 P[4] = { h1,
                                          make_uint4(ss.hpow[0][0], ss.hpow[0][1], ss.hpow[0][2], ss.hpow[0][3]),
                                          make_uint4(ss.hpow[1][0], ss.hpow[1][1], ss.hpow[1][2], ss.hpow[1][3]),
                                          make_uint4(ss.hpow[2][0], ss.hpow[2][1], ss.hpow[2][2], ss.hpow[2][3]) };
