@@ -364,7 +364,7 @@ def end_to_end(M, kt, recs, arena, out_arena, n, stride, lead, head, content, wi
         d["data_offset"] = 0
         d["data_len"] = wire
     res = M.results(E)
-    chunk = 64 << 20
+    chunk = int(os.environ.get("BENCH_E2E_CHUNK_MB", "64")) << 20    # pipeline chunk (measurement override)
     dec = direction == "decrypt"
     M.host_batch(dec, kt, d, res, E, host_in, host_out, chunk_bytes=chunk)      # warm-up
     best = None
