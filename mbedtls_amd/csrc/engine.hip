@@ -342,7 +342,8 @@ extern "C" void tlsrec__scratch_release(tlsrec_scratch_lease *lease)
 /* Device scratch of one bucketed batch (the stream's kind-0 scratch). */
 struct BucketScratch {
     tlsrec_scratch_lease lease = { nullptr, nullptr };
-    uint32_t *counts, *offs, *cursor, *perm;
+    uint32_t *counts, *offs, *perm;
+    uint2 *keyrank;
     void *scan_tmp;
     size_t scan_bytes;
 };
@@ -359,15 +360,16 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     const size_t al = 256;
     const size_t szk = (nk * 4 + al - 1) / al * al, szp = ((size_t) n * 4 + al - 1) / al * al;
-    const size_t total = 3 * szk + szp + b.scan_bytes + al;
+    const size_t szr = ((size_t) n * 8 + al - 1) / al * al;
+    const size_t total = 2 * szk + szp + szr + b.scan_bytes + al;
     const int lr = tlsrec__scratch_acquire(st, 0, total, &b.lease);
     if (lr) return lr;
     uint8_t *m = (uint8_t *) b.lease.mem;
     b.counts = (uint32_t *) m;
     b.offs = (uint32_t *) (m + szk);
-    b.cursor = (uint32_t *) (m + 2 * szk);
-    b.perm = (uint32_t *) (m + 3 * szk);
-    b.scan_tmp = m + 3 * szk + szp;
+    b.perm = (uint32_t *) (m + 2 * szk);
+    b.keyrank = (uint2 *) (m + 2 * szk + szp);
+    b.scan_tmp = m + 2 * szk + szp + szr;
     BucketArgs a;
     a.slots = kt->d_slots;
     a.cipher_of = kt->d_cipher;
@@ -377,7 +379,7 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     a.capacity = kt->capacity;
     a.counts = b.counts;
     a.offs = b.offs;
-    a.cursor = b.cursor;
+    a.keyrank = b.keyrank;
     a.nk = (uint32_t) nk;
     a.perm = b.perm;
     if (tlsrec__launch_bucket_zero(&a, st) != hipSuccess ||

@@ -92,7 +92,7 @@ struct BucketArgs {
     uint32_t capacity;
     uint32_t *counts;         /* [nk = 10 * capacity + 2] records per (class, slot) */
     const uint32_t *offs;     /* [nk] their exclusive prefix sums (class start in perm) */
-    uint32_t *cursor;         /* [nk] records placed so far, from zero (the scatter) */
+    uint2 *keyrank;           /* [n] each record's (key, rank within its key) from the count pass */
     uint32_t nk;
     uint32_t *perm;           /* [n] */
 };
