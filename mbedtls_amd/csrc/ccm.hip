@@ -77,7 +77,9 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             const uint32_t s = a.recs[my_rec].slot;
             const bool usable = s < a.capacity && a.slots[s].km.cipher != 0;
             const int c = usable ? a.slots[s].km.cipher : 0;   /* no read past the table */
-            if (usable && (ARIA ? tlsrec_cipher_is_alt_ccm(c) && tlsrec_cipher_alt_nr(c) == NR
+            if (my_rec == a.skip) {
+                /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
+            } else if (usable && (ARIA ? tlsrec_cipher_is_alt_ccm(c) && tlsrec_cipher_alt_nr(c) == NR
                                 : tlsrec_cipher_is_ccm(c) && tlsrec_cipher_nr(c) == NR))
                 my_slot = s;
             else if (!a.perm && !usable && a.flag_nr == (ARIA ? 100u + NR : (uint32_t) NR))

@@ -278,6 +278,7 @@ static uint32_t pick_rpw(uint64_t n, uint32_t waves_per_wg, uint32_t R, uint32_t
 struct ScratchEntry {
     int device;
     hipStream_t stream;
+    uintptr_t thread;         /* hipStreamPerThread: the calling thread (its own real stream) */
     int kind;
     void *mem;
     size_t bytes;
@@ -291,9 +292,14 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    /* one handle, one ordered queue -- except hipStreamPerThread, which names
+     * a different real stream in every thread: two threads' batches on it run
+     * unordered on the GPU, so each thread gets its own scratch (the null
+     * stream is one queue for every thread and needs nothing) */
+    const uintptr_t thr = st == hipStreamPerThread ? (uintptr_t) pthread_self() : 0;
     pthread_mutex_lock(&g_scratch_mu);
     ScratchEntry *e = g_scratch;
-    while (e && !(e->device == dev && e->stream == st && e->kind == kind)) e = e->next;
+    while (e && !(e->device == dev && e->stream == st && e->thread == thr && e->kind == kind)) e = e->next;
     if (!e) {
         e = (ScratchEntry *) calloc(1, sizeof(*e));
         if (!e) {
@@ -302,6 +308,7 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
         }
         e->device = dev;
         e->stream = st;
+        e->thread = thr;
         e->kind = kind;
         pthread_mutex_init(&e->mu, NULL);
         e->next = g_scratch;
@@ -395,22 +402,36 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
 /* avg_bytes: mean record size when the caller knows it (the stream / DTLS
  * layers and the host pipeline do; 0 = unknown) -- it decides the GCM launch
  * for many keys with little work each (below). */
+/* test hook (tlsrec__test_skip_record): the AEAD kernels leave this record
+ * index unreached, so a test can show that its result stays INTERNAL_ERROR */
+static volatile uint32_t g_test_skip = 0xffffffffu;
+
+extern "C" void tlsrec__test_skip_record(uint32_t index) { g_test_skip = index; }
+
+/* prefilled: the caller already wrote INTERNAL_ERROR into every result (the
+ * single-record engine stages it with the record's upload) */
 static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
                  const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec, uint32_t only_cipher = 0,
-                 uint32_t avg_bytes = 0)
+                 uint32_t avg_bytes = 0, bool prefilled = false)
 {
     if (!kt || (!recs && n) || (!res && n)) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t) stream;
     const int cu = kt->cu;
     const uint32_t cmask = only_cipher ? (kt->cipher_mask & (1u << only_cipher)) : kt->cipher_mask;
+    const uint32_t skip = g_test_skip;
     /* A table holding a single key, or a batch of one record, needs no
      * grouping: the kernels walk the descriptors in order and flag records
      * naming an unusable slot.  Otherwise the bucket pass groups GCM records
-     * by key (then ChaCha). */
+     * by key (then ChaCha).  Either way every result reads INTERNAL_ERROR
+     * before the AEAD kernels run (the guard kernel, or the bucket count
+     * kernel), so a record that no kernel reaches fails closed -- the
+     * reference's auth_done check, ssl_msg.c:1260 / :1804. */
     BucketScratch bs;
     const bool identity = kt->nloaded == 1 || n == 1;
-    if (!identity) {
+    if (identity) {
+        if (!prefilled && tlsrec__launch_res_guard(res, n, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    } else {
         int r = bucket(kt, recs, res, n, st, bs);
         if (r) {
             tlsrec__scratch_release(&bs.lease);
@@ -491,6 +512,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.cipher = (uint32_t) cipher;
         a.g5 = gcm_g5();
         a.tm = gcm_tm();
+        a.skip = skip;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
@@ -521,6 +543,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.cipher = (uint32_t) c;
         a.g5 = 0;
         a.tm = 0;
+        a.skip = skip;
         const uint64_t per_wg = (uint64_t) ARIA_GCM_WAVES * a.rpw;
         const uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_gcm_aria(&a, dec, (int) tlsrec_cipher_alt_nr(c), (int) kt->has_cid, grid, st) != hipSuccess)
@@ -545,6 +568,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.capacity = cap;
         a.flag_nr = 0;
         a.cid = kt->has_cid;
+        a.skip = skip;
         if (tlsrec__launch_ccm(&a, dec, ccm_nr, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (!rc && (cmask & (1u << TLSREC_CIPHER_CHACHA20_POLY1305))) {
@@ -567,6 +591,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.rpw = pick_rpw(n, CP_WAVES, 64 / L, (uint32_t) cu * 4);
         a.capacity = cap;
         a.cid = kt->has_cid;
+        a.skip = skip;
         uint64_t per_wg = (uint64_t) CP_WAVES * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
@@ -981,12 +1006,21 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
             up += d.cid_len;
         }
         memcpy(c->h, &d, sizeof(d));
+        {
+            /* the result slot goes up with the record as INTERNAL_ERROR: only
+             * the kernel can turn it into a verdict (ssl_msg.c:1260 / :1804);
+             * otherwise the previous record's result would still be there */
+            tlsrec_batch_res g;
+            memset(&g, 0, sizeof(g));
+            g.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
+            memcpy(c->h + 64, &g, sizeof(g));
+        }
         if (buf_len) memcpy(c->h + 128, buf, buf_len);
         tlsrec_batch_rec *d_rec = (tlsrec_batch_rec *) c->d;
         tlsrec_batch_res *d_res = (tlsrec_batch_res *) (c->d + 64);
         hipError_t e = hipMemcpyAsync(c->d, c->h, up, hipMemcpyHostToDevice, c->st);
         if (e == hipSuccess) {
-            r = batch(kt, d_rec, d_res, 1, c->d + 128, c->d + 128, 0, c->st, dec, cipher);
+            r = batch(kt, d_rec, d_res, 1, c->d + 128, c->d + 128, 0, c->st, dec, cipher, 0, true);
             if (r == 0)
                 e = hipMemcpyAsync(c->h + 64, c->d + 64, 64 + buf_len, hipMemcpyDeviceToHost, c->st);
             if (e == hipSuccess) e = hipStreamSynchronize(c->st);

@@ -437,6 +437,31 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_zero_kernel(BucketArgs a)
     if (i < a.nk) a.counts[i] = 0;
 }
 
+/* Fail closed, as the reference's `auth_done != 1 -> INTERNAL_ERROR` check
+ * (ssl_msg.c:1260 encrypt, :1804 decrypt): before any AEAD kernel of a batch
+ * runs, every record's result reads INTERNAL_ERROR, and only the kernel that
+ * protects (or rejects) the record overwrites it.  A record no kernel reaches
+ * can never read as success, whatever the caller left in `res`.  The bucket
+ * count kernel writes the same sentinel for the records it groups; this one
+ * covers identity order. */
+__device__ __forceinline__ void unreached_result(tlsrec_batch_res *res)
+{
+    tlsrec_batch_res r;
+    r.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
+    r.data_offset = 0;
+    r.data_len = 0;
+    r.type = 0;
+    r.cid_len = 0;
+    r.reserved[0] = r.reserved[1] = 0;
+    *res = r;
+}
+
+__global__ __launch_bounds__(256) void tlsrec_res_guard_kernel(tlsrec_batch_res *res, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) unreached_result(&res[i]);
+}
+
 __global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
 {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -444,7 +469,10 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
     if (i < a.n) {
         const tlsrec_batch_rec d = a.recs[i];
         key = bucket_key(a, d);
-        if (key == 0xffffffffu) bad_slot_result(d, &a.res[i]);
+        if (key == 0xffffffffu)
+            bad_slot_result(d, &a.res[i]);
+        else
+            unreached_result(&a.res[i]);    /* the record's AEAD kernel overwrites it */
     }
     /* the count's old value is the record's rank within its key: the
      * scatter then needs no second round of atomics (with keys round-robin,
@@ -633,9 +661,10 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const tlsrec_batch_rec d = a.recs[my_rec];
-            if (!a.perm && !(d.slot < a.capacity && a.slots[d.slot].km.cipher != 0))
+            const bool reach = my_rec != a.skip;   /* test hook: the guard's INTERNAL_ERROR stays */
+            if (reach && !a.perm && !(d.slot < a.capacity && a.slots[d.slot].km.cipher != 0))
                 bad_slot_result(d, &a.res[my_rec]);
-            if (d.slot < a.capacity && a.slots[d.slot].km.cipher == TLSREC_CIPHER_CHACHA20_POLY1305) {
+            if (reach && d.slot < a.capacity && a.slots[d.slot].km.cipher == TLSREC_CIPHER_CHACHA20_POLY1305) {
                 mine = true;
                 const tlsrec_key_material km = a.slots[d.slot].km;
                 __builtin_memcpy(dm, &d, sizeof(dm));
@@ -1017,6 +1046,13 @@ extern "C" hipError_t tlsrec__launch_bucket_count(const BucketArgs *a, hipStream
 {
     if (a->n == 0) return hipSuccess;
     hipLaunchKernelGGL(tlsrec_bucket_count_kernel, dim3((a->n + 255) / 256), dim3(256), 0, st, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tlsrec_res_guard_kernel, dim3((n + 255) / 256), dim3(256), 0, st, res, n);
     return hipGetLastError();
 }
 

@@ -277,6 +277,19 @@ __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out 
     const uint64_t left = (uint64_t) si.in_len - src_off;
     const uint32_t len = left < f ? (uint32_t) left : f;
     const uint64_t pos = si.out_off + (uint64_t) k * (5 + out_body(sh, f));
+    /* a record whose sequence number would come after the counter wrapped is
+     * never protected: the reference stops with COUNTER_WRAPPING after the
+     * record that wraps it (:2749-2756), before encrypting anything under a
+     * reused sequence number (= a reused nonce).  No slot, no bytes. */
+    if ((uint64_t) k > ~be64(si.out_ctr)) {
+        if (lane == 0) {
+            tlsrec_batch_rec d;
+            memset(&d, 0, sizeof(d));
+            d.slot = NO_SLOT;
+            recs[j] = d;
+        }
+        return;
+    }
     const uint8_t *src = in + si.in_off + src_off;
     uint8_t *dst = out + pos + 5 + sh.head;
     const uint32_t nv = len / 16;
@@ -549,8 +562,24 @@ __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsr
 
 /* ssl_get_next_record over each connection's datagrams in arrival order, on
  * the decrypt results (one lane per connection). */
+/* A record the speculative pass decrypted but the in-order pass does not
+ * reach (after a fatal error, in the rest of a datagram dropped for a bad
+ * MAC, or a replay inside the batch): the reference never decrypts it, so its
+ * plaintext must not stay in the arena -- its content bytes are zeroed. */
+__device__ __forceinline__ void dtls_unreach_wipe(uint8_t *arena, const tlsrec_batch_rec *recs,
+                                                  const tlsrec_batch_res *res, const SlotState *slots, uint32_t kk)
+{
+    const tlsrec_batch_rec &d = recs[kk];
+    if (d.slot == NO_SLOT || res[kk].status != 0) return;
+    /* the whole decrypted AEAD region: content, and with a CID the inner type
+     * byte and padding (res.data_offset is past the explicit IV) */
+    const uint32_t end = d.data_offset + d.data_len - slots[d.slot].km.taglen;
+    uint8_t *b = arena + d.buf_off;
+    for (uint32_t x = res[kk].data_offset; x < end; x++) b[x] = 0;
+}
+
 __global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
-                                   const uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
+                                   uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
                                    const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
                                    const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
 {
@@ -571,15 +600,19 @@ __global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tl
             const int32_t stop = dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len,
                                            [&](const DtlsHdr &, const uint8_t *p) {
                 const uint32_t kk = k++;
-                if (st) { disp[kk] = TLSREC_DTLS_NOT_REACHED; return; }
-                if (dropped) { disp[kk] = TLSREC_DTLS_DROPPED; return; }
+                if (st) { disp[kk] = TLSREC_DTLS_NOT_REACHED; dtls_unreach_wipe(arena, recs, res, slots, kk); return; }
+                if (dropped) { disp[kk] = TLSREC_DTLS_DROPPED; dtls_unreach_wipe(arena, recs, res, slots, kk); return; }
                 const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
                 if (epoch != ci.in_epoch) {            /* :3755-3768, skipped after the handshake (:4727-4800) */
                     disp[kk] = epoch == (uint32_t) ci.in_epoch + 1 ? TLSREC_ERR_SSL_EARLY_MESSAGE
                                                                    : TLSREC_ERR_SSL_UNEXPECTED_RECORD;
                     return;
                 }
-                if (!w.fresh(p + 3)) { disp[kk] = TLSREC_ERR_SSL_UNEXPECTED_RECORD; return; }   /* :3769-3776 */
+                if (!w.fresh(p + 3)) {                 /* :3769-3776 */
+                    disp[kk] = TLSREC_ERR_SSL_UNEXPECTED_RECORD;
+                    dtls_unreach_wipe(arena, recs, res, slots, kk);
+                    return;
+                }
                 if (recs[kk].slot == NO_SLOT) {        /* not decrypted: impossible, the window only grows */
                     st = TLSREC_ERR_SSL_INTERNAL_ERROR;
                     disp[kk] = st;
@@ -694,6 +727,17 @@ __global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream
     const uint64_t left = (uint64_t) si.in_len - src_off;
     const uint32_t len = left < f ? (uint32_t) left : f;
     const uint64_t pos = si.out_off + (uint64_t) k * (hdr + dtls_body(sh, cid, f));
+    /* past the 48-bit wrap (:2741-2756): never protected, no bytes written --
+     * record k would reuse sequence number (epoch, k - wrap), i.e. a nonce */
+    if ((uint64_t) k > 0xFFFFFFFFFFFFull - ReplayWindow::seq48(si.out_ctr)) {
+        if (lane == 0) {
+            tlsrec_batch_rec d;
+            memset(&d, 0, sizeof(d));
+            d.slot = NO_SLOT;
+            recs[j] = d;
+        }
+        return;
+    }
     const uint8_t *src = in + si.in_off + src_off;
     uint8_t *dst = out + pos + hdr + sh.head;
     const uint32_t nv = len / 16;
@@ -961,7 +1005,7 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     }
     if (r == 0) {
         hipLaunchKernelGGL(dtls_finish_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                           ndgrams, (const uint8_t *) arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
+                           ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     tlsrec__scratch_release(&sc.lease);

@@ -173,7 +173,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const uint32_t s = a.recs[my_rec].slot;
-            if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
+            if (my_rec == a.skip) {
+                /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
+            } else if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
                 my_slot = s;
             } else if (!a.perm && !(s < a.capacity && a.slots[s].km.cipher != 0)) {
                 /* identity order: this kernel is the only one that sees the record */

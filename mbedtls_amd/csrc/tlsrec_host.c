@@ -156,6 +156,9 @@ static int run(int dec, tlsrec_transform *t, tlsrec_record *rec)
     d.cid_len = dec ? rec->cid_len : 0;
     int r = tlsrec__engine_run(dec, &d, rec->buf, rec->buf_len, rec->cid, &res);
     if (r != 0) return r;
+    /* no kernel reached the record: the staged INTERNAL_ERROR is returned and
+     * rec is left as it was (ssl_msg.c:1260 / :1804, auth_done != 1) */
+    if (res.status == TLSREC_ERR_SSL_INTERNAL_ERROR) return res.status;
     rec->data_offset = res.data_offset;
     rec->data_len = res.data_len;
     rec->type = res.type;

@@ -64,6 +64,7 @@ struct GcmArgs {
     uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM / _192_GCM */
     uint32_t g5;              /* host-side launch choice: 5-bit GHASH Horner table (8-lane, 16-wave kernel) */
     uint32_t tm;              /* 16-lane wave passes: lane tree by table-free multiplies (tlsrec_clmul.h) */
+    uint32_t skip;            /* test hook (tlsrec__test_skip_record): this record index is never reached */
 };
 
 struct CpArgs {
@@ -78,6 +79,7 @@ struct CpArgs {
     uint32_t rpw;
     uint32_t capacity;
     uint32_t cid;             /* the key table holds DTLS connection IDs: CID kernel variant */
+    uint32_t skip;            /* test hook, as GcmArgs::skip */
 };
 
 /* Bucket pass: key index of a record = AES-128-GCM slot, AES-256-GCM slot,
@@ -110,6 +112,7 @@ struct CcmArgs {
     uint32_t capacity;
     uint32_t flag_nr;         /* identity order: the launch (AES rounds) that flags unusable slots */
     uint32_t cid;             /* the key table holds DTLS connection IDs: CID kernel variant */
+    uint32_t skip;            /* test hook, as GcmArgs::skip */
 };
 
 } /* namespace tlsrec */
@@ -146,6 +149,8 @@ int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, t
 hipError_t tlsrec__launch_bucket_zero(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_count(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_t st);
+/* every result of a batch to INTERNAL_ERROR before its AEAD kernels (fail closed, kernels.hip) */
+hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st);
 }
 
 #endif

@@ -84,6 +84,10 @@ def lib():
                                         ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         L.orc_bench_records.restype = ctypes.c_double
+        L.orc_bench_records_multi.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                              ctypes.c_void_p]
+        L.orc_bench_records_multi.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -615,6 +619,20 @@ def evp_lib():
                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         L.evp_bench_records.restype = ctypes.c_double
+        L.evp_mixed_create.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.evp_mixed_create.restype = ctypes.c_void_p
+        L.evp_mixed_free.argtypes = [ctypes.c_void_p]
+        L.evp_mixed_free.restype = None
+        L.evp_mixed_records.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        L.evp_mixed_records.restype = ctypes.c_double
+        L.evp_call_profile.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.evp_call_profile.restype = ctypes.c_int
+        L.evp_check_records.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_void_p]
+        L.evp_check_records.restype = ctypes.c_int
         _evp = L
     return _evp
 
@@ -632,3 +650,80 @@ def evp_bench(cipher: int, tls_version: int, key: bytes, iv: bytes, direction: i
     return evp_lib().evp_bench_records(cipher, int(tls_version == TLS1_3), bytes(key), bytes(iv), direction,
                                        arena.ctypes.data, stride, data_len, n, seq0, threads,
                                        status.ctypes.data)
+
+
+def bench_multi(transforms, direction: int, arena, stride: int, data_len: int, n: int, threads: int,
+                status) -> float:
+    """Time orc_bench_records_multi: record i under transforms[i % len],
+    sequence number i // len, one thread per connection subset.  Seconds."""
+    arr = (ctypes.c_void_p * len(transforms))(*[ctypes.addressof(t._mem) for t in transforms])
+    return lib().orc_bench_records_multi(arr, len(transforms), direction, arena.ctypes.data, stride, data_len, n,
+                                         threads, status.ctypes.data)
+
+
+class EvpMixed:
+    """evp_mixed_*: one OpenSSL EVP context per connection (the c4 / c4s CPU
+    leg).  ciphers: uint8 array (AES_128_GCM / AES_256_GCM / CHACHA20_POLY1305
+    per connection), keys (n, 32), ivs (n, 12) uint8 arrays."""
+
+    def __init__(self, ciphers, keys, ivs, tls_version):
+        import numpy as np
+        c = np.ascontiguousarray(ciphers, dtype=np.uint8)
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(len(c), 32)
+        v = np.ascontiguousarray(ivs, dtype=np.uint8).reshape(len(c), 12)
+        if not set(np.unique(c).tolist()) <= set(EVP_CIPHERS):
+            raise ValueError("EvpMixed: AES-128/256-GCM and ChaCha20-Poly1305 only")
+        self._h = evp_lib().evp_mixed_create(len(c), c.ctypes.data, k.ctypes.data, v.ctypes.data,
+                                              int(tls_version == TLS1_3))
+        if not self._h:
+            raise RuntimeError("evp_mixed_create failed")
+
+    def run(self, direction: int, arena, stride: int, data_len: int, n: int, threads: int, status) -> float:
+        return evp_lib().evp_mixed_records(self._h, direction, arena.ctypes.data, stride, data_len, n, threads,
+                                           status.ctypes.data)
+
+    def close(self):
+        if self._h:
+            evp_lib().evp_mixed_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def evp_call_profile(cipher: int, length: int, iters: int = 20000):
+    """Microseconds per record spent in each EVP call of the EVP leg:
+    {init_aad, update, final, tag} (evp_call_profile in evp_bench.c)."""
+    out = (ctypes.c_double * 4)()
+    if evp_lib().evp_call_profile(cipher, length, iters, out) != 0:
+        return None
+    return {"init_aad_us": round(out[0], 3), "update_us": round(out[1], 3), "final_us": round(out[2], 3),
+            "tag_us": round(out[3], 3)}
+
+
+def evp_check_records(mode: int, cipher: int, tls_version: int, keys, ivs, keyidx, seq, off, lengths, plain,
+                      got=None, threads: int = 8):
+    """Bulk EVP check of variable-length records (evp_check_records in
+    evp_bench.c): mode 0 seals `plain` in place, mode 1 compares `got` (GPU
+    encrypt output) with EVP's seal of `plain`, mode 2 compares the content of
+    `got` (GPU decrypt output) with `plain`.  Returns the per-record int32
+    result (0 = match / status 0)."""
+    import numpy as np
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    ivs = np.ascontiguousarray(ivs, dtype=np.uint8)
+    keyidx = np.ascontiguousarray(keyidx, dtype=np.uint32)
+    seq = np.ascontiguousarray(seq, dtype=np.uint64)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = len(off)
+    res = np.zeros(n, dtype=np.int32)
+    g = got.ctypes.data if got is not None else None
+    r = evp_lib().evp_check_records(mode, cipher, int(tls_version == TLS1_3), len(keys), keys.ctypes.data,
+                                    ivs.ctypes.data, n, keyidx.ctypes.data, seq.ctypes.data, off.ctypes.data,
+                                    lengths.ctypes.data, plain.ctypes.data, g, threads, res.ctypes.data)
+    if r != 0:
+        raise RuntimeError("evp_check_records failed")
+    return res

@@ -19,6 +19,7 @@
 #define _POSIX_C_SOURCE 200809L
 #include <openssl/evp.h>
 #include <pthread.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 #include <time.h>
@@ -46,97 +47,100 @@ static const EVP_CIPHER *eb_cipher(int c)
     }
 }
 
+/* One record through an EVP context that already holds its connection's key:
+ * the framing of mbedtls_ssl_encrypt_buf / _decrypt_buf around one AEAD. */
+static int32_t eb_record(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, const uint8_t *iv, uint8_t *buf,
+                         size_t data_len, uint64_t seq)
+{
+    const int explicit_iv = !tls13 && cipher != EB_CHACHA20_POLY1305;   /* ivlen != fixed_ivlen, :739-743 */
+    uint8_t ctr[8], nonce[12], aad[13];
+    for (int k = 7; k >= 0; k--) { ctr[k] = (uint8_t) seq; seq >>= 8; }
+    /* ssl_build_record_nonce: fixed IV ^ (0^4 || seq), or iv4 || seq (TLS 1.2 GCM) */
+    if (explicit_iv) {
+        memcpy(nonce, iv, 4);
+        memcpy(nonce + 4, ctr, 8);
+    } else {
+        memcpy(nonce, iv, 12);
+        for (int k = 0; k < 8; k++) nonce[4 + k] ^= ctr[k];
+    }
+    int ok;
+    int outl = 0;
+    if (dir) {
+        /* encrypt: content at buf[off], TLS 1.3 inner plaintext = content || 23 || 0^pad */
+        size_t off = explicit_iv ? 8 : 0, len = data_len;
+        uint8_t *p = buf + off;
+        if (tls13) {
+            p[len++] = 23;
+            size_t pad = (16 - len % 16) % 16;
+            memset(p + len, 0, pad);
+            len += pad;
+        }
+        size_t aadlen;
+        if (tls13) {
+            const size_t l = len + 16;
+            aad[0] = 23; aad[1] = 3; aad[2] = 3; aad[3] = (uint8_t) (l >> 8); aad[4] = (uint8_t) l;
+            aadlen = 5;
+        } else {
+            memcpy(aad, ctr, 8);
+            aad[8] = 23; aad[9] = 3; aad[10] = 3; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
+            aadlen = 13;
+        }
+        ok = EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 1) == 1 &&
+             EVP_CipherUpdate(ctx, NULL, &outl, aad, (int) aadlen) == 1 &&
+             EVP_CipherUpdate(ctx, p, &outl, p, (int) len) == 1 &&
+             EVP_CipherFinal_ex(ctx, p + len, &outl) == 1 &&
+             EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, 16, p + len) == 1;
+        if (explicit_iv) memcpy(buf, ctr, 8);
+        return ok ? 0 : -1;
+    }
+    /* decrypt: record body at buf[0] (explicit IV first for TLS 1.2 GCM) */
+    size_t off = explicit_iv ? 8 : 0;
+    if (data_len < off + 16) return -0x7180;
+    size_t len = data_len - off - 16;
+    uint8_t *p = buf + off;
+    if (explicit_iv) memcpy(nonce + 4, buf, 8);
+    size_t aadlen;
+    if (tls13) {
+        const size_t l = len + 16;
+        aad[0] = 23; aad[1] = 3; aad[2] = 3; aad[3] = (uint8_t) (l >> 8); aad[4] = (uint8_t) l;
+        aadlen = 5;
+    } else {
+        memcpy(aad, ctr, 8);
+        aad[8] = 23; aad[9] = 3; aad[10] = 3; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
+        aadlen = 13;
+    }
+    ok = EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 0) == 1 &&
+         EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_TAG, 16, p + len) == 1 &&
+         EVP_CipherUpdate(ctx, NULL, &outl, aad, (int) aadlen) == 1 &&
+         EVP_CipherUpdate(ctx, p, &outl, p, (int) len) == 1 &&
+         EVP_CipherFinal_ex(ctx, p + len, &outl) == 1;
+    if (!ok) {
+        memset(p, 0, len);                 /* PSA wipes the output on a bad tag */
+        return -0x7180;                    /* MBEDTLS_ERR_SSL_INVALID_MAC */
+    }
+    if (tls13) {
+        /* ssl_parse_inner_plaintext: strip zero padding, recover the type */
+        size_t k = len;
+        while (k > 0 && p[k - 1] == 0) k--;
+        return k == 0 ? -0x7200 : 0;
+    }
+    return 0;
+}
+
 static void *eb_worker(void *arg)
 {
     eb_job *j = (eb_job *) arg;
     EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
     const EVP_CIPHER *ev = eb_cipher(j->cipher);
-    const int explicit_iv = !j->tls13 && j->cipher != EB_CHACHA20_POLY1305;   /* ivlen != fixed_ivlen, :739-743 */
     /* the connection's key, set once (psa_import_key at transform setup) */
     if (!ctx || !ev || EVP_CipherInit_ex(ctx, ev, NULL, j->key, NULL, j->dir) != 1) {
         for (uint64_t i = j->lo; i < j->hi; i++) j->status[i] = -1;
         EVP_CIPHER_CTX_free(ctx);
         return NULL;
     }
-    for (uint64_t i = j->lo; i < j->hi; i++) {
-        uint8_t *buf = j->arena + i * j->stride;
-        uint8_t ctr[8], nonce[12], aad[13];
-        uint64_t s = j->seq0 + i;
-        for (int k = 7; k >= 0; k--) { ctr[k] = (uint8_t) s; s >>= 8; }
-        /* ssl_build_record_nonce: fixed IV ^ (0^4 || seq), or iv4 || seq (TLS 1.2 GCM) */
-        if (explicit_iv) {
-            memcpy(nonce, j->iv, 4);
-            memcpy(nonce + 4, ctr, 8);
-        } else {
-            memcpy(nonce, j->iv, 12);
-            for (int k = 0; k < 8; k++) nonce[4 + k] ^= ctr[k];
-        }
-        int ok;
-        int outl = 0;
-        if (j->dir) {
-            /* encrypt: content at buf[off], TLS 1.3 inner plaintext = content || 23 || 0^pad */
-            size_t off = explicit_iv ? 8 : 0, len = j->data_len;
-            uint8_t *p = buf + off;
-            if (j->tls13) {
-                p[len++] = 23;
-                size_t pad = (16 - len % 16) % 16;
-                memset(p + len, 0, pad);
-                len += pad;
-            }
-            size_t aadlen;
-            if (j->tls13) {
-                const size_t l = len + 16;
-                aad[0] = 23; aad[1] = 3; aad[2] = 3; aad[3] = (uint8_t) (l >> 8); aad[4] = (uint8_t) l;
-                aadlen = 5;
-            } else {
-                memcpy(aad, ctr, 8);
-                aad[8] = 23; aad[9] = 3; aad[10] = 3; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
-                aadlen = 13;
-            }
-            ok = EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 1) == 1 &&
-                 EVP_CipherUpdate(ctx, NULL, &outl, aad, (int) aadlen) == 1 &&
-                 EVP_CipherUpdate(ctx, p, &outl, p, (int) len) == 1 &&
-                 EVP_CipherFinal_ex(ctx, p + len, &outl) == 1 &&
-                 EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, 16, p + len) == 1;
-            if (explicit_iv) memcpy(buf, ctr, 8);
-            j->status[i] = ok ? 0 : -1;
-        } else {
-            /* decrypt: record body at buf[0] (explicit IV first for TLS 1.2 GCM) */
-            size_t off = explicit_iv ? 8 : 0;
-            if (j->data_len < off + 16) { j->status[i] = -0x7180; continue; }
-            size_t len = j->data_len - off - 16;
-            uint8_t *p = buf + off;
-            if (explicit_iv) memcpy(nonce + 4, buf, 8);
-            size_t aadlen;
-            if (j->tls13) {
-                const size_t l = len + 16;
-                aad[0] = 23; aad[1] = 3; aad[2] = 3; aad[3] = (uint8_t) (l >> 8); aad[4] = (uint8_t) l;
-                aadlen = 5;
-            } else {
-                memcpy(aad, ctr, 8);
-                aad[8] = 23; aad[9] = 3; aad[10] = 3; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
-                aadlen = 13;
-            }
-            ok = EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 0) == 1 &&
-                 EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_SET_TAG, 16, p + len) == 1 &&
-                 EVP_CipherUpdate(ctx, NULL, &outl, aad, (int) aadlen) == 1 &&
-                 EVP_CipherUpdate(ctx, p, &outl, p, (int) len) == 1 &&
-                 EVP_CipherFinal_ex(ctx, p + len, &outl) == 1;
-            if (!ok) {
-                memset(p, 0, len);                 /* PSA wipes the output on a bad tag */
-                j->status[i] = -0x7180;            /* MBEDTLS_ERR_SSL_INVALID_MAC */
-                continue;
-            }
-            if (j->tls13) {
-                /* ssl_parse_inner_plaintext: strip zero padding, recover the type */
-                size_t k = len;
-                while (k > 0 && p[k - 1] == 0) k--;
-                j->status[i] = k == 0 ? -0x7200 : 0;
-            } else {
-                j->status[i] = 0;
-            }
-        }
-    }
+    for (uint64_t i = j->lo; i < j->hi; i++)
+        j->status[i] = eb_record(ctx, j->cipher, j->tls13, j->dir, j->iv, j->arena + i * j->stride, j->data_len,
+                                 j->seq0 + i);
     EVP_CIPHER_CTX_free(ctx);
     return NULL;
 }
@@ -162,4 +166,218 @@ double evp_bench_records(int cipher, int tls13, const uint8_t *key, const uint8_
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &b);
     return (double) (b.tv_sec - a.tv_sec) + 1e-9 * (double) (b.tv_nsec - a.tv_nsec);
+}
+
+/* ---- many connections: one EVP context per connection -------------------
+ * The multi-connection configs (c4 / c4s): record i belongs to connection
+ * i % nconn (records round-robin over connections, as the GPU batch), each
+ * connection has its own key context (the reference keeps one transform per
+ * connection, ssl_misc.h:1073-1120), and a connection is served by one thread
+ * (thread = connection % threads).  evp_mixed_create sets every key once
+ * (untimed: psa_import_key at transform setup). */
+typedef struct {
+    uint32_t nconn;
+    int tls13;
+    EVP_CIPHER_CTX **ctx;
+    uint8_t *cipher;
+    uint8_t (*iv)[12];
+} eb_mixed;
+
+void evp_mixed_free(eb_mixed *m);
+
+eb_mixed *evp_mixed_create(uint32_t nconn, const uint8_t *ciphers, const uint8_t *keys /* 32 B each */,
+                           const uint8_t *ivs /* 12 B each */, int tls13)
+{
+    eb_mixed *m = calloc(1, sizeof(*m));
+    if (!m) return NULL;
+    m->nconn = nconn;
+    m->tls13 = tls13;
+    m->ctx = calloc(nconn, sizeof(*m->ctx));
+    m->cipher = malloc(nconn);
+    m->iv = malloc((size_t) nconn * 12);
+    if (!m->ctx || !m->cipher || !m->iv) { evp_mixed_free(m); return NULL; }
+    memcpy(m->cipher, ciphers, nconn);
+    memcpy(m->iv, ivs, (size_t) nconn * 12);
+    for (uint32_t c = 0; c < nconn; c++) {
+        const EVP_CIPHER *ev = eb_cipher(ciphers[c]);
+        m->ctx[c] = EVP_CIPHER_CTX_new();
+        if (!ev || !m->ctx[c] || EVP_CipherInit_ex(m->ctx[c], ev, NULL, keys + 32 * (size_t) c, NULL, 1) != 1) {
+            evp_mixed_free(m);
+            return NULL;
+        }
+    }
+    return m;
+}
+
+void evp_mixed_free(eb_mixed *m)
+{
+    if (!m) return;
+    if (m->ctx)
+        for (uint32_t c = 0; c < m->nconn; c++) EVP_CIPHER_CTX_free(m->ctx[c]);
+    free(m->ctx);
+    free(m->cipher);
+    free(m->iv);
+    free(m);
+}
+
+typedef struct {
+    const eb_mixed *m;
+    int dir, t, threads;
+    uint8_t *arena;
+    size_t stride, data_len;
+    uint64_t n;
+    int32_t *status;
+} eb_mjob;
+
+static void *eb_mworker(void *arg)
+{
+    eb_mjob *j = (eb_mjob *) arg;
+    const eb_mixed *m = j->m;
+    for (uint64_t i = 0; i < j->n; i++) {
+        const uint32_t c = (uint32_t) (i % m->nconn);
+        if ((int) (c % (uint32_t) j->threads) != j->t) continue;
+        j->status[i] = eb_record(m->ctx[c], m->cipher[c], m->tls13, j->dir, m->iv[c], j->arena + i * j->stride,
+                                 j->data_len, i / m->nconn);   /* the connection's own sequence number */
+    }
+    return NULL;
+}
+
+double evp_mixed_records(const eb_mixed *m, int dir, uint8_t *arena, size_t stride, size_t data_len, uint64_t n,
+                         int threads, int32_t *status)
+{
+    if (threads < 1) threads = 1;
+    if (threads > 512) threads = 512;
+    pthread_t tid[512];
+    eb_mjob jobs[512];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int i = 0; i < threads; i++) {
+        jobs[i] = (eb_mjob) { m, dir, i, threads, arena, stride, data_len, n, status };
+        if (pthread_create(&tid[i], NULL, eb_mworker, &jobs[i]) != 0) return -1.0;
+    }
+    for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    return (double) (b.tv_sec - a.tv_sec) + 1e-9 * (double) (b.tv_nsec - a.tv_nsec);
+}
+
+/* Where an EVP record's time goes (bench.py reports it beside the EVP leg):
+ * out[0] = nonce re-init + AAD, out[1] = the payload update, out[2] = final,
+ * out[3] = tag ctrl, each in microseconds per record (encrypt, len bytes,
+ * one context, warm cache).  OpenSSL 3's provider dispatch costs ~0.1-0.5 us
+ * per call, which at 1.4 KiB is as much as the ChaCha20-Poly1305 arithmetic. */
+static double eb_now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double) t.tv_sec + 1e-9 * (double) t.tv_nsec;
+}
+
+int evp_call_profile(int cipher, size_t len, int iters, double out[4])
+{
+    const EVP_CIPHER *ev = eb_cipher(cipher);
+    EVP_CIPHER_CTX *ctx = EVP_CIPHER_CTX_new();
+    uint8_t key[32] = { 1 }, nonce[12] = { 2 }, aad[5] = { 23, 3, 3, 0, 0 }, tag[16];
+    uint8_t *buf = calloc(1, len + 32);
+    if (!ev || !ctx || !buf || EVP_CipherInit_ex(ctx, ev, NULL, key, NULL, 1) != 1) {
+        EVP_CIPHER_CTX_free(ctx);
+        free(buf);
+        return -1;
+    }
+    double t[4] = { 0, 0, 0, 0 };
+    int outl = 0, ok = 1;
+    for (int i = 0; i < iters; i++) {
+        nonce[11] = (uint8_t) i;
+        nonce[10] = (uint8_t) (i >> 8);
+        const double a = eb_now();
+        ok &= EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 1) == 1;
+        ok &= EVP_CipherUpdate(ctx, NULL, &outl, aad, 5) == 1;
+        const double b = eb_now();
+        ok &= EVP_CipherUpdate(ctx, buf, &outl, buf, (int) len) == 1;
+        const double c = eb_now();
+        ok &= EVP_CipherFinal_ex(ctx, buf + len, &outl) == 1;
+        const double d = eb_now();
+        ok &= EVP_CIPHER_CTX_ctrl(ctx, EVP_CTRL_AEAD_GET_TAG, 16, tag) == 1;
+        const double e = eb_now();
+        t[0] += b - a; t[1] += c - b; t[2] += d - c; t[3] += e - d;
+    }
+    for (int k = 0; k < 4; k++) out[k] = t[k] / iters * 1e6;
+    EVP_CIPHER_CTX_free(ctx);
+    free(buf);
+    return ok ? 0 : -1;
+}
+
+/* ---- bulk independent parity (tests/test_evp_parity_gpu.py) --------------
+ * Records of any length under a few keys, checked against OpenSSL EVP with
+ * the ssl_msg.c framing of eb_record:
+ *   mode 0: seal record i in place (content at off[i] + head, for GPU decrypt)
+ *   mode 1: seal a copy of record i's plaintext (plain + off[i] + head) and
+ *           compare the wire bytes with got + off[i] (the GPU's encrypt output)
+ *   mode 2: compare the content bytes of got (decrypted by the GPU) with plain
+ * head = 8 for TLS 1.2 GCM (explicit nonce), else 0.  result[i] = 0 when the
+ * record matches (mode 0: the EVP status), 1 when it does not. */
+typedef struct {
+    int mode, cipher, tls13, t, threads;
+    uint32_t nkeys;
+    const uint8_t *keys, *ivs;
+    uint64_t n;
+    const uint32_t *keyidx, *len;
+    const uint64_t *seq, *off;
+    uint8_t *plain;
+    const uint8_t *got;
+    int32_t *result;
+} eb_vjob;
+
+static void *eb_vworker(void *arg)
+{
+    eb_vjob *j = (eb_vjob *) arg;
+    const EVP_CIPHER *ev = eb_cipher(j->cipher);
+    EVP_CIPHER_CTX **ctx = calloc(j->nkeys, sizeof(*ctx));
+    uint8_t *scratch = malloc(16384 + 64);
+    const size_t head = (!j->tls13 && j->cipher != EB_CHACHA20_POLY1305) ? 8 : 0;
+    int ok = ev && ctx && scratch;
+    for (uint32_t k = 0; ok && k < j->nkeys; k++) {
+        ctx[k] = EVP_CIPHER_CTX_new();
+        ok = ctx[k] && EVP_CipherInit_ex(ctx[k], ev, NULL, j->keys + 32 * (size_t) k, NULL, 1) == 1;
+    }
+    for (uint64_t i = (uint64_t) j->t; i < j->n; i += (uint64_t) j->threads) {
+        if (!ok || j->keyidx[i] >= j->nkeys || j->len[i] > 16384) { j->result[i] = -1; continue; }
+        const uint32_t k = j->keyidx[i];
+        const size_t len = j->len[i];
+        const size_t inner = j->tls13 ? len + 1 + (16 - (len + 1) % 16) % 16 : len;
+        const size_t wire = head + inner + 16;
+        if (j->mode == 0) {
+            j->result[i] = eb_record(ctx[k], j->cipher, j->tls13, 1, j->ivs + 12 * (size_t) k, j->plain + j->off[i],
+                                     len, j->seq[i]);
+        } else if (j->mode == 1) {
+            memset(scratch, 0, wire);
+            memcpy(scratch + head, j->plain + j->off[i] + head, len);
+            const int32_t st = eb_record(ctx[k], j->cipher, j->tls13, 1, j->ivs + 12 * (size_t) k, scratch, len,
+                                         j->seq[i]);
+            j->result[i] = st != 0 || memcmp(scratch, j->got + j->off[i], wire) != 0;
+        } else {
+            j->result[i] = memcmp(j->plain + j->off[i] + head, j->got + j->off[i] + head, len) != 0;
+        }
+    }
+    if (ctx)
+        for (uint32_t k = 0; k < j->nkeys; k++) EVP_CIPHER_CTX_free(ctx[k]);
+    free(ctx);
+    free(scratch);
+    return NULL;
+}
+
+int evp_check_records(int mode, int cipher, int tls13, uint32_t nkeys, const uint8_t *keys, const uint8_t *ivs,
+                      uint64_t n, const uint32_t *keyidx, const uint64_t *seq, const uint64_t *off,
+                      const uint32_t *len, uint8_t *plain, const uint8_t *got, int threads, int32_t *result)
+{
+    if (threads < 1) threads = 1;
+    if (threads > 512) threads = 512;
+    pthread_t tid[512];
+    eb_vjob jobs[512];
+    for (int i = 0; i < threads; i++) {
+        jobs[i] = (eb_vjob) { mode, cipher, tls13, i, threads, nkeys, keys, ivs, n, keyidx, len, seq, off, plain, got,
+                              result };
+        if (pthread_create(&tid[i], NULL, eb_vworker, &jobs[i]) != 0) return -1;
+    }
+    for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
+    return 0;
 }

@@ -917,3 +917,58 @@ double orc_bench_records(const orc_transform *t, int dir, uint8_t *arena,
     clock_gettime(CLOCK_MONOTONIC, &b);
     return (double) (b.tv_sec - a.tv_sec) + 1e-9 * (double) (b.tv_nsec - a.tv_nsec);
 }
+
+/* Many connections (the c4 / c4s CPU leg): record i belongs to connection
+ * i % nconn with the connection's own sequence number i / nconn, and each
+ * connection is served by one thread (connection % threads), as
+ * evp_mixed_records in evp_bench.c. */
+typedef struct {
+    const orc_transform *const *ts;
+    uint32_t nconn;
+    int dir, t, threads;
+    uint8_t *arena;
+    size_t stride, data_len;
+    uint64_t n;
+    int32_t *status;
+} bench_mjob;
+
+static void *bench_mworker(void *arg)
+{
+    bench_mjob *j = (bench_mjob *) arg;
+    for (uint64_t i = 0; i < j->n; i++) {
+        const uint32_t c = (uint32_t) (i % j->nconn);
+        if ((int) (c % (uint32_t) j->threads) != j->t) continue;
+        const orc_transform *t = j->ts[c];
+        orc_record rec;
+        rec.cid_len = 0;
+        uint64_t seq = i / j->nconn;
+        for (int k = 7; k >= 0; k--) { rec.ctr[k] = (uint8_t) seq; seq >>= 8; }
+        rec.type = 23;
+        rec.ver[0] = 3; rec.ver[1] = 3;
+        rec.buf = j->arena + i * j->stride;
+        rec.buf_len = j->stride;
+        rec.data_offset = (j->dir && t->ivlen != t->fixed_ivlen) ? 8 : 0;
+        rec.data_len = j->data_len;
+        const int r = j->dir ? orc_encrypt_buf(t, &rec) : orc_decrypt_buf(t, &rec);
+        if (j->status) j->status[i] = r;
+    }
+    return NULL;
+}
+
+double orc_bench_records_multi(const orc_transform *const *ts, uint32_t nconn, int dir, uint8_t *arena,
+                               size_t stride, size_t data_len, uint64_t n, int threads, int32_t *status)
+{
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    bench_mjob jobs[256];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int i = 0; i < threads; i++) {
+        jobs[i] = (bench_mjob) { ts, nconn, dir, i, threads, arena, stride, data_len, n, status };
+        if (pthread_create(&tid[i], NULL, bench_mworker, &jobs[i]) != 0) return -1.0;
+    }
+    for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    return (double) (b.tv_sec - a.tv_sec) + 1e-9 * (double) (b.tv_nsec - a.tv_nsec);
+}

@@ -215,6 +215,9 @@ int orc_decrypt_buf(const orc_transform *t, orc_record *rec);
 double orc_bench_records(const orc_transform *t, int dir, uint8_t *arena,
                          size_t stride, size_t data_len, uint64_t n,
                          uint64_t seq0, int threads, int32_t *status);
+/* record i under ts[i % nconn] with sequence number i / nconn (c4 / c4s CPU leg) */
+double orc_bench_records_multi(const orc_transform *const *ts, uint32_t nconn, int dir, uint8_t *arena,
+                               size_t stride, size_t data_len, uint64_t n, int threads, int32_t *status);
 
 /* ---- TLS 1.3 key schedule (oracle/keysched.c) -------------------------- */
 /* hash identifiers: the psa_algorithm_t values PSA_ALG_SHA_256 / _384 of the

@@ -1,9 +1,13 @@
 """Batch calls through libtlsrec.so on the SYSTEM HIP runtime (/opt/rocm, no
 torch in the process -- the runtime a C host links): a sequence of encrypt
 ('e') and decrypt ('d') calls over a many-key table, each call's results
-array pre-filled with 0x55, reporting how many results each call wrote.
+array pre-filled with 0x55 (or 0x00, which reads as success), reporting how
+many results each call wrote and how many carry a kernel's verdict (encrypt:
+status 0 with the protected length 1456; decrypt of the static descriptors:
+INVALID_MAC) -- with a zero pre-fill only the verdict count tells an unwritten
+result from a real one.
 
-    python tests/sysrt_seq.py <records> <keys> <sequence> [pageable|memset|pinned]
+    python tests/sysrt_seq.py <records> <keys> <sequence> [pageable|memset|pinned] [prefill byte]
 
 Run as a subprocess by tests/test_c_host.py (not collected by pytest).
 Regression: with the stream-ordered allocator (hipMallocAsync) for the
@@ -25,6 +29,7 @@ import mbedtls_amd as M  # noqa: E402
 L = _abi.load()
 n, NK, seq = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
 MODE = sys.argv[4] if len(sys.argv) > 4 else "pageable"
+FILL = int(sys.argv[5], 0) if len(sys.argv) > 5 else 0x55
 
 
 def dmalloc(nb):
@@ -72,11 +77,13 @@ arena = rng.integers(0, 256, n * stride).astype(np.uint8)
 da, dr, ds = dmalloc(arena.nbytes), dmalloc(recs.nbytes), dmalloc(n * 16)
 h2d(da, arena)
 h2d(dr, recs)
-written = []
+written, verdicts = [], []
+fillword = int.from_bytes(bytes([FILL]) * 4, "little")
+fillword = fillword - (1 << 32) if fillword >= 1 << 31 else fillword
 for c in seq:
-    r = np.full(n * 16, 0x55, dtype=np.uint8).view(M.BATCH_RES)
+    r = np.full(n * 16, FILL, dtype=np.uint8).view(M.BATCH_RES)
     if MODE == "memset":
-        assert hip.hipMemset(ds, 0x55, ctypes.c_size_t(n * 16)) == 0
+        assert hip.hipMemset(ds, FILL, ctypes.c_size_t(n * 16)) == 0
         hip.hipDeviceSynchronize()
     else:
         h2d(ds, r)
@@ -84,6 +91,13 @@ for c in seq:
     assert fn(kt, dr, ds, n, da, da, 0, None) == 0
     hip.hipDeviceSynchronize()
     d2h(r, ds)
-    written.append(int((r["status"] != 0x55555555).sum()))
+    raw = r.view(np.uint8).reshape(n, 16)
+    written.append(int((raw != FILL).any(axis=1).sum()))
+    if c == "e":
+        ok = (r["status"] == 0) & (r["data_len"] == 1456)
+    else:
+        ok = r["status"] == M.ERR_SSL_INVALID_MAC
+    verdicts.append(int(ok.sum()))
 L.tlsrec_keytab_free(kt)
-print(json.dumps({"records": n, "keys": NK, "sequence": seq, "mode": MODE, "written": written}))
+print(json.dumps({"records": n, "keys": NK, "sequence": seq, "mode": MODE, "fill": FILL, "written": written,
+                  "verdicts": verdicts}))

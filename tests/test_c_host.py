@@ -104,19 +104,24 @@ def test_c_multi_gpu_host_one_rank(records, content):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fill", ["0x55", "0"])
 @pytest.mark.parametrize("mode", ["pageable", "memset", "pinned"])
-def test_system_runtime_direction_switches(mode):
+def test_system_runtime_direction_switches(mode, fill):
     """Batch calls alternating encrypt / decrypt over a 256-key table on the
     system HIP runtime (no torch in the process: what a C host links).  Every
     call must write every result -- with the stream-ordered allocator for the
-    bucket scratch, the first call after a direction change wrote none."""
+    bucket scratch, the first call after a direction change wrote none.  With
+    a zero pre-fill (which reads as success) every result must still carry the
+    kernel's verdict: the fail-closed contract (ssl_msg.c:1260 / :1804)."""
     assert _gpu(), "needs a GPU"
     env = dict(os.environ)
-    p = subprocess.run(["python3", os.path.join(ROOT, "tests", "sysrt_seq.py"), "64", "256", "eddeedde", mode],
+    p = subprocess.run(["python3", os.path.join(ROOT, "tests", "sysrt_seq.py"), "64", "256", "eddeedde", mode, fill],
                        capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
-    assert out["written"] == [64] * 8, out
+    assert out["verdicts"] == [64] * 8, out
+    if fill != "0":
+        assert out["written"] == [64] * 8, out
 
 
 DTLS = os.path.join(ROOT, "tests", "c", "dtls_host")

@@ -125,3 +125,44 @@ def test_c_shard_bounds_matches_python(n, world):
     s, c = ctypes.c_uint64(), ctypes.c_uint64()
     assert lib.tlsrec_shard_bounds(n, world, world, ctypes.byref(s), ctypes.byref(c)) == M.ERR_SSL_BAD_INPUT_DATA
     assert lib.tlsrec_shard_bounds(n, 0, 0, ctypes.byref(s), ctypes.byref(c)) == M.ERR_SSL_BAD_INPUT_DATA
+
+
+def _evidence_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        km = np.zeros(5, dtype=M.KEY_MATERIAL)
+        if rank == 0:
+            km["cipher"] = M.CIPHER_AES_256_GCM
+            km["key"] = np.arange(5 * 32, dtype=np.uint8).reshape(5, 32)
+        keys = M.broadcast_keys(km, "cpu")
+        q.put((rank, bench.rank_evidence(dist, keys, "cpu", rank)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_evidence_two_ranks():
+    """bench.py's record of what the process group formed (the driver's SCALE
+    run checks it): world size and backend as torch.distributed reports them,
+    every rank, and the key-table digest all-gathered and equal on all ranks."""
+    import hashlib
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_evidence_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    km = np.zeros(5, dtype=M.KEY_MATERIAL)
+    km["cipher"] = M.CIPHER_AES_256_GCM
+    km["key"] = np.arange(5 * 32, dtype=np.uint8).reshape(5, 32)
+    want = hashlib.sha256(km.tobytes()).hexdigest()
+    for rank, ev in got:
+        assert ev["world_size"] == 2 and ev["backend"] == "gloo"
+        assert [r["rank"] for r in ev["ranks"]] == [0, 1]
+        assert ev["key_table_equal_on_all_ranks"] and ev["key_table_sha256"] == want

@@ -82,6 +82,7 @@ class Table:
         sr = sres.cpu().numpy().view(S.STREAM_OUT_RES)
         rc = recs.cpu().numpy().view(M.BATCH_REC)
         rs = res.cpu().numpy().view(M.BATCH_RES)
+        self.last_regions = [o[p:p + size].tobytes() for p, size in outs]   # each job's whole output region
         return [(sr[i], o[p:p + int(sr[i]["out_len"])].tobytes(), rc, rs) for i, (p, _) in enumerate(outs)]
 
     def decrypt(self, conns):
@@ -144,6 +145,13 @@ def check_vs_oracle(tab, conns, got):
         for k, (dgi, off, doff, dlen, dsp, typ) in enumerate(wrecs):
             assert int(disp[f + k]) == dsp, (i, k, dsp, int(disp[f + k]))
             assert int(recs[f + k]["buf_off"]) == offs[i][dgi] + off, (i, k)
+            if dsp in (M.DTLS_DROPPED, M.DTLS_NOT_REACHED, M.ERR_SSL_UNEXPECTED_RECORD):
+                # never decrypted by the reference: no plaintext may be left
+                # (each byte is the received one, or wiped to zero)
+                s0 = offs[i][dgi] + off
+                got_b = a[s0:s0 + doff + dlen]
+                rx = np.frombuffer(after[dgi][off:off + doff + dlen], dtype=np.uint8)
+                assert ((got_b == rx) | (got_b == 0)).all(), (i, k, dsp)
             if dsp == 0:
                 r = res[f + k]
                 assert (int(r["data_offset"]), int(r["data_len"]), int(r["type"])) == (doff, dlen, typ), (i, k)
@@ -295,4 +303,8 @@ def test_send_counter_wrap():
     assert st == M.ERR_SSL_COUNTER_WRAPPING and nrec == 2 and c2 == ctr(4, 0)
     assert (int(r["status"]), int(r["nrec"]), bytes(r["out_ctr"])) == (st, nrec, c2)
     assert out == want
+    # the third record would reuse sequence number (4, 0) -- a reused nonce:
+    # it is never sealed, and its bytes of the output stay zero (ssl_msg.c:2741-2756)
+    region = tab.last_regions[0]
+    assert len(region) > len(out) and region[len(out):] == bytes(len(region) - len(out))
     tab.close()

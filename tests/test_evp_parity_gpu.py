@@ -1,0 +1,205 @@
+"""Bulk, independent parity of the GPU record path against OpenSSL EVP.
+
+The reference's own tests hold ciphertext KATs only for TLS 1.3 AES-128-GCM
+(/root/reference/tests/suites/test_suite_ssl.data:2776-2834).  For the headline
+ciphers these tests compare the GPU's own output with OpenSSL 3 libcrypto
+(EVP_aes_128_gcm / _256_gcm / EVP_chacha20_poly1305) wrapped in the ssl_msg.c
+record framing (oracle/evp_bench.c evp_check_records; pinned on the CPU against
+the oracle by tests/test_evp_baseline.py) -- no record passes through this
+repository's oracle:
+
+* >= 10^5 records per (cipher, TLS version) and direction,
+  at the edge lengths {0, 1, 15, 16, 17, 1400, 16383} plus random lengths,
+  16 keys round-robin (bucket order) and one key (identity order);
+* config 2 at its stated size (2^20 x 16 KiB TLS 1.3 AES-256-GCM decrypt, the
+  8-lane G5 kernel) with 1 record in 1024 bit-flipped, INVALID_MAC expected at
+  exactly those indices (ssl_msg.c:1412-1424), every other
+  record's plaintext checked on the device, and a strided sample of 4096
+  records' ciphertexts checked against EVP.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import mbedtls_amd as M
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EDGE = np.array([0, 1, 15, 16, 17, 1400, 16383], dtype=np.uint32)
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "needs a GPU"
+    return torch
+
+
+def _threads():
+    import bench
+    return bench.host_cores()[0]
+
+
+def _layout(n, head, rng):
+    """lengths (25 % edge values, 75 % uniform 0..2048, every edge value at
+    least 100 times), 128-B aligned record buffers with tag / padding room"""
+    lens = rng.integers(0, 2049, n).astype(np.uint32)
+    pick = rng.random(n) < 0.25
+    lens[pick] = EDGE[rng.integers(0, len(EDGE), int(pick.sum()))]
+    lens[:len(EDGE) * 100] = np.tile(EDGE, 100)
+    size = head + lens.astype(np.uint64) + 48
+    al = (size + 127) // 128 * 128
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(al)[:-1]
+    return lens, size, off, int(off[-1] + al[-1])
+
+
+def _keys(cipher, nkeys, rng):
+    kl = M.KEYLEN[cipher]
+    keys = rng.integers(0, 256, (nkeys, 32), dtype=np.uint8)
+    keys[:, kl:] = 0
+    ivs = rng.integers(0, 256, (nkeys, 12), dtype=np.uint8)
+    return keys, ivs
+
+
+CASES = [(c, v) for c in (M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305)
+         for v in (M.VERSION_TLS1_2, M.VERSION_TLS1_3)]
+
+
+@pytest.mark.parametrize("nkeys,n", [(16, 100_000), (1, 30_000)], ids=["16keys", "1key"])
+@pytest.mark.parametrize("cipher,ver", CASES, ids=lambda x: str(x))
+def test_bulk_records_vs_openssl_evp(cipher, ver, nkeys, n):
+    torch = _torch()
+    dev = torch.device("cuda")
+    rng = np.random.default_rng(cipher * 100 + ver + nkeys)
+    head = 8 if ver == M.VERSION_TLS1_2 and cipher != M.CIPHER_CHACHA20_POLY1305 else 0
+    lens, size, off, total = _layout(n, head, rng)
+    keys, ivs = _keys(cipher, nkeys, rng)
+    kl = M.KEYLEN[cipher]
+    km = np.concatenate([M.key_material(cipher, ver, bytes(k[:kl]), bytes(v)) for k, v in zip(keys, ivs)])
+    keyidx = (np.arange(n) % nkeys).astype(np.uint32)
+    seq = rng.integers(0, 1 << 62, n, dtype=np.uint64)
+    plain = rng.integers(0, 256, total, dtype=np.uint8)
+    kt = M.KeyTable(nkeys)
+    kt.load(km)
+    threads = _threads()
+    try:
+        # ---- encrypt on the GPU, check every byte against EVP -------------
+        d = M.records(n)
+        d["buf_off"] = off
+        d["buf_len"] = size
+        d["data_offset"] = head
+        d["data_len"] = lens
+        d["slot"] = keyidx
+        d["ctr"] = M.seq_bytes(seq)
+        d["type"] = 23
+        d["ver"] = (3, 3)
+        arena = torch.from_numpy(plain).to(dev)
+        out = torch.zeros_like(arena)
+        res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        recs = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        M.batch_encrypt(kt, recs, res, n, arena, out)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(M.BATCH_RES)
+        inner = lens + 1 + (16 - (lens + 1) % 16) % 16 if ver == M.VERSION_TLS1_3 else lens
+        wire = head + inner + 16
+        assert (r["status"] == 0).all()
+        assert (r["data_offset"] == 0).all() and (r["data_len"] == wire).all()
+        got = out.cpu().numpy()
+        bad = O.evp_check_records(1, cipher, ver, keys, ivs, keyidx, seq, off, lens, plain, got, threads)
+        assert int((bad != 0).sum()) == 0, f"{int((bad != 0).sum())} of {n} records differ from OpenSSL, " \
+                                           f"first {np.flatnonzero(bad)[:5]}"
+        # ---- decrypt EVP-sealed records on the GPU -------------------------
+        sealed = plain.copy()
+        st = O.evp_check_records(0, cipher, ver, keys, ivs, keyidx, seq, off, lens, sealed, None, threads)
+        assert (st == 0).all()
+        dd = d.copy()
+        dd["data_offset"] = 0
+        dd["data_len"] = wire
+        arena = torch.from_numpy(sealed).to(dev)
+        res.zero_()
+        recs = torch.from_numpy(dd.view(np.uint8).copy()).to(dev)
+        M.batch_decrypt(kt, recs, res, n, arena, arena)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(M.BATCH_RES)
+        assert (r["status"] == 0).all(), np.unique(r["status"])
+        assert (r["data_offset"] == head).all() and (r["data_len"] == lens).all() and (r["type"] == 23).all()
+        bad = O.evp_check_records(2, cipher, ver, keys, ivs, keyidx, seq, off, lens, plain, arena.cpu().numpy(),
+                                  threads)
+        assert int((bad != 0).sum()) == 0, f"{int((bad != 0).sum())} plaintexts differ"
+    finally:
+        kt.close()
+
+
+def test_c2_full_size_tamper_1_in_1024_and_evp_sample():
+    """2^20 x 16 KiB TLS 1.3 AES-256-GCM decrypt (BASELINE configs[1]) through
+    the kernel the bench times (single key: identity order, 8 lanes, G5)."""
+    torch = _torch()
+    dev = torch.device("cuda")
+    n, content, inner, wire, stride = 1 << 20, 16383, 16384, 16400, 16512
+    rng = np.random.default_rng(0xC2)
+    keys, ivs = _keys(M.CIPHER_AES_256_GCM, 1, rng)
+    km = M.key_material(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, bytes(keys[0]), bytes(ivs[0]))
+    kt = M.KeyTable(1)
+    kt.load(km)
+    try:
+        d = M.records(n)
+        d["buf_off"] = np.arange(n, dtype=np.uint64) * stride
+        d["buf_len"] = stride
+        d["data_len"] = content
+        d["ctr"] = M.seq_bytes(np.arange(n, dtype=np.uint64))
+        d["type"] = 23
+        d["ver"] = (3, 3)
+        g = torch.Generator(device=dev)
+        g.manual_seed(12345)
+        A = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
+        B = torch.empty_like(A)
+        res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        M.batch_encrypt(kt, torch.from_numpy(d.view(np.uint8).copy()).to(dev), res, n, A, B)
+        torch.cuda.synchronize()
+        st = res.view(torch.int32)[0::4]
+        assert int((st != 0).sum()) == 0 and bool((res.view(torch.int32)[2::4] == wire).all())
+
+        # EVP: a strided sample of 4096 ciphertexts, sealed independently
+        sample = np.arange(0, n, 256, dtype=np.int64)
+        rows_a = A.view(n, stride)[torch.from_numpy(sample).to(dev)].cpu().numpy()
+        rows_b = B.view(n, stride)[torch.from_numpy(sample).to(dev)].cpu().numpy()
+        off = np.arange(len(sample), dtype=np.uint64) * stride
+        plain_h, got_h = rows_a.reshape(-1).copy(), rows_b.reshape(-1).copy()
+        bad = O.evp_check_records(1, M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, keys, ivs,
+                                  np.zeros(len(sample), np.uint32), sample.astype(np.uint64), off,
+                                  np.full(len(sample), content, np.uint32), plain_h, got_h, _threads())
+        assert int((bad != 0).sum()) == 0, f"{int((bad != 0).sum())} of 4096 sampled ciphertexts differ from OpenSSL"
+
+        # 1 record in 1024 bit-flipped: odd ones in the tag, even ones in the ciphertext
+        tam = np.arange(17, n, 1024, dtype=np.int64)
+        pos = np.where(np.arange(len(tam)) % 2 == 1, inner + (tam % 16), (tam * 37) % inner)
+        flat = torch.from_numpy(tam * stride + pos).to(dev)
+        bit = torch.from_numpy((1 << (tam % 8)).astype(np.uint8)).to(dev)
+        B[flat] = B[flat] ^ bit
+        dd = d.copy()
+        dd["data_len"] = wire
+        C = torch.empty_like(A)
+        res.zero_()
+        M.batch_decrypt(kt, torch.from_numpy(dd.view(np.uint8).copy()).to(dev), res, n, B, C)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(M.BATCH_RES)
+        want = np.zeros(n, dtype=np.int32)
+        want[tam] = M.ERR_SSL_INVALID_MAC
+        assert np.array_equal(r["status"], want), np.flatnonzero(r["status"] != want)[:10]
+        ok = np.ones(n, bool)
+        ok[tam] = False
+        assert (r["data_len"][ok] == content).all() and (r["type"][ok] == 23).all()
+        # every other record's plaintext, on the device; the tampered ones wiped
+        Av, Cv = A.view(n, stride), C.view(n, stride)
+        okd = torch.from_numpy(ok).to(dev)
+        for lo in range(0, n, 1 << 15):
+            hi = lo + (1 << 15)
+            same = (Av[lo:hi, :content] == Cv[lo:hi, :content]).all(dim=1)
+            assert bool((same | ~okd[lo:hi]).all()), f"plaintext mismatch in rows {lo}..{hi}"
+        wiped = Cv[torch.from_numpy(tam).to(dev)]
+        assert int(wiped.count_nonzero()) == 0, "a record that failed its tag kept output bytes"
+        del A, B, C
+    finally:
+        kt.close()

@@ -67,6 +67,7 @@ class Conns:
         torch.cuda.synchronize()
         o = tout.cpu().numpy()
         sr = sres.cpu().numpy().view(S.STREAM_OUT_RES)
+        self.last_regions = [o[p:p + size].tobytes() for p, size in outs]   # each job's whole output region
         return [(sr[i], o[p:p + int(sr[i]["out_len"])].tobytes()) for i, (p, _) in enumerate(outs)]
 
     def decrypt(self, conns):
@@ -291,4 +292,25 @@ def test_many_keys_small_records_wave_passes(cipher):
             o = int(recs[f + k]["buf_off"]) + int(res[f + k]["data_offset"])
             assert int(res[f + k]["data_len"]) == 1400
             assert a[o:o + 1400].tobytes() == pt[1400 * k:1400 * (k + 1)], (i, k)
+    c.close()
+
+
+def test_send_counter_wrap_encrypts_nothing_past_the_wrap():
+    """out_ctr = 2^64 - 2, three records: the reference writes the records with
+    sequence numbers 2^64-2 and 2^64-1, then stops with COUNTER_WRAPPING
+    (ssl_msg.c:2749-2756) -- nothing is ever encrypted under sequence 0 again
+    (a reused nonce).  The third record's bytes of the output stream stay zero."""
+    slots = [(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, prng_bytes(21, 32), prng_bytes(22, 12), 0),
+             (M.CIPHER_CHACHA20_POLY1305, M.VERSION_TLS1_2, prng_bytes(23, 32), prng_bytes(24, 12), 0)]
+    c = Conns(slots)
+    start = (1 << 64) - 2
+    pt = prng_bytes(25, 3000)
+    got = c.encrypt([(0, pt, start, 1000, 23), (1, pt, start, 1000, 23)])
+    for slot, (r, out) in enumerate(got):
+        st, want, nrec, c2 = O.stream_encrypt(c.ot[slot], pt, 23, start.to_bytes(8, "big"), 1000)
+        assert st == M.ERR_SSL_COUNTER_WRAPPING and nrec == 2 and c2 == bytes(8)
+        assert (int(r["status"]), int(r["nrec"]), bytes(r["out_ctr"])) == (st, nrec, c2)
+        assert out == want
+        region = c.last_regions[slot]
+        assert region[len(out):] == bytes(len(region) - len(out)), "bytes written past the wrap"
     c.close()
