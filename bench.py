@@ -336,7 +336,9 @@ def main():
                    "lanes_per_record": args.lanes or "auto", "slot_align": args.align, "aead_region_offset": lead + head,
                    "parallelism": f"shard{world}"},
         "records_per_s": round(n * world / steps_s, 1),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "limiter": (f"{ceiling['limiter']} ({ceiling['busy_frac']:.0%} busy, measured)"
+                                                 if ceiling else None),
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": KERNEL_OF.get(cname, "tlsrec_gcm_kernel"), "ceiling": ceiling,
                      "algorithmic_bytes_per_record": alg_per_rec, "kernel_ms_avg": round(kern_avg_s * 1e3, 4),
@@ -543,8 +545,8 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
     evp_ok = all(int(c) in O.EVP_CIPHERS for c in km["cipher"]) if mix else cipher in O.EVP_CIPHERS
     if evp_ok:
         if mix:
-            em = O.EvpMixed(km["cipher"], keys, ivs, tls)
-            evp_do = lambda d, a, ln, n: em.run(d, a, stride, ln, n, threads, st_cache[n])  # noqa: E731
+            em = O.EvpMixed(km["cipher"], keys, ivs, tls, threads)
+            evp_do = lambda d, a, ln, n: em.run(d, a, stride, ln, n, st_cache[n])  # noqa: E731
         else:
             evp_do = lambda d, a, ln, n: O.evp_bench(cipher, tls, key, iv, d, a, stride, ln, n, 0,  # noqa: E731
                                                      threads, st_cache[n])
@@ -570,7 +572,8 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
                      "sample": f"{n} records ({reps} passes) x {inner} B inner plaintext, {direction}, {what}: "
                                f"ssl_msg.c record framing around OpenSSL 3 EVP AEAD (AES-NI/VAES GCM, SIMD "
                                f"ChaCha20-Poly1305; oracle/libevpbench.so), nonce-only re-init per record as libssl "
-                               f"does for TLS 1.3, {el:.2f} s wall on {threads} threads",
+                               f"does for TLS 1.3, one OpenSSL library context per thread, {el:.2f} s wall on "
+                               f"{threads} threads",
                      "evp_us_per_record_one_thread": prof})
         if mix:
             em.close()

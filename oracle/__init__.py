@@ -619,12 +619,13 @@ def evp_lib():
                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         L.evp_bench_records.restype = ctypes.c_double
-        L.evp_mixed_create.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.evp_mixed_create.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_int]
         L.evp_mixed_create.restype = ctypes.c_void_p
         L.evp_mixed_free.argtypes = [ctypes.c_void_p]
         L.evp_mixed_free.restype = None
         L.evp_mixed_records.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
-                                        ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+                                        ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
         L.evp_mixed_records.restype = ctypes.c_double
         L.evp_call_profile.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.evp_call_profile.restype = ctypes.c_int
@@ -666,20 +667,22 @@ class EvpMixed:
     leg).  ciphers: uint8 array (AES_128_GCM / AES_256_GCM / CHACHA20_POLY1305
     per connection), keys (n, 32), ivs (n, 12) uint8 arrays."""
 
-    def __init__(self, ciphers, keys, ivs, tls_version):
+    def __init__(self, ciphers, keys, ivs, tls_version, threads: int = 1):
         import numpy as np
         c = np.ascontiguousarray(ciphers, dtype=np.uint8)
         k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(len(c), 32)
         v = np.ascontiguousarray(ivs, dtype=np.uint8).reshape(len(c), 12)
         if not set(np.unique(c).tolist()) <= set(EVP_CIPHERS):
             raise ValueError("EvpMixed: AES-128/256-GCM and ChaCha20-Poly1305 only")
+        self.threads = threads
         self._h = evp_lib().evp_mixed_create(len(c), c.ctypes.data, k.ctypes.data, v.ctypes.data,
-                                              int(tls_version == TLS1_3))
+                                              int(tls_version == TLS1_3), threads)
         if not self._h:
             raise RuntimeError("evp_mixed_create failed")
 
-    def run(self, direction: int, arena, stride: int, data_len: int, n: int, threads: int, status) -> float:
-        return evp_lib().evp_mixed_records(self._h, direction, arena.ctypes.data, stride, data_len, n, threads,
+    def run(self, direction: int, arena, stride: int, data_len: int, n: int, status) -> float:
+        """n records on the threads given at construction"""
+        return evp_lib().evp_mixed_records(self._h, direction, arena.ctypes.data, stride, data_len, n,
                                            status.ctypes.data)
 
     def close(self):

@@ -66,11 +66,11 @@ def test_mixed_connection_legs_match_oracle(ver, content):
         plain[i * stride + h:i * stride + h + content] = np.frombuffer(prng_bytes(900 + i, content), np.uint8)
     ts = [O.Transform(ver, int(c), bytes(k), bytes(k), bytes(v) + bytes(4), bytes(v) + bytes(4))
           for c, k, v in zip(ciphers, keys, ivs)]
-    evp = O.EvpMixed(ciphers, keys, ivs, ver)
+    evp = O.EvpMixed(ciphers, keys, ivs, ver, 3)
     try:
         a_evp, a_port = plain.copy(), plain.copy()
         st = np.zeros(n, dtype=np.int32)
-        evp.run(1, a_evp, stride, content, n, 3, st)
+        evp.run(1, a_evp, stride, content, n, st)
         assert (st == 0).all()
         O.bench_multi(ts, 1, a_port, stride, content, n, 3, st)
         assert (st == 0).all()
@@ -86,7 +86,7 @@ def test_mixed_connection_legs_match_oracle(ver, content):
             assert a_port[i * stride:i * stride + wire].tobytes() == rec.data(), i
         wires = [heads[i % nconn] + inner + 16 for i in range(n)]
         assert len(set(wires)) <= 2
-        for arena, run in ((a_evp, lambda a, w: evp.run(0, a, stride, w, n, 2, st)),
+        for arena, run in ((a_evp, lambda a, w: evp.run(0, a, stride, w, n, st)),
                            (a_port, lambda a, w: O.bench_multi(ts, 0, a, stride, w, n, 2, st))):
             if len(set(wires)) == 1:
                 arena[3 * stride + wires[3] - 2] ^= 1
