@@ -7,7 +7,7 @@
  * transformed by the kernels in kernels.hip.
  */
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -351,7 +351,7 @@ struct BucketScratch {
     tlsrec_scratch_lease lease = { nullptr, nullptr };
     uint32_t *counts, *offs, *perm;
     uint2 *keyrank;
-    void *scan_tmp;
+    void *scan_tmp;           /* tlsrec__exclusive_scan's block sums */
     size_t scan_bytes;
 };
 
@@ -361,10 +361,7 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, ARIA-128/192/256-GCM,
      * Camellia-128/192/256-GCM slots, end */
     const size_t nk = 10 * (size_t) kt->capacity + 2;
-    b.scan_bytes = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, b.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
-                                         (int) nk, st) != hipSuccess)
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    b.scan_bytes = tlsrec__scan_scratch_bytes((uint32_t) nk);
     const size_t al = 256;
     const size_t szk = (nk * 4 + al - 1) / al * al, szp = ((size_t) n * 4 + al - 1) / al * al;
     const size_t szr = ((size_t) n * 8 + al - 1) / al * al;
@@ -391,7 +388,7 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     a.perm = b.perm;
     if (tlsrec__launch_bucket_zero(&a, st) != hipSuccess ||
         tlsrec__launch_bucket_count(&a, st) != hipSuccess ||
-        hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, b.scan_bytes, b.counts, b.offs, (int) nk, st) != hipSuccess ||
+        tlsrec__exclusive_scan(b.counts, b.offs, (uint32_t) nk, (uint32_t *) b.scan_tmp, st) != hipSuccess ||
         tlsrec__launch_bucket_scatter(&a, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     return 0;
@@ -408,17 +405,36 @@ static volatile uint32_t g_test_skip = 0xffffffffu;
 
 extern "C" void tlsrec__test_skip_record(uint32_t index) { g_test_skip = index; }
 
-/* prefilled: the caller already wrote INTERNAL_ERROR into every result (the
- * single-record engine stages it with the record's upload) */
+/* Launch options of one batch:
+ *   only_mask  launch only these ciphers' kernels (1 << TLSREC_CIPHER_*; the
+ *              single-record engine knows its records' ciphers), 0 = every
+ *              cipher the table holds
+ *   avg_bytes  mean record size when the caller knows it (the stream / DTLS
+ *              layers, the host pipeline; 0 = unknown) -- it decides the GCM
+ *              launch for many keys with little work each (below)
+ *   prefilled  the caller already wrote INTERNAL_ERROR into every result (the
+ *              single-record engine stages it with the upload)
+ *   coalesced  a few records of many connections gathered from concurrent
+ *              single-record calls: identity order (no bucket pass: its four
+ *              launches would cost more than the batch), GCM in 16-lane wave
+ *              passes, so each wave serves its own record's key */
+struct BatchOpt {
+    uint32_t only_mask = 0;
+    uint32_t avg_bytes = 0;
+    bool prefilled = false;
+    bool coalesced = false;
+};
+
 static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
-                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec, uint32_t only_cipher = 0,
-                 uint32_t avg_bytes = 0, bool prefilled = false)
+                 const uint8_t *in, uint8_t *out, uint32_t lanes, void *stream, int dec, const BatchOpt &opt = BatchOpt())
 {
     if (!kt || (!recs && n) || (!res && n)) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t) stream;
     const int cu = kt->cu;
-    const uint32_t cmask = only_cipher ? (kt->cipher_mask & (1u << only_cipher)) : kt->cipher_mask;
+    const uint32_t avg_bytes = opt.avg_bytes;
+    const bool prefilled = opt.prefilled;
+    const uint32_t cmask = opt.only_mask ? (kt->cipher_mask & opt.only_mask) : kt->cipher_mask;
     const uint32_t skip = g_test_skip;
     /* A table holding a single key, or a batch of one record, needs no
      * grouping: the kernels walk the descriptors in order and flag records
@@ -428,7 +444,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
      * kernel), so a record that no kernel reaches fails closed -- the
      * reference's auth_done check, ssl_msg.c:1260 / :1804. */
     BucketScratch bs;
-    const bool identity = kt->nloaded == 1 || n == 1;
+    const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced;
     if (identity) {
         if (!prefilled && tlsrec__launch_res_guard(res, n, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else {
@@ -503,11 +519,15 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
                            small2 || small4;
         if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && light)
             L = small2 ? 2 : (small4 ? 4 : ((rpk >= 3 && Lfill <= 16) ? 16 : 64));
-        const bool wp = !kt->has_cid && !identity && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
-                        (wpe == 1 || (wpe != 0 && light));
+        bool wp = !kt->has_cid && !identity && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
+                  (wpe == 1 || (wpe != 0 && light));
+        if (opt.coalesced && auto_l && !kt->has_cid && nr != 12) {
+            L = 16;        /* a wave per 4 records, each wave its records' keys */
+            wp = true;
+        }
         if (L == 2 && !wp) L = 4;     /* 2 lanes: wave passes only */
         const int waves = wp ? 8 : (kt->has_cid ? 16 : gcm_waves());
-        a.rpw = pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
+        a.rpw = opt.coalesced ? (uint32_t) (64 / L) : pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         a.g5 = gcm_g5();
@@ -618,21 +638,27 @@ extern "C" int tlsrec_batch_encrypt_sized(const tlsrec_keytab *kt, const tlsrec_
                                           uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
                                           uint32_t mean_record_bytes, void *stream)
 {
-    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 0, 0, mean_record_bytes);
+    BatchOpt o;
+    o.avg_bytes = mean_record_bytes;
+    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 0, o);
 }
 
 extern "C" int tlsrec_batch_decrypt_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
                                           uint32_t n, const uint8_t *in_arena, uint8_t *out_arena,
                                           uint32_t mean_record_bytes, void *stream)
 {
-    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 1, 0, mean_record_bytes);
+    BatchOpt o;
+    o.avg_bytes = mean_record_bytes;
+    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 1, o);
 }
 
 extern "C" int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
                                    uint32_t n, const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec,
                                    uint32_t avg_bytes)
 {
-    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, dec, 0, avg_bytes);
+    BatchOpt o;
+    o.avg_bytes = avg_bytes;
+    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, dec, o);
 }
 
 
@@ -778,8 +804,9 @@ static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_ba
         /* the descriptors' buf_off are offsets into the host arena: shift the
          * device arena base so that base + buf_off lands in the slot */
         uint8_t *dev = (uint8_t *) ((uintptr_t) p->slot[k] - (uintptr_t) C.base);
-        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, zc ? zc : dev, lanes, p->cmp, dec, 0,
-                   (uint32_t) (C.span / (C.count ? C.count : 1)));
+        BatchOpt o;
+        o.avg_bytes = (uint32_t) (C.span / (C.count ? C.count : 1));
+        rc = batch(kt, p->d_recs + C.first, p->d_res + C.first, C.count, dev, zc ? zc : dev, lanes, p->cmp, dec, o);
         if (rc) break;
         e = hipEventRecord(p->ev_cmp[k], p->cmp);
         if (zc) {
@@ -825,49 +852,87 @@ extern "C" int tlsrec_host_batch_decrypt(tlsrec_keytab *kt, const tlsrec_batch_r
  *
  * Key slots live in pages of ENGINE_PAGE_SLOTS (one key table each), added
  * as connections arrive -- ENGINE_MAX_PAGES x 4096 = 1 M slots, i.e. 512 K
- * connections per process.  Records run on one of ENGINE_CTXS staging
- * contexts (stream + pinned host buffer + device buffer), so threads serving
- * different connections do not serialise on one lock.  A record is one
- * H2D copy (descriptor + buffer + CID), one kernel of its own cipher (no
- * bucket pass: a batch of one), one D2H copy (result + buffer), one sync.
+ * connections per process.
+ *
+ * Concurrent calls are coalesced (flat combining, per page): a call queues
+ * its record; if fewer than ENGINE_SETS batches of the page are in flight it
+ * becomes the leader of the next one, takes every queued record (up to
+ * ENGINE_BATCH, either direction), stages them in one pinned buffer, and runs
+ * one H2D copy, one launch per direction and cipher (identity order: no
+ * bucket pass), one D2H copy and one sync for all of them; the callers whose
+ * records it carried are woken with their results.  A lone call is its own
+ * leader: one record, one round trip.  Under load a round trip carries as
+ * many records as arrived during the previous one.
  * ==================================================================== */
 #define ENGINE_PAGE_SLOTS 4096
 #define ENGINE_MAX_PAGES 256
-#define ENGINE_CTXS 8
+#define ENGINE_SETS 2                    /* batches of a page in flight at once */
+#define ENGINE_BATCH 256                 /* records per coalesced batch */
+#define ENGINE_ALIGN 128                 /* record slots in the staging arena */
+
+struct EngineReq {
+    int dec;
+    tlsrec_batch_rec d;                  /* slot = page-local */
+    uint32_t cipher;
+    unsigned char *buf;
+    size_t buf_len;
+    const unsigned char *cid;
+    tlsrec_batch_res res;
+    int rc;
+    int done;                            /* guarded by the combiner's mutex */
+    EngineReq *next;
+};
+
+/* one staging set: [descriptors][results][arena], pinned host and device */
+struct EngineSet {
+    hipStream_t st;
+    uint8_t *h, *d;
+    size_t cap;
+    int busy;
+};
+
+struct Combiner {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    EngineReq *head, *tail;
+    EngineSet set[ENGINE_SETS];
+    uint64_t batches, records;           /* statistics (tlsrec__engine_stats) */
+};
 
 struct EnginePage {
     tlsrec_keytab *kt;
     uint8_t used[ENGINE_PAGE_SLOTS];
     uint32_t nused;
-};
-
-struct EngineCtx {
-    pthread_mutex_t mu;
-    hipStream_t st;
-    uint8_t *h;              /* pinned: [rec 64][res 64][buffer][cid] */
-    uint8_t *d;
-    size_t cap;
+    Combiner *co;
 };
 
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;   /* slot allocation, page growth */
 static EnginePage g_pages[ENGINE_MAX_PAGES];
 static volatile int g_npages = 0;
 static hipStream_t g_load = NULL;
-static EngineCtx g_ctx[ENGINE_CTXS];
-static volatile int g_ctx_ready = 0;
+static volatile int g_ready = 0;
 
 static int engine_init_locked(void)
 {
-    if (g_ctx_ready) return 0;
+    if (g_ready) return 0;
     if (tlsrec_device_check() != 0) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     if (hipStreamCreateWithFlags(&g_load, hipStreamNonBlocking) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    for (int i = 0; i < ENGINE_CTXS; i++) {
-        pthread_mutex_init(&g_ctx[i].mu, NULL);
-        if (hipStreamCreateWithFlags(&g_ctx[i].st, hipStreamNonBlocking) != hipSuccess)
-            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    }
-    g_ctx_ready = 1;
+    g_ready = 1;
     return 0;
+}
+
+static Combiner *combiner_new(void)
+{
+    Combiner *c = (Combiner *) calloc(1, sizeof(Combiner));
+    if (!c) return NULL;
+    pthread_mutex_init(&c->mu, NULL);
+    pthread_cond_init(&c->cv, NULL);
+    for (int i = 0; i < ENGINE_SETS; i++)
+        if (hipStreamCreateWithFlags(&c->set[i].st, hipStreamNonBlocking) != hipSuccess) {
+            free(c);
+            return NULL;
+        }
+    return c;
 }
 
 static tlsrec_keytab *slot_table(int slot, uint32_t *idx)
@@ -893,6 +958,11 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
                 r = TLSREC_ERR_SSL_ALLOC_FAILED;
             } else {
                 r = tlsrec_keytab_create(&g_pages[pg].kt, ENGINE_PAGE_SLOTS);
+                if (r == 0 && !(g_pages[pg].co = combiner_new())) {
+                    tlsrec_keytab_free(g_pages[pg].kt);
+                    g_pages[pg].kt = NULL;
+                    r = TLSREC_ERR_SSL_ALLOC_FAILED;
+                }
                 if (r == 0) g_npages = pg + 1;
             }
         }
@@ -945,28 +1015,105 @@ extern "C" int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, s
     return r;
 }
 
-/* a staging context: the first free one from a per-thread start, else wait */
-static EngineCtx *ctx_acquire(void)
+static size_t al(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+/* Leader: stage `n` records (linked from `first`), run them, fill in their
+ * results.  Records of one direction are contiguous in the staging area
+ * (encrypt first), each in its own ENGINE_ALIGN-aligned arena slot with its
+ * CID bytes behind the buffer. */
+static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t n)
 {
-    static volatile unsigned next = 0;
-    static __thread int home = -1;
-    if (home < 0) home = (int) (__atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED) % ENGINE_CTXS);
-    for (int k = 0; k < ENGINE_CTXS; k++) {
-        EngineCtx *c = &g_ctx[(home + k) % ENGINE_CTXS];
-        if (pthread_mutex_trylock(&c->mu) == 0) return c;
+    EngineReq *v[ENGINE_BATCH];
+    uint32_t k = 0, ne = 0;
+    for (EngineReq *r = first; r && k < n; r = r->next) v[k++] = r;
+    /* encrypt records first */
+    std::stable_partition(v, v + n, [](const EngineReq *r) { return !r->dec; });
+    while (ne < n && !v[ne]->dec) ne++;
+    const size_t off_res = al((size_t) n * sizeof(tlsrec_batch_rec), 256);
+    const size_t off_arena = al(off_res + (size_t) n * sizeof(tlsrec_batch_res), 256);
+    size_t used = 0;
+    size_t boff[ENGINE_BATCH];
+    for (uint32_t i = 0; i < n; i++) {
+        boff[i] = used;
+        used = al(used + v[i]->buf_len + v[i]->d.cid_len + 16, ENGINE_ALIGN);
     }
-    EngineCtx *c = &g_ctx[home];
-    pthread_mutex_lock(&c->mu);
-    return c;
+    const size_t need = off_arena + used + ENGINE_ALIGN;
+    if (S.cap < need) {
+        hipStreamSynchronize(S.st);
+        hipHostFree(S.h);
+        hipFree(S.d);
+        S.h = NULL;
+        S.d = NULL;
+        S.cap = 0;
+        const size_t want = need > (1u << 20) ? need + need / 2 : (1u << 20);
+        if (hipHostMalloc((void **) &S.h, want, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void **) &S.d, want) != hipSuccess)
+            return TLSREC_ERR_SSL_ALLOC_FAILED;
+        S.cap = want;
+    }
+    tlsrec_batch_rec *hd = (tlsrec_batch_rec *) S.h;
+    tlsrec_batch_res *hr = (tlsrec_batch_res *) (S.h + off_res);
+    uint8_t *ha = S.h + off_arena;
+    uint32_t mask_e = 0, mask_d = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        EngineReq *r = v[i];
+        tlsrec_batch_rec d = r->d;
+        d.buf_off = boff[i];
+        if (r->buf_len) memcpy(ha + boff[i], r->buf, r->buf_len);
+        if (d.cid_len) {
+            memcpy(ha + boff[i] + r->buf_len, r->cid, d.cid_len);
+            const uint32_t o = (uint32_t) r->buf_len;
+            d.cid_off[0] = (uint8_t) o; d.cid_off[1] = (uint8_t) (o >> 8);
+            d.cid_off[2] = (uint8_t) (o >> 16); d.cid_off[3] = (uint8_t) (o >> 24);
+        }
+        hd[i] = d;
+        /* each result goes up as INTERNAL_ERROR: only a kernel turns it into a
+         * verdict (ssl_msg.c:1260 / :1804, auth_done) */
+        memset(&hr[i], 0, sizeof(hr[i]));
+        hr[i].status = TLSREC_ERR_SSL_INTERNAL_ERROR;
+        (r->dec ? mask_d : mask_e) |= 1u << r->cipher;
+    }
+    const size_t total = off_arena + used;
+    hipError_t e = hipMemcpyAsync(S.d, S.h, total, hipMemcpyHostToDevice, S.st);
+    int rc = e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    tlsrec_batch_rec *dd = (tlsrec_batch_rec *) S.d;
+    tlsrec_batch_res *dr = (tlsrec_batch_res *) (S.d + off_res);
+    uint8_t *da = S.d + off_arena;
+    BatchOpt o;
+    o.prefilled = true;
+    o.coalesced = n > 1;
+    if (!rc && ne) {
+        o.only_mask = mask_e;
+        rc = batch(kt, dd, dr, ne, da, da, 0, S.st, 0, o);
+    }
+    if (!rc && n > ne) {
+        o.only_mask = mask_d;
+        rc = batch(kt, dd + ne, dr + ne, n - ne, da, da, 0, S.st, 1, o);
+    }
+    if (!rc) {
+        e = hipMemcpyAsync(S.h + off_res, S.d + off_res, total - off_res, hipMemcpyDeviceToHost, S.st);
+        if (e == hipSuccess) e = hipStreamSynchronize(S.st);
+        if (e != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    } else {
+        hipStreamSynchronize(S.st);
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        EngineReq *r = v[i];
+        r->rc = rc;
+        if (!rc) {
+            r->res = hr[i];
+            if (r->buf_len) memcpy(r->buf, ha + boff[i], r->buf_len);
+        }
+    }
+    return rc;
 }
 
 /* Run one record through the kernels: host buffer -> device -> host.  A
- * decrypted record's CID (cid_len bytes) is staged right after the buffer
- * (rec->cid_off = buf_len). */
+ * decrypted record's CID (cid_len bytes) is staged right after the buffer. */
 extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
                                   const unsigned char *cid, tlsrec_batch_res *out)
 {
-    if (!g_ctx_ready) {
+    if (!g_ready) {
         pthread_mutex_lock(&g_mu);
         int r = engine_init_locked();
         pthread_mutex_unlock(&g_mu);
@@ -977,60 +1124,70 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
     if (!kt) return TLSREC_ERR_SSL_INTERNAL_ERROR;
     const uint32_t cipher = kt->h_cipher[idx];
     if (cipher == 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
-    EngineCtx *c = ctx_acquire();
-    int r = 0;
-    const size_t need = 128 + buf_len + TLSREC_CID_LEN_MAX + 16;
-    if (c->cap < need) {
-        hipHostFree(c->h);
-        hipFree(c->d);
-        c->h = NULL;
-        c->d = NULL;
-        c->cap = 0;
-        const size_t want = need > 65536 ? need : 65536;
-        if (hipHostMalloc((void **) &c->h, want, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc((void **) &c->d, want) != hipSuccess)
-            r = TLSREC_ERR_SSL_ALLOC_FAILED;
-        else
-            c->cap = want;
+    if (buf_len > 0xffffffffu - 64) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co;
+    EngineReq me;
+    me.dec = dec;
+    me.d = *rec;
+    me.d.slot = idx;
+    me.cipher = cipher;
+    me.buf = buf;
+    me.buf_len = buf_len;
+    me.cid = cid;
+    me.rc = 0;
+    me.done = 0;
+    me.next = NULL;
+    pthread_mutex_lock(&co->mu);
+    if (co->tail) co->tail->next = &me; else co->head = &me;
+    co->tail = &me;
+    while (!me.done) {
+        int si = -1;
+        for (int i = 0; i < ENGINE_SETS; i++)
+            if (!co->set[i].busy) { si = i; break; }
+        if (si < 0 || co->head == NULL) {
+            pthread_cond_wait(&co->cv, &co->mu);
+            continue;
+        }
+        /* leader: take the queue (up to ENGINE_BATCH records) */
+        EngineSet &S = co->set[si];
+        S.busy = 1;
+        EngineReq *first = co->head;
+        uint32_t n = 0;
+        EngineReq *last = NULL;
+        for (EngineReq *r = first; r && n < ENGINE_BATCH; r = r->next) { last = r; n++; }
+        co->head = last->next;
+        if (!co->head) co->tail = NULL;
+        last->next = NULL;
+        co->batches++;
+        co->records += n;
+        pthread_mutex_unlock(&co->mu);
+        run_batch(kt, S, first, n);
+        pthread_mutex_lock(&co->mu);
+        for (EngineReq *r = first, *nx; r; r = nx) {
+            nx = r->next;
+            r->done = 1;
+        }
+        S.busy = 0;
+        pthread_cond_broadcast(&co->cv);
     }
-    if (r == 0) {
-        tlsrec_batch_rec d = *rec;
-        d.slot = idx;
-        d.buf_off = 0;
-        size_t up = 128 + buf_len;
-        if (d.cid_len) {
-            memcpy(c->h + 128 + buf_len, cid, d.cid_len);
-            const uint32_t off = (uint32_t) buf_len;
-            d.cid_off[0] = (uint8_t) off; d.cid_off[1] = (uint8_t) (off >> 8);
-            d.cid_off[2] = (uint8_t) (off >> 16); d.cid_off[3] = (uint8_t) (off >> 24);
-            up += d.cid_len;
-        }
-        memcpy(c->h, &d, sizeof(d));
-        {
-            /* the result slot goes up with the record as INTERNAL_ERROR: only
-             * the kernel can turn it into a verdict (ssl_msg.c:1260 / :1804);
-             * otherwise the previous record's result would still be there */
-            tlsrec_batch_res g;
-            memset(&g, 0, sizeof(g));
-            g.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
-            memcpy(c->h + 64, &g, sizeof(g));
-        }
-        if (buf_len) memcpy(c->h + 128, buf, buf_len);
-        tlsrec_batch_rec *d_rec = (tlsrec_batch_rec *) c->d;
-        tlsrec_batch_res *d_res = (tlsrec_batch_res *) (c->d + 64);
-        hipError_t e = hipMemcpyAsync(c->d, c->h, up, hipMemcpyHostToDevice, c->st);
-        if (e == hipSuccess) {
-            r = batch(kt, d_rec, d_res, 1, c->d + 128, c->d + 128, 0, c->st, dec, cipher, 0, true);
-            if (r == 0)
-                e = hipMemcpyAsync(c->h + 64, c->d + 64, 64 + buf_len, hipMemcpyDeviceToHost, c->st);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->st);
-        }
-        if (e != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) {
-            memcpy(out, c->h + 64, sizeof(*out));
-            if (buf_len) memcpy(buf, c->h + 128, buf_len);
-        }
+    pthread_mutex_unlock(&co->mu);
+    if (me.rc) return me.rc;
+    *out = me.res;
+    return 0;
+}
+
+/* coalescing statistics over every page: batches run and records carried */
+extern "C" void tlsrec__engine_stats(uint64_t *batches, uint64_t *records)
+{
+    uint64_t b = 0, r = 0;
+    for (int pg = 0; pg < g_npages; pg++) {
+        Combiner *c = g_pages[pg].co;
+        if (!c) continue;
+        pthread_mutex_lock(&c->mu);
+        b += c->batches;
+        r += c->records;
+        pthread_mutex_unlock(&c->mu);
     }
-    pthread_mutex_unlock(&c->mu);
-    return r;
+    if (batches) *batches = b;
+    if (records) *records = r;
 }

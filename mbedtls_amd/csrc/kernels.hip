@@ -921,13 +921,19 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
                 acc = p_sel((dq >> i) & 1, p_mul(acc, rp), acc);
                 if (i + 1 < LOGL) rp = p_mul(rp, rp);
             }
+            /* the L lanes' sum by DPP butterfly steps (VALU, not the LDS pipe) */
+            auto step = [&](auto sc) {
+                constexpr int S = decltype(sc)::value;
+                if constexpr (S < L) {
+                    P5 w;
 #pragma unroll
-            for (int o = 1; o < L; o <<= 1) {
-                P5 w;
-#pragma unroll
-                for (int i = 0; i < 5; i++) w.v[i] = __shfl_xor(acc.v[i], o);
-                acc = p_add(acc, w);
-            }
+                    for (int i = 0; i < 5; i++) w.v[i] = partner<S>(acc.v[i], lane);
+                    acc = p_add(acc, w);
+                }
+            };
+            step(std::integral_constant<int, 1>());
+            step(std::integral_constant<int, 2>());
+            step(std::integral_constant<int, 4>());
         }
         /* H1 = A r^M + sum_i C_i r^(M-1-i); tag = (H1 r + LEN) r + s */
         P5 X = M ? p_carry(acc) : (cidaad ? p_lds(aadf) : p_from_words(aadw));
@@ -953,7 +959,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
             }
         } else {
             uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
-            diff = __shfl(diff, leader);
+            diff = group_or<L>(lane == leader ? diff : 0u);       /* the leader's verdict, to all */
             uint32_t nzkey = 0;
             if (tls13 && nzpos) {
                 const uint32_t pos = nzpos - 1;
@@ -1047,6 +1053,146 @@ extern "C" hipError_t tlsrec__launch_bucket_count(const BucketArgs *a, hipStream
     if (a->n == 0) return hipSuccess;
     hipLaunchKernelGGL(tlsrec_bucket_count_kernel, dim3((a->n + 255) / 256), dim3(256), 0, st, *a);
     return hipGetLastError();
+}
+
+/* ======================================================================
+ * Exclusive scan of uint32 counts (the bucket pass's per-key offsets, the
+ * stream / DTLS layers' per-connection record offsets): reduce-then-scan in
+ * two launches.  Block b owns SCAN_CHUNK consecutive counts; the reduce
+ * kernel writes each block's sum, the apply kernel re-sums the sums of the
+ * blocks before it (at most a few hundred: 64 K keys x 10 classes is 161
+ * blocks) and scans its chunk.  No library call, no host sync; scratch =
+ * one word per block.
+ * ==================================================================== */
+constexpr uint32_t SCAN_THREADS = 256, SCAN_PER_THREAD = 16, SCAN_CHUNK = SCAN_THREADS * SCAN_PER_THREAD;
+
+/* exclusive scan over the block's 256 thread values (LDS, Hillis-Steele) */
+__device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t *sh)
+{
+    const uint32_t t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t o = 1; o < SCAN_THREADS; o <<= 1) {
+        const uint32_t add = t >= o ? sh[t - o] : 0u;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    const uint32_t incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void tlsrec_scan_reduce_kernel(const uint32_t *in, uint32_t n,
+                                                                        uint32_t *bsum)
+{
+    __shared__ uint32_t sh[SCAN_THREADS];
+    const uint64_t base = (uint64_t) blockIdx.x * SCAN_CHUNK;
+    uint32_t v = 0;
+    for (uint32_t k = threadIdx.x; k < SCAN_CHUNK; k += SCAN_THREADS)
+        if (base + k < n) v += in[base + k];
+    const uint32_t ex = block_exclusive(v, sh);
+    if (threadIdx.x == SCAN_THREADS - 1) bsum[blockIdx.x] = ex + v;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void tlsrec_scan_apply_kernel(const uint32_t *in, uint32_t n,
+                                                                       const uint32_t *bsum, uint32_t *out)
+{
+    __shared__ uint32_t sh[SCAN_THREADS];
+    /* the sums of the blocks before this one */
+    uint32_t pre = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += SCAN_THREADS) pre += bsum[b];
+    const uint32_t prex = block_exclusive(pre, sh);
+    if (threadIdx.x == SCAN_THREADS - 1) sh[0] = prex + pre;    /* after block_exclusive's last barrier */
+    __syncthreads();
+    const uint32_t block_base = sh[0];
+    __syncthreads();
+    /* thread t scans its SCAN_PER_THREAD consecutive counts */
+    const uint64_t first = (uint64_t) blockIdx.x * SCAN_CHUNK + (uint64_t) threadIdx.x * SCAN_PER_THREAD;
+    uint32_t v[SCAN_PER_THREAD], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER_THREAD; k++) {
+        v[k] = first + k < n ? in[first + k] : 0u;
+        sum += v[k];
+    }
+    uint32_t run = block_base + block_exclusive(sum, sh);
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER_THREAD; k++) {
+        if (first + k < n) out[first + k] = run;
+        run += v[k];
+    }
+}
+
+/* Self-test of the cross-lane helpers (tlsrec_recdev.h) for
+ * tests/test_lane_ops_gpu.py: one wave, lane i holds v_i = (i * 37 + 11) & 63
+ * plus 100 * i; rows of 64 words:
+ *   0-5 partner<1, 2, 4, 8, 16, 32>, 6-11 from_up<1, 2, 4, 8, 16, 32>,
+ *   12 wave_max, 13 wave_min, 14 group_max<8>, 15 group_or<4> of 1 << (i % 32),
+ *   16 group sum<8> by the Poly1305 butterfly steps */
+__global__ __launch_bounds__(64) void tlsrec_lane_ops_kernel(uint32_t *out)
+{
+    const int lane = threadIdx.x;
+    const uint32_t v = (uint32_t) ((lane * 37 + 11) & 63) + 100u * (uint32_t) lane;
+    out[0 * 64 + lane] = partner<1>(v, lane);
+    out[1 * 64 + lane] = partner<2>(v, lane);
+    out[2 * 64 + lane] = partner<4>(v, lane);
+    out[3 * 64 + lane] = partner<8>(v, lane);
+    out[4 * 64 + lane] = partner<16>(v, lane);
+    out[5 * 64 + lane] = partner<32>(v, lane);
+    out[6 * 64 + lane] = from_up<1>(v, lane);
+    out[7 * 64 + lane] = from_up<2>(v, lane);
+    out[8 * 64 + lane] = from_up<4>(v, lane);
+    out[9 * 64 + lane] = from_up<8>(v, lane);
+    out[10 * 64 + lane] = from_up<16>(v, lane);
+    out[11 * 64 + lane] = from_up<32>(v, lane);
+    out[12 * 64 + lane] = wave_max(v);
+    out[13 * 64 + lane] = wave_min(v);
+    out[14 * 64 + lane] = group_max<8>(v);
+    out[15 * 64 + lane] = group_or<4>(1u << (lane & 31));
+    uint32_t sum = v;
+    sum += partner<1>(sum, lane);
+    sum += partner<2>(sum, lane);
+    sum += partner<4>(sum, lane);
+    out[16 * 64 + lane] = sum;
+}
+
+extern "C" int tlsrec__test_lane_ops(uint32_t *host_out /* 17 x 64 words */)
+{
+    uint32_t *d = nullptr;
+    if (hipMalloc((void **) &d, 17 * 64 * 4) != hipSuccess) return -1;
+    hipLaunchKernelGGL(tlsrec_lane_ops_kernel, dim3(1), dim3(64), 0, 0, d);
+    const hipError_t e = hipMemcpy(host_out, d, 17 * 64 * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    return e == hipSuccess ? 0 : -1;
+}
+
+extern "C" size_t tlsrec__scan_scratch_bytes(uint32_t n)
+{
+    return ((size_t) n + SCAN_CHUNK - 1) / SCAN_CHUNK * 4 + 4;
+}
+
+extern "C" hipError_t tlsrec__exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *scratch,
+                                             hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    hipLaunchKernelGGL(tlsrec_scan_reduce_kernel, dim3(nb), dim3(SCAN_THREADS), 0, st, in, n, scratch);
+    hipLaunchKernelGGL(tlsrec_scan_apply_kernel, dim3(nb), dim3(SCAN_THREADS), 0, st, in, n, scratch, out);
+    return hipGetLastError();
+}
+
+/* tests/test_scan_gpu.py: the scan over host arrays (copies in, scans, copies out) */
+extern "C" int tlsrec__test_scan(const uint32_t *host_in, uint32_t n, uint32_t *host_out)
+{
+    uint32_t *d = nullptr;
+    const size_t sb = tlsrec__scan_scratch_bytes(n);
+    if (hipMalloc((void **) &d, (size_t) n * 8 + sb + 16) != hipSuccess) return -1;
+    hipError_t e = hipMemcpy(d, host_in, (size_t) n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = tlsrec__exclusive_scan(d, d + n, n, d + 2 * (size_t) n, 0);
+    if (e == hipSuccess) e = hipMemcpy(host_out, d + n, (size_t) n * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    return e == hipSuccess ? 0 : -1;
 }
 
 extern "C" hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st)

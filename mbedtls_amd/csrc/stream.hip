@@ -24,7 +24,6 @@
  * plaintext into its record slot (one wave per record).
  */
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <string.h>
 
@@ -833,9 +832,7 @@ struct Scratch {
 
 static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
 {
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, sc.scan_bytes, (uint32_t *) nullptr, (uint32_t *) nullptr,
-                                         (int) n + 1, st) != hipSuccess)
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    sc.scan_bytes = tlsrec__scan_scratch_bytes(n + 1);
     const size_t a = 256, sz4 = (((size_t) n + 1) * 4 + a - 1) / a * a, szs = ((size_t) n * sizeof(HdrStop) + a) / a * a;
     const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + a + sc.scan_bytes + a, &sc.lease);
     if (lr) return lr;
@@ -853,7 +850,7 @@ static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
 static int scan_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total, uint32_t *avg_bytes = nullptr)
 {
     unsigned long long bytes = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, sc.scan_bytes, sc.counts, sc.offs, (int) n + 1, st) != hipSuccess)
+    if (tlsrec__exclusive_scan(sc.counts, sc.offs, n + 1, (uint32_t *) sc.scan_tmp, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(&bytes, sc.bytes, sizeof(bytes), hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -109,7 +109,7 @@ template <int SH>
 __device__ __forceinline__ uint4 gtree_v(const uint4 (&P)[4], uint4 Y, int lane, int q)
 {
     if constexpr (SH >= 1) {
-        uint4 o = shfl4(Y, (lane + SH) & 63);
+        uint4 o = from_up4<SH>(Y, lane);
         if (q < SH) Y = xor4(gf_mul_v(Y, P[Log2<SH>::v]), o);
         return gtree_v<SH / 2>(P, Y, lane, q);
     } else {
@@ -125,7 +125,7 @@ template <int SH>
 __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane, int q)
 {
     if constexpr (SH >= 1) {
-        uint4 o = shfl4(Y, (lane + SH) & 63);
+        uint4 o = from_up4<SH>(Y, lane);
         if (q < SH) Y = xor4(gmul<Log2<SH>::v>(lds, Y), o);
         return gtree<SH / 2>(lds, Y, lane, q);
     } else {
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             } else {
                 uint4 want = load_block(jb.src, jb.aead_len, jb.aead_len + 16, jb.aead_len + 16, 0, false);
                 uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
-                diff = __shfl(diff, lane - q);                        /* group leader's verdict */
+                diff = group_or<L>(q == 0 ? diff : 0u);               /* the group leader's verdict, to all */
                 uint32_t key = group_max<L>(nzkey);
                 tlsrec_batch_res r;
                 r.data_offset = p.data_offset;

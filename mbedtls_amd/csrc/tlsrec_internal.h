@@ -149,6 +149,10 @@ int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, t
 hipError_t tlsrec__launch_bucket_zero(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_count(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_t st);
+/* exclusive scan of n uint32 (kernels.hip): two launches, scratch of
+ * tlsrec__scan_scratch_bytes(n) bytes, in and out may not alias */
+size_t tlsrec__scan_scratch_bytes(uint32_t n);
+hipError_t tlsrec__exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *scratch, hipStream_t st);
 /* every result of a batch to INTERNAL_ERROR before its AEAD kernels (fail closed, kernels.hip) */
 hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st);
 }

@@ -108,26 +108,108 @@ __device__ __forceinline__ uint4 shfl4(uint4 v, int src)
     return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
 }
 
+/* ----------------------------------------------------------------------
+ * Cross-lane moves on the VALU (DPP, v_permlane16/32_swap) instead of
+ * ds_bpermute, which is an LDS-pipe instruction -- the pipe the table
+ * kernels are bound by.  gfx950 DPP controls: quad_perm
+ * 0x00-0xFF, row_shl:n 0x100+n, row_ror:n 0x120+n, row_mirror 0x140,
+ * row_half_mirror 0x141 (a row = 16 lanes).
+ * -------------------------------------------------------------------- */
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v)
+{
+    return (uint32_t) __builtin_amdgcn_update_dpp((int) v, (int) v, CTRL, 0xF, 0xF, false);
+}
+
+/* lane i gets lane i ^ 16 (v_permlane16_swap: odd rows <-> even rows) */
+__device__ __forceinline__ uint32_t xor16(uint32_t v, int lane)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((lane >> 4) & 1) ? r[0] : r[1];
+}
+
+/* lane i gets lane i ^ 32 (v_permlane32_swap: upper half <-> lower half) */
+__device__ __forceinline__ uint32_t xor32(uint32_t v, int lane)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane >> 5) ? r[0] : r[1];
+}
+
+/* Butterfly partner of step S (1, 2, 4, 8, 16, 32) for a reduction over
+ * aligned groups of 2S lanes: after the steps 1 .. S every lane holds the
+ * reduction of its group.  Steps 4 and 8 are mirrors (i <-> 7 - i, i <-> 15 - i
+ * within the row), not xors: they pair each lane with one of the other half,
+ * which already holds that half's reduction. */
+template <int S>
+__device__ __forceinline__ uint32_t partner(uint32_t v, int lane)
+{
+    static_assert(S == 1 || S == 2 || S == 4 || S == 8 || S == 16 || S == 32, "butterfly step");
+    if constexpr (S == 1) return dpp<0xB1>(v);          /* quad_perm [1,0,3,2] */
+    else if constexpr (S == 2) return dpp<0x4E>(v);     /* quad_perm [2,3,0,1] */
+    else if constexpr (S == 4) return dpp<0x141>(v);    /* row_half_mirror */
+    else if constexpr (S == 8) return dpp<0x140>(v);    /* row_mirror */
+    else if constexpr (S == 16) return xor16(v, lane);
+    else return xor32(v, lane);
+}
+
+/* lane i gets lane i + SH, for the lanes q < SH of aligned groups of 2 SH or
+ * more lanes (the GHASH lane tree); other lanes get unspecified values */
+template <int SH>
+__device__ __forceinline__ uint32_t from_up(uint32_t v, int lane)
+{
+    if constexpr (SH < 16) return dpp<0x100 + SH>(v);    /* row_shl:SH */
+    else if constexpr (SH == 16) return xor16(v, lane);
+    else return xor32(v, lane);
+}
+
+template <int SH>
+__device__ __forceinline__ uint4 from_up4(uint4 v, int lane)
+{
+    return make_uint4(from_up<SH>(v.x, lane), from_up<SH>(v.y, lane), from_up<SH>(v.z, lane), from_up<SH>(v.w, lane));
+}
+
+/* For a symmetric op the 16- and 32-lane steps need no lane select: after
+ * v_permlane16/32_swap(v, v) the two results hold, in every lane, its own
+ * value and its partner's (in some order), and op(own, partner) is the same
+ * either way. */
+template <int G, typename F>
+__device__ __forceinline__ uint32_t group_reduce(uint32_t v, F op)
+{
+    if constexpr (G >= 2) v = op(v, dpp<0xB1>(v));
+    if constexpr (G >= 4) v = op(v, dpp<0x4E>(v));
+    if constexpr (G >= 8) v = op(v, dpp<0x141>(v));
+    if constexpr (G >= 16) v = op(v, dpp<0x140>(v));
+    if constexpr (G >= 32) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = op(r[0], r[1]);
+    }
+    if constexpr (G >= 64) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = op(r[0], r[1]);
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t) __shfl_xor(v, o));
-    return v;
+    return group_reduce<64>(v, [](uint32_t a, uint32_t b) { return max(a, b); });
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t) __shfl_xor(v, o));
-    return v;
+    return group_reduce<64>(v, [](uint32_t a, uint32_t b) { return min(a, b); });
 }
 
 template <int L>
 __device__ __forceinline__ uint32_t group_max(uint32_t v)
 {
-#pragma unroll
-    for (int o = L / 2; o > 0; o >>= 1) v = max(v, (uint32_t) __shfl_xor(v, o));
-    return v;
+    return group_reduce<L>(v, [](uint32_t a, uint32_t b) { return max(a, b); });
+}
+
+template <int L>
+__device__ __forceinline__ uint32_t group_or(uint32_t v)
+{
+    return group_reduce<L>(v, [](uint32_t a, uint32_t b) { return a | b; });
 }
 
 __device__ __forceinline__ void zero_range(uint8_t *dst, uint32_t from, uint32_t to, int q, int L)

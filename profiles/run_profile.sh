@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
     -- python3 "$R/bench.py" --no-cpu --no-e2e "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
-PMC_ARGS=(--no-cpu --no-e2e --steps 2 --warmup 1 --records 262144 "$@")
+PMC_ARGS=(--no-cpu --no-e2e --steps 2 --warmup 1 --records ${PMC_RECORDS:-262144} "$@")
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
     --kernel-trace -d "$OUT/pmc_sq1" -o run --output-format csv \
     -- python3 "$R/bench.py" "${PMC_ARGS[@]}" > "$OUT/pmc_sq1.json" 2> "$OUT/pmc_sq1.err"

@@ -241,6 +241,9 @@ static void *thr_main(void *arg)
     return NULL;
 }
 
+/* libtlsrec internal: how many coalesced batches carried how many records */
+void tlsrec__engine_stats(uint64_t *batches, uint64_t *records);
+
 static int threads(char **a)
 {
     const int nt = atoi(a[0]), records = atoi(a[1]);
@@ -258,8 +261,11 @@ static int threads(char **a)
         bad += jobs[i].bad;
     }
     const double us = now_us() - t0;
-    printf("{\"threads\": %d, \"records_per_thread\": %d, \"round_trips_per_s\": %.0f, \"bad\": %d}\n", nt, records,
-           1e6 * nt * records / us, bad);
+    uint64_t nb = 0, nr = 0;
+    tlsrec__engine_stats(&nb, &nr);
+    printf("{\"threads\": %d, \"records_per_thread\": %d, \"round_trips_per_s\": %.0f, \"bad\": %d, "
+           "\"engine_batches\": %llu, \"engine_records\": %llu, \"records_per_batch\": %.2f}\n", nt, records,
+           1e6 * nt * records / us, bad, (unsigned long long) nb, (unsigned long long) nr, nb ? (double) nr / nb : 0.0);
     return bad ? 1 : 0;
 }
 
