@@ -258,6 +258,14 @@ static uint32_t gcm_tm(void)
     return e ? (uint32_t) atoi(e) & 3u : 1u;
 }
 
+/* paired wave passes (16 waves, two per key table) for small records of many
+ * keys; TLSREC_GCM_PAIR=0 keeps the 8-wave wave passes (read per batch) */
+static int gcm_pair_env(void)
+{
+    const char *e = getenv("TLSREC_GCM_PAIR");
+    return e ? atoi(e) : 1;
+}
+
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */
 static uint32_t gcm_lanes_env(void)
 {
@@ -525,8 +533,29 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
             L = 16;        /* a wave per 4 records, each wave its records' keys */
             wp = true;
         }
+        /* Paired wave passes: small records (<= 4 KiB), 12..127 per key.  The
+         * 8-wave passes above hold one 8 KiB H^L table per wave beside the
+         * 64 KiB T-tables, so they run at half the single-key kernel's
+         * occupancy and wait on LDS latency (r02 PMC, DTLS 16 x 1.4 KiB per
+         * key: LDS 35 %, VALU 53 % busy); with two waves per table, 16 waves
+         * fit.  Each wave takes half of a key's records, so L is picked for
+         * a round to hold that half: 2 lanes (32 records) from 48 records per
+         * key, 4 from 24, 8 below. */
+        /* Large records (known > 4 KiB) with 4..11 per key (k4, 16 KiB
+         * streams): the same pairing at 16 or 32 lanes, 4 or 2 records of a key
+         * per wave. */
+        bool pair = false;
+        if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0) {
+            int Lp = 0;
+            if (small) Lp = rpk >= 48 ? 2 : (rpk >= 24 ? 4 : 8);
+            else if (avg_bytes > 4096 && rpk >= 4 && rpk < 12) Lp = rpk >= 8 ? 16 : 32;
+            if (Lp && (uint64_t) n >= (uint64_t) cu * 16 * (uint64_t) (64 / Lp)) {
+                L = Lp;
+                wp = pair = true;
+            }
+        }
         if (L == 2 && !wp) L = 4;     /* 2 lanes: wave passes only */
-        const int waves = wp ? 8 : (kt->has_cid ? 16 : gcm_waves());
+        const int waves = pair ? 16 : (wp ? 8 : (kt->has_cid ? 16 : gcm_waves()));
         a.rpw = opt.coalesced ? (uint32_t) (64 / L) : pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
@@ -535,7 +564,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.skip = skip;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
-        if (tlsrec__launch_gcm(&a, dec, L, nr, wp ? -8 : (kt->has_cid ? -16 : waves), grid, st) != hipSuccess)
+        if (tlsrec__launch_gcm(&a, dec, L, nr, pair ? -32 : (wp ? -8 : (kt->has_cid ? -16 : waves)), grid, st) !=
+            hipSuccess)
             rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     /* ARIA-GCM and Camellia-GCM: the GCM kernel around the LDS-table cipher
@@ -883,13 +913,30 @@ struct EngineReq {
     EngineReq *next;
 };
 
-/* one staging set: [descriptors][results][arena], pinned host and device */
+/* one staging set: [descriptors][results][arena], pinned host memory the
+ * device can address (hd = its device address), and a device copy */
 struct EngineSet {
     hipStream_t st;
-    uint8_t *h, *d;
+    uint8_t *h, *hd, *d;
     size_t cap;
     int busy;
 };
+
+/* Batches up to this many staged bytes run zero-copy: the kernels read the
+ * records from, and write them back to, the pinned staging area over PCIe
+ * (no copy-engine round trips: measured on MI355X, an H2D or D2H copy of a
+ * small record costs ~12 us with its sync, a whole kernel launch ~10 us,
+ * tools/probes/latency_probe.hip).  TLSREC_ENGINE_ZC=0 stages through device
+ * memory always; =<bytes> moves the bound. */
+static size_t engine_zc_max(void)
+{
+    static size_t v = (size_t) -1;
+    if (v == (size_t) -1) {
+        const char *e = getenv("TLSREC_ENGINE_ZC");
+        v = e ? (size_t) strtoull(e, NULL, 0) : (size_t) (64u << 10);
+    }
+    return v;
+}
 
 struct Combiner {
     pthread_mutex_t mu;
@@ -1042,11 +1089,11 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
         hipStreamSynchronize(S.st);
         hipHostFree(S.h);
         hipFree(S.d);
-        S.h = NULL;
-        S.d = NULL;
+        S.h = S.hd = S.d = NULL;
         S.cap = 0;
         const size_t want = need > (1u << 20) ? need + need / 2 : (1u << 20);
-        if (hipHostMalloc((void **) &S.h, want, hipHostMallocDefault) != hipSuccess ||
+        if (hipHostMalloc((void **) &S.h, want, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void **) &S.hd, S.h, 0) != hipSuccess ||
             hipMalloc((void **) &S.d, want) != hipSuccess)
             return TLSREC_ERR_SSL_ALLOC_FAILED;
         S.cap = want;
@@ -1074,11 +1121,13 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
         (r->dec ? mask_d : mask_e) |= 1u << r->cipher;
     }
     const size_t total = off_arena + used;
-    hipError_t e = hipMemcpyAsync(S.d, S.h, total, hipMemcpyHostToDevice, S.st);
+    const bool zc = total <= engine_zc_max();
+    uint8_t *base = zc ? S.hd : S.d;
+    hipError_t e = zc ? hipSuccess : hipMemcpyAsync(S.d, S.h, total, hipMemcpyHostToDevice, S.st);
     int rc = e == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    tlsrec_batch_rec *dd = (tlsrec_batch_rec *) S.d;
-    tlsrec_batch_res *dr = (tlsrec_batch_res *) (S.d + off_res);
-    uint8_t *da = S.d + off_arena;
+    tlsrec_batch_rec *dd = (tlsrec_batch_rec *) base;
+    tlsrec_batch_res *dr = (tlsrec_batch_res *) (base + off_res);
+    uint8_t *da = base + off_arena;
     BatchOpt o;
     o.prefilled = true;
     o.coalesced = n > 1;
@@ -1091,7 +1140,7 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
         rc = batch(kt, dd + ne, dr + ne, n - ne, da, da, 0, S.st, 1, o);
     }
     if (!rc) {
-        e = hipMemcpyAsync(S.h + off_res, S.d + off_res, total - off_res, hipMemcpyDeviceToHost, S.st);
+        e = zc ? hipSuccess : hipMemcpyAsync(S.h + off_res, S.d + off_res, total - off_res, hipMemcpyDeviceToHost, S.st);
         if (e == hipSuccess) e = hipStreamSynchronize(S.st);
         if (e != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else {

@@ -31,18 +31,47 @@ namespace tlsrec {
  * multiplies by H^8 .. H^1 held as values (gtree_v, GcmArgs::tm). */
 /* G5: the Horner table H^L is the 13 KiB 5-bit form (gmul5) after the tree's
  * 4-bit tables H^1 .. H^(L/2). */
-template <int L, int W, bool WP = false, bool G5 = false>
+/* PAIR (paired wave passes): 16 waves, the two waves of a pair share one
+ * H^L table (8 pairs x 8 KiB), so small records of many keys run at the
+ * 16-wave occupancy of the single-key kernel; the AAD-fold slots shrink to
+ * one per record of a round (64 / L per wave) to fit. */
+template <int L, int W, bool WP = false, bool G5 = false, bool PAIR = false>
 struct GcmLds {
-    static constexpr int NT = WP ? W : Log2<L>::v + (G5 ? 0 : 1);  /* 4-bit GHASH tables, or one H^L per wave */
-    static constexpr int GH = 0;
-    static constexpr int HG5 = NT * 8192;               /* G5 Horner table */
-    static constexpr int AES = HG5 + (G5 ? KEY_G5_WORDS * 16 : 0);   /* T0/T1 x 32 copies */
-    static constexpr int EJ0 = AES + 65536;             /* W waves x 64 x 16 B */
-    static constexpr int FOLD = EJ0 + W * 64 * 16;      /* W waves x 64 x 16 B: AAD fold */
-    static constexpr int CTL = FOLD + W * 64 * 16;
-    static constexpr int BYTES = CTL + 16;
+    static constexpr int NT = PAIR ? W / 2 : (WP ? W : Log2<L>::v + (G5 ? 0 : 1));  /* 4-bit GHASH tables */
+    /* The wave-pass kernels hold 64 KiB of per-wave (per-pair) tables: the
+     * T-tables go first there, so that every lookup address (< 64 KiB) folds
+     * into the 16-bit ds_read offset; behind 64 KiB of tables each of the 202
+     * lookups of a step cost one more v_or for its address.  The per-wave
+     * tables are addressed from a register base anyway. */
+    static constexpr int GH = WP ? 65536 : 0;
+    static constexpr int HG5 = GH + NT * 8192;          /* G5 Horner table */
+    static constexpr int AES = WP ? 0 : HG5 + (G5 ? KEY_G5_WORDS * 16 : 0);   /* T0/T1 x 32 copies */
+    static constexpr int EJ0 = WP ? HG5 : AES + 65536;  /* W waves x 64 x 16 B */
+    static constexpr int FOLDN = PAIR ? 64 / L : 64;    /* AAD-fold slots per wave */
+    static constexpr int FOLD = EJ0 + W * 64 * 16;      /* W waves x FOLDN x 16 B: AAD fold */
+    static constexpr int CTL = FOLD + W * FOLDN * 16;
+    static constexpr int BYTES = CTL + (PAIR ? 128 : 16);
     static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
+
+/* Barrier of the two waves of a pair (PAIR): a monotonic LDS counter that
+ * both waves bump once per barrier; every wave of a pair passes the same
+ * number of barriers (both see the same key sequence), so the spin always
+ * ends. The fences order the table writes before the bump and the reads
+ * after it. */
+__device__ __forceinline__ void pair_sync(uint32_t *cnt, uint32_t &phase, int lane)
+{
+    phase += 2;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v >= phase) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 /* Per-record state that the AEAD loop reads (kept small: it lives in
  * VGPRs across the loop). */
@@ -136,11 +165,12 @@ __device__ __forceinline__ uint4 gtree(const uint8_t *lds, uint4 Y, int lane, in
 /* ARIA: the block cipher is ARIA (NR = 12/14/16 rounds, S-box tables in the
  * T-table LDS region, round keys SlotState::ark) -- GCM around it unchanged */
 template <int L, int NR, bool DEC, int W, int B, bool WP = false, bool CID = false, bool ARIA = false,
-          bool G5 = false>
+          bool G5 = false, bool PAIR = false>
 __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
 {
     static_assert(!G5 || (L == 1 << KEY_G5_POWER && !WP && !CID && !ARIA && B == 1), "G5: the 8-lane 16-wave kernel");
-    using LY = GcmLds<L, W, WP, G5>;
+    static_assert(!PAIR || (WP && W == 16 && B == 1 && !CID && !ARIA && !G5), "PAIR: 16-wave paired wave passes");
+    using LY = GcmLds<L, W, WP, G5, PAIR>;
     constexpr int NTHR = W * 64;
     constexpr int LOGL = Log2<L>::v;
     constexpr int R = 64 / L;
@@ -165,11 +195,16 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     else
         aes_fill_tables(lds + LY::AES, tid, NTHR);
 
+    /* PAIR: wave w is half ph of pair pr; the pair owns 2 rpw contiguous
+     * positions and its halves take them alternately, so both see the same
+     * key runs */
+    const int pr = wave & (W / 2 - 1), ph = wave / (W / 2);
     /* pass membership: lane l tracks the record at chunk position k = l */
     uint32_t my_slot = 0xffffffffu, my_rec = 0;
     {
         /* WP: a wave's positions are contiguous (its key runs stay together) */
-        const uint64_t pos = WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
+        const uint64_t pos = PAIR ? wg_base + (uint64_t) pr * 2 * a.rpw + 2 * (uint64_t) lane + (uint64_t) ph
+                             : WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const uint32_t s = a.recs[my_rec].slot;
@@ -184,14 +219,32 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
         }
     }
     if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
+    if (PAIR && tid >= 4 && tid < 32) ctl[tid] = 0;     /* pair minima [4, 20), barrier counters [20, 28) */
     __syncthreads();
 
     /* Horner multiplier table H^L (hor) and the per-record tables H^1..H^(L/2) (gp) */
     constexpr int HPI = WP ? 0 : LOGL;                   /* H^L table index from hor */
-    const uint8_t *hor = WP ? lds + LY::GH + wave * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
+    const uint8_t *hor = WP ? lds + LY::GH + (PAIR ? pr : wave) * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
+    uint32_t phase = 0;                                  /* PAIR barrier count */
     for (int iter = 0;; iter++) {
         uint32_t s;
-        if constexpr (WP) {
+        if constexpr (PAIR) {
+            /* the pair's smallest pending slot: both halves agree on it, stage
+             * half of its H^L table each, and meet before the table is used
+             * (the first barrier also tells the pair the previous table is no
+             * longer read) */
+            uint32_t *pmin = ctl + 4 + 2 * pr;
+            uint32_t *pcnt = ctl + 20 + pr;
+            const uint32_t m = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
+            if (lane == 0) pmin[ph] = m;
+            pair_sync(pcnt, phase, lane);
+            s = __builtin_amdgcn_readfirstlane(min(pmin[0], pmin[1]));
+            if (s == 0xffffffffu) break;
+            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
+            uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
+            for (int i = lane + ph * 256; i < (ph + 1) * 256; i += 64) dst[i] = src[i];
+            pair_sync(pcnt, phase, lane);
+        } else if constexpr (WP) {
             /* wave pass: the wave's smallest pending slot; stage its H^L table
              * into the wave's LDS (in-order LDS queue: the wave's writes land
              * before its reads; the asm keeps the compiler from hoisting) */
@@ -287,7 +340,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
              * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
              * only the step with cc == 0 reads it. */
-            uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + wave * 64 + lane;
+            uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + (PAIR ? wave * LY::FOLDN + g : wave * 64 + lane);
             if (jb.run && (uint32_t) q == z % L)      /* the lane that holds block 0 (cc == 0) */
                 *fold = m ? gmul<0>(gp, jb.aadw) : jb.aadw;
             /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
@@ -479,6 +532,15 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
  * Launchers
  * ==================================================================== */
 template <int L, int NR, bool DEC>
+static hipError_t launch_gcm_pair(const GcmArgs &a, uint32_t grid, hipStream_t st)
+{
+    /* paired wave passes: 16 waves x 1 block per lane, a pair per H^L table */
+    hipLaunchKernelGGL((tlsrec_gcm_kernel<L, NR, DEC, 16, 1, true, false, false, false, true>), dim3(grid),
+                       dim3(16 * 64), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int L, int NR, bool DEC>
 static hipError_t launch_gcm_wp(const GcmArgs &a, uint32_t grid, hipStream_t st)
 {
     /* wave passes: 8 waves x 2 blocks per lane (LDS: 8 x 8 KiB H^L + 64 KiB T-tables) */
@@ -538,6 +600,13 @@ static hipError_t launch_gcm_nr(const GcmArgs &a, int nr, int waves, uint32_t gr
         }
         return hipErrorInvalidValue;
     }
+    if (waves == -32) {  /* paired wave passes (engine: many keys, small records) */
+        if constexpr (L == 4 || L == 8 || L == 16) {
+            if (nr == 10) return launch_gcm_pair<L, 10, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_pair<L, 14, DEC>(a, grid, st);
+        }
+        return hipErrorInvalidValue;
+    }
     if (waves == -8) {   /* wave-pass variant (engine: many keys, few records each) */
         if constexpr (L == 4 || L == 16 || L == 64) {
             if (nr == 10) return launch_gcm_wp<L, 10, DEC>(a, grid, st);
@@ -556,6 +625,11 @@ hipError_t gcm_dispatch(const GcmArgs &a, int lanes, int nr, int waves, uint32_t
 {
     switch (lanes) {
         case 2:   /* wave passes only */
+            if (waves == -32) {
+                if (nr == 10) return launch_gcm_pair<2, 10, DEC>(a, grid, st);
+                if (nr == 14) return launch_gcm_pair<2, 14, DEC>(a, grid, st);
+                return hipErrorInvalidValue;
+            }
             if (waves != -8) return hipErrorInvalidValue;
             if (nr == 10) return launch_gcm_wp<2, 10, DEC>(a, grid, st);
             if (nr == 14) return launch_gcm_wp<2, 14, DEC>(a, grid, st);
@@ -563,6 +637,11 @@ hipError_t gcm_dispatch(const GcmArgs &a, int lanes, int nr, int waves, uint32_t
         case 4: return launch_gcm_nr<4, DEC>(a, nr, waves, grid, st);
         case 8: return launch_gcm_nr<8, DEC>(a, nr, waves, grid, st);
         case 16: return launch_gcm_nr<16, DEC>(a, nr, waves, grid, st);
+        case 32:  /* paired wave passes only (a wave holds 2 records of a key) */
+            if (waves != -32) return hipErrorInvalidValue;
+            if (nr == 10) return launch_gcm_pair<32, 10, DEC>(a, grid, st);
+            if (nr == 14) return launch_gcm_pair<32, 14, DEC>(a, grid, st);
+            return hipErrorInvalidValue;
         case 64: return launch_gcm_nr<64, DEC>(a, nr, waves, grid, st);
         default: return hipErrorInvalidValue;
     }

@@ -41,13 +41,17 @@ def _threads():
     return bench.host_cores()[0]
 
 
-def _layout(n, head, rng):
+def _layout(n, head, rng, span=None):
     """lengths (25 % edge values, 75 % uniform 0..2048, every edge value at
-    least 100 times), 128-B aligned record buffers with tag / padding room"""
-    lens = rng.integers(0, 2049, n).astype(np.uint32)
-    pick = rng.random(n) < 0.25
-    lens[pick] = EDGE[rng.integers(0, len(EDGE), int(pick.sum()))]
-    lens[:len(EDGE) * 100] = np.tile(EDGE, 100)
+    least 100 times; or uniform in span), 128-B aligned record buffers with
+    tag / padding room"""
+    if span:
+        lens = rng.integers(span[0], span[1] + 1, n).astype(np.uint32)
+    else:
+        lens = rng.integers(0, 2049, n).astype(np.uint32)
+        pick = rng.random(n) < 0.25
+        lens[pick] = EDGE[rng.integers(0, len(EDGE), int(pick.sum()))]
+        lens[:len(EDGE) * 100] = np.tile(EDGE, 100)
     size = head + lens.astype(np.uint64) + 48
     al = (size + 127) // 128 * 128
     off = np.zeros(n, dtype=np.uint64)
@@ -70,11 +74,29 @@ CASES = [(c, v) for c in (M.CIPHER_AES_128_GCM, M.CIPHER_AES_256_GCM, M.CIPHER_C
 @pytest.mark.parametrize("nkeys,n", [(16, 100_000), (1, 30_000)], ids=["16keys", "1key"])
 @pytest.mark.parametrize("cipher,ver", CASES, ids=lambda x: str(x))
 def test_bulk_records_vs_openssl_evp(cipher, ver, nkeys, n):
+    _evp_case(cipher, ver, nkeys, n)
+
+
+@pytest.mark.parametrize("nkeys,rpk,span,mean", [(2048, 64, (1000, 1500), 1300), (2048, 32, (1000, 1500), 1300),
+                                                  (4096, 16, (1000, 1500), 1300), (4096, 8, (12000, 16383), 14000),
+                                                  (8192, 4, (12000, 16383), 14000)],
+                         ids=["L2", "L4", "L8", "L16", "L32"])
+@pytest.mark.parametrize("cipher,ver", [(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3), (M.CIPHER_AES_128_GCM, M.VERSION_TLS1_2)],
+                         ids=lambda x: str(x))
+def test_paired_wave_passes_vs_openssl_evp(cipher, ver, nkeys, rpk, span, mean):
+    """many keys x 4..64 records, round-robin over keys, with the record-size
+    hint: the paired wave passes (16 waves, two per key table) at 2, 4 and 8
+    lanes for ~1.4 KiB records and 16, 32 lanes for ~14 KiB records"""
+    _evp_case(cipher, ver, nkeys, nkeys * rpk, lens=span, mean_bytes=mean)
+
+
+def _evp_case(cipher, ver, nkeys, n, lens=None, mean_bytes=0):
     torch = _torch()
     dev = torch.device("cuda")
-    rng = np.random.default_rng(cipher * 100 + ver + nkeys)
+    rng = np.random.default_rng(cipher * 100 + ver + nkeys + n)
     head = 8 if ver == M.VERSION_TLS1_2 and cipher != M.CIPHER_CHACHA20_POLY1305 else 0
-    lens, size, off, total = _layout(n, head, rng)
+    lens_, size, off, total = _layout(n, head, rng, lens)
+    lens = lens_
     keys, ivs = _keys(cipher, nkeys, rng)
     kl = M.KEYLEN[cipher]
     km = np.concatenate([M.key_material(cipher, ver, bytes(k[:kl]), bytes(v)) for k, v in zip(keys, ivs)])
@@ -99,7 +121,7 @@ def test_bulk_records_vs_openssl_evp(cipher, ver, nkeys, n):
         out = torch.zeros_like(arena)
         res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
         recs = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
-        M.batch_encrypt(kt, recs, res, n, arena, out)
+        M.batch_encrypt(kt, recs, res, n, arena, out, mean_bytes=mean_bytes)
         torch.cuda.synchronize()
         r = res.cpu().numpy().view(M.BATCH_RES)
         inner = lens + 1 + (16 - (lens + 1) % 16) % 16 if ver == M.VERSION_TLS1_3 else lens
@@ -120,7 +142,7 @@ def test_bulk_records_vs_openssl_evp(cipher, ver, nkeys, n):
         arena = torch.from_numpy(sealed).to(dev)
         res.zero_()
         recs = torch.from_numpy(dd.view(np.uint8).copy()).to(dev)
-        M.batch_decrypt(kt, recs, res, n, arena, arena)
+        M.batch_decrypt(kt, recs, res, n, arena, arena, mean_bytes=mean_bytes)
         torch.cuda.synchronize()
         r = res.cpu().numpy().view(M.BATCH_RES)
         assert (r["status"] == 0).all(), np.unique(r["status"])
