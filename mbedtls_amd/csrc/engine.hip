@@ -530,7 +530,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         bool wp = !kt->has_cid && !identity && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
                   (wpe == 1 || (wpe != 0 && light));
         if (opt.coalesced && auto_l && !kt->has_cid && nr != 12) {
-            L = 16;        /* a wave per 4 records, each wave its records' keys */
+            L = 16;        /* a wave per record: each wave its own record's key, in parallel */
             wp = true;
         }
         /* Paired wave passes: small records (<= 4 KiB), 12..127 per key.  The
@@ -556,11 +556,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         }
         if (L == 2 && !wp) L = 4;     /* 2 lanes: wave passes only */
         const int waves = pair ? 16 : (wp ? 8 : (kt->has_cid ? 16 : gcm_waves()));
-        a.rpw = opt.coalesced ? (uint32_t) (64 / L) : pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
+        a.rpw = (opt.coalesced && wp) ? 1u : pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         a.g5 = gcm_g5();
-        a.tm = gcm_tm();
+        /* coalesced calls wait on the lane tree: from the key's tables (one
+         * L2 round trip per level) rather than table-free (~1 700 dependent
+         * VALU ticks per level) */
+        a.tm = opt.coalesced ? 0u : gcm_tm();
         a.skip = skip;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
@@ -896,7 +899,7 @@ extern "C" int tlsrec_host_batch_decrypt(tlsrec_keytab *kt, const tlsrec_batch_r
  * ==================================================================== */
 #define ENGINE_PAGE_SLOTS 4096
 #define ENGINE_MAX_PAGES 256
-#define ENGINE_SETS 2                    /* batches of a page in flight at once */
+#define ENGINE_SETS 4                    /* batches of a page in flight at once (own streams) */
 #define ENGINE_BATCH 256                 /* records per coalesced batch */
 #define ENGINE_ALIGN 128                 /* record slots in the staging arena */
 
@@ -1130,7 +1133,7 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
     uint8_t *da = base + off_arena;
     BatchOpt o;
     o.prefilled = true;
-    o.coalesced = n > 1;
+    o.coalesced = true;     /* identity order, a wave per GCM record (one record too: 8 KiB of tables, not 56) */
     if (!rc && ne) {
         o.only_mask = mask_e;
         rc = batch(kt, dd, dr, ne, da, da, 0, S.st, 0, o);
