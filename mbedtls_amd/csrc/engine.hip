@@ -529,8 +529,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
             L = small2 ? 2 : (small4 ? 4 : ((rpk >= 3 && Lfill <= 16) ? 16 : 64));
         bool wp = !kt->has_cid && !identity && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
                   (wpe == 1 || (wpe != 0 && light));
-        if (opt.coalesced && auto_l && !kt->has_cid && nr != 12) {
-            L = 16;        /* a wave per record: each wave its own record's key, in parallel */
+        if (opt.coalesced && n > 1 && auto_l && !kt->has_cid && nr != 12) {
+            L = 64;        /* a wave per record, 64 lanes on it: each wave its own record's key, in parallel */
             wp = true;
         }
         /* Paired wave passes: small records (<= 4 KiB), 12..127 per key.  The
@@ -899,7 +899,7 @@ extern "C" int tlsrec_host_batch_decrypt(tlsrec_keytab *kt, const tlsrec_batch_r
  * ==================================================================== */
 #define ENGINE_PAGE_SLOTS 4096
 #define ENGINE_MAX_PAGES 256
-#define ENGINE_SETS 4                    /* batches of a page in flight at once (own streams) */
+#define ENGINE_SETS 2                    /* batches of a queue in flight at once (own streams) */
 #define ENGINE_BATCH 256                 /* records per coalesced batch */
 #define ENGINE_ALIGN 128                 /* record slots in the staging arena */
 
@@ -949,11 +949,23 @@ struct Combiner {
     uint64_t batches, records;           /* statistics (tlsrec__engine_stats) */
 };
 
+/* A page queues records per (AEAD family, direction): each batch is then one
+ * kernel launch, and a call never waits behind another family's kernel --
+ * CCM's CBC-MAC is one dependent AES chain per record (a 1.4 KiB record is
+ * ~170 us on one lane), GCM and ChaCha20-Poly1305 records take ~25 us. */
+#define ENGINE_QUEUES 6
+static int engine_queue(uint32_t cipher, int dec)
+{
+    const int fam = cipher == TLSREC_CIPHER_CHACHA20_POLY1305 ? 1
+                    : (tlsrec_cipher_is_ccm((int) cipher) || tlsrec_cipher_is_alt_ccm((int) cipher)) ? 2 : 0;
+    return fam * 2 + (dec ? 1 : 0);
+}
+
 struct EnginePage {
     tlsrec_keytab *kt;
     uint8_t used[ENGINE_PAGE_SLOTS];
     uint32_t nused;
-    Combiner *co;
+    Combiner *co[ENGINE_QUEUES];
 };
 
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;   /* slot allocation, page growth */
@@ -1008,10 +1020,11 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
                 r = TLSREC_ERR_SSL_ALLOC_FAILED;
             } else {
                 r = tlsrec_keytab_create(&g_pages[pg].kt, ENGINE_PAGE_SLOTS);
-                if (r == 0 && !(g_pages[pg].co = combiner_new())) {
+                for (int q = 0; r == 0 && q < ENGINE_QUEUES; q++)
+                    if (!(g_pages[pg].co[q] = combiner_new())) r = TLSREC_ERR_SSL_ALLOC_FAILED;
+                if (r != 0 && g_pages[pg].kt) {
                     tlsrec_keytab_free(g_pages[pg].kt);
                     g_pages[pg].kt = NULL;
-                    r = TLSREC_ERR_SSL_ALLOC_FAILED;
                 }
                 if (r == 0) g_npages = pg + 1;
             }
@@ -1177,7 +1190,7 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
     const uint32_t cipher = kt->h_cipher[idx];
     if (cipher == 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
     if (buf_len > 0xffffffffu - 64) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co;
+    Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co[engine_queue(cipher, dec)];
     EngineReq me;
     me.dec = dec;
     me.d = *rec;
@@ -1232,14 +1245,15 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
 extern "C" void tlsrec__engine_stats(uint64_t *batches, uint64_t *records)
 {
     uint64_t b = 0, r = 0;
-    for (int pg = 0; pg < g_npages; pg++) {
-        Combiner *c = g_pages[pg].co;
-        if (!c) continue;
-        pthread_mutex_lock(&c->mu);
-        b += c->batches;
-        r += c->records;
-        pthread_mutex_unlock(&c->mu);
-    }
+    for (int pg = 0; pg < g_npages; pg++)
+        for (int q = 0; q < ENGINE_QUEUES; q++) {
+            Combiner *c = g_pages[pg].co[q];
+            if (!c) continue;
+            pthread_mutex_lock(&c->mu);
+            b += c->batches;
+            r += c->records;
+            pthread_mutex_unlock(&c->mu);
+        }
     if (batches) *batches = b;
     if (records) *records = r;
 }

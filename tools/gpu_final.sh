@@ -8,7 +8,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 mkdir -p gpurun_out
-TAG=${TAG:-r02i}
+TAG=${TAG:-r03}
 if [ "$1" = rows ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.txt 2>&1 || { echo "gpu tests failed"; tail -20 gpurun_out/gpu_tests.txt; exit 1; }
   tail -1 gpurun_out/gpu_tests.txt

@@ -13,8 +13,8 @@ row() {   # name, timeout, command...
 }
 summ() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d.get('value'), d.get('roofline',{}).get('kernel_ms_avg'), d.get('roofline',{}).get('frac'), d.get('check'))" $O/$1.json $1; }
 row c2 400 python3 bench.py && summ c2 &&
-for c in c3 c4 c1 ccm ccm8 gcm192 aria256 camellia128 chacha16k k4 c4s; do
-  row $c 400 python3 bench.py --config $c --no-e2e $( [ $c = c4 ] || [ $c = c4s ] || [ $c = k4 ] || [ $c = chacha16k ] && echo --no-cpu ) && summ $c || exit 1
+for c in c3 c4 c1 ccm ccm8 gcm192 aria256 camellia128 chacha16k k4 c4s c2s c3d; do
+  row $c 400 python3 bench.py --config $c --no-e2e && summ $c || exit 1
 done &&
 row stream16 300 python3 tools/bench_stream.py --conns 65536 --recs 16 && cat $O/stream16.json &&
 row stream4 300 python3 tools/bench_stream.py --conns 65536 --recs 4 && cat $O/stream4.json &&
@@ -26,4 +26,5 @@ row keysched 300 python3 tools/bench_keysched.py && cat $O/keysched.json &&
 : > $O/latency.jsonl &&
 for a in "2 1.3 16383" "2 1.3 1400" "3 1.3 1400" "1 1.2 1400" "2 1.3 100"; do
   timeout -k 10 120 ./tests/c/abi_host latency $a 2000 >> $O/latency.jsonl || exit 1
-done && timeout -k 10 120 ./tests/c/abi_host threads 16 400 >> $O/latency.jsonl && cat $O/latency.jsonl
+done && for t in 1 16 32; do timeout -k 10 120 ./tests/c/abi_host threads $t 2000 >> $O/latency.jsonl || exit 1; done &&
+cat $O/latency.jsonl
