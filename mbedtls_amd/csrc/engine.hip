@@ -368,7 +368,7 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
 {
     /* AES-128-GCM, AES-256-GCM, AES-192-GCM, AES-CCM slots, ChaCha, ARIA-128/192/256-GCM,
      * Camellia-128/192/256-GCM slots, end */
-    const size_t nk = 10 * (size_t) kt->capacity + 2;
+    const size_t nk = 10 * (size_t) kt->capacity + CP_SPREAD + 1;
     b.scan_bytes = tlsrec__scan_scratch_bytes((uint32_t) nk);
     const size_t al = 256;
     const size_t szk = (nk * 4 + al - 1) / al * al, szp = ((size_t) n * 4 + al - 1) / al * al;
@@ -572,14 +572,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
             rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     /* ARIA-GCM and Camellia-GCM: the GCM kernel around the LDS-table cipher
-     * (8 lanes, 16 waves); bucket classes (4, 5, 6) cap + 1 and (7, 8, 9) cap + 1 */
+     * (8 lanes, 16 waves); bucket classes (4, 5, 6) cap + CP_SPREAD and (7, 8, 9) cap + CP_SPREAD */
     static const int alt_gcm[6] = { TLSREC_CIPHER_ARIA_128_GCM, TLSREC_CIPHER_ARIA_192_GCM, TLSREC_CIPHER_ARIA_256_GCM,
                                     TLSREC_CIPHER_CAMELLIA_128_GCM, TLSREC_CIPHER_CAMELLIA_192_GCM,
                                     TLSREC_CIPHER_CAMELLIA_256_GCM };
     for (int ci = 0; ci < 6 && !rc; ci++) {
         const int c = alt_gcm[ci];
         if (!(cmask & (1u << c))) continue;
-        const size_t base = (size_t) (4 + ci) * cap + 1;
+        const size_t base = (size_t) (4 + ci) * cap + CP_SPREAD;
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;
@@ -638,7 +638,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.n = n;
         a.perm = identity ? nullptr : bs.perm;
         a.lo = identity ? nullptr : bs.offs + 4 * (size_t) cap;
-        a.hi = identity ? nullptr : bs.offs + 4 * (size_t) cap + 1;
+        a.hi = identity ? nullptr : bs.offs + 4 * (size_t) cap + CP_SPREAD;
         a.in = in;
         a.out = out;
         a.rpw = pick_rpw(n, CP_WAVES, 64 / L, (uint32_t) cu * 4);

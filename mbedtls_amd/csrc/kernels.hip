@@ -374,23 +374,24 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
  * Atomics are wave-aggregated when the wave's records share one key (a
  * batch already grouped by key costs one atomic per wave).
  * ==================================================================== */
-__device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec_batch_rec &d)
+__device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec_batch_rec &d, uint32_t i)
 {
     if (d.slot >= a.capacity) return 0xffffffffu;
     const int c = a.cipher_of[d.slot];
+    constexpr uint32_t S = CP_SPREAD;
     switch (c) {
         case TLSREC_CIPHER_AES_128_GCM: return d.slot;
         case TLSREC_CIPHER_AES_256_GCM: return a.capacity + d.slot;
         case TLSREC_CIPHER_AES_192_GCM: return 2 * a.capacity + d.slot;
-        case TLSREC_CIPHER_CHACHA20_POLY1305: return 4 * a.capacity;
-        /* ARIA-GCM classes after the ChaCha counter: 4 cap + 1 + (0..2) cap + slot */
-        case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + 1 + d.slot;
-        case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + 1 + d.slot;
-        case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + 1 + d.slot;
-        /* Camellia-GCM classes after ARIA's: (7, 8, 9) cap + 1 + slot */
-        case TLSREC_CIPHER_CAMELLIA_128_GCM: return 7 * a.capacity + 1 + d.slot;
-        case TLSREC_CIPHER_CAMELLIA_192_GCM: return 8 * a.capacity + 1 + d.slot;
-        case TLSREC_CIPHER_CAMELLIA_256_GCM: return 9 * a.capacity + 1 + d.slot;
+        case TLSREC_CIPHER_CHACHA20_POLY1305: return 4 * a.capacity + ((i >> 6) & (S - 1));   /* the wave's counter */
+        /* ARIA-GCM classes after the ChaCha counters: 4 cap + S + (0..2) cap + slot */
+        case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + S + d.slot;
+        case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + S + d.slot;
+        case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + S + d.slot;
+        /* Camellia-GCM classes after ARIA's: (7, 8, 9) cap + S + slot */
+        case TLSREC_CIPHER_CAMELLIA_128_GCM: return 7 * a.capacity + S + d.slot;
+        case TLSREC_CIPHER_CAMELLIA_192_GCM: return 8 * a.capacity + S + d.slot;
+        case TLSREC_CIPHER_CAMELLIA_256_GCM: return 9 * a.capacity + S + d.slot;
         default:
             return (tlsrec_cipher_is_ccm(c) || tlsrec_cipher_is_alt_ccm(c)) ? 3 * a.capacity + d.slot : 0xffffffffu;
     }
@@ -420,7 +421,7 @@ __device__ __forceinline__ uint32_t claim_group(uint32_t *ctr, uint32_t key, boo
  * grouped by key), else one per record (distinct addresses, no contention). */
 __device__ __forceinline__ uint32_t bucket_claim(const BucketArgs &a, uint32_t *ctr, uint32_t key)
 {
-    const bool cp = key == 4 * a.capacity;
+    const bool cp = key >= 4 * a.capacity && key < 4 * a.capacity + CP_SPREAD;
     const uint32_t pc = claim_group(ctr, key, cp);
     const uint32_t pg = claim_group(ctr, key, key != 0xffffffffu && !cp);
     return cp ? pc : pg;
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_count_kernel(BucketArgs a)
     uint32_t key = 0xffffffffu;
     if (i < a.n) {
         const tlsrec_batch_rec d = a.recs[i];
-        key = bucket_key(a, d);
+        key = bucket_key(a, d, i);
         if (key == 0xffffffffu)
             bad_slot_result(d, &a.res[i]);
         else

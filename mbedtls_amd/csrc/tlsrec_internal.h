@@ -20,6 +20,11 @@ constexpr int KEY_G5_OFF = KEY_TABLES * 512;        /* uint4 offset of the G5 ta
 constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512 + KEY_G5_WORDS;   /* uint4 entries per slot (69 KiB) */
 
 constexpr int GCM_WAVES = 16;                       /* default waves per workgroup (one WG per CU) */
+/* The bucket pass counts ChaCha20-Poly1305 records (one class for every key:
+ * the kernel takes each record's key itself) on CP_SPREAD counters, a wave's
+ * records on counter (wave index mod CP_SPREAD): on one counter, 2 M records
+ * round-robin over keys were 65 K same-address atomics, 0.75 ms of a c4s step. */
+constexpr uint32_t CP_SPREAD = 64;
 constexpr int CP_THREADS = 256;
 constexpr int ARIA_GCM_WAVES = 16;   /* waves per ARIA-GCM workgroup (kernels.hip launch_gcm_aria) */
 constexpr int CP_WAVES = CP_THREADS / 64;
@@ -92,7 +97,7 @@ struct BucketArgs {
     tlsrec_batch_res *res;
     uint32_t n;
     uint32_t capacity;
-    uint32_t *counts;         /* [nk = 10 * capacity + 2] records per (class, slot) */
+    uint32_t *counts;         /* [nk = 10 * capacity + CP_SPREAD + 1] records per (class, slot) */
     const uint32_t *offs;     /* [nk] their exclusive prefix sums (class start in perm) */
     uint2 *keyrank;           /* [n] each record's (key, rank within its key) from the count pass */
     uint32_t nk;
