@@ -251,11 +251,16 @@ static uint32_t gcm_g5(void)
  * instead of the key's H^8 / H^4 / H^2 / H^1 tables from HBM (24 KiB more per
  * key pass).  Same-box: k4 455 -> 461 GiB/s, stream 4 x 16 KiB per key
  * receive 424/429 -> 432/432.  TLSREC_GCM_TREEMUL=0 selects the tables. */
-static uint32_t gcm_tm(void)
+static uint32_t gcm_tm(bool pair)
 {
-    /* bit 0: 16-lane wave passes (default on); bit 1: 2- and 4-lane ones */
+    /* bit 0: 16-lane wave passes (default on); bit 1: 2- and 4-lane ones
+     * (default on for the paired passes: c4s 740 -> 750 GiB/s same-box; ±1 %
+     * in the 8-wave passes); bit 2: the AAD fold and the two final multiplies
+     * by H as a value too (default on for the paired passes, same-box: c4s
+     * 720 -> 742, k4 549 -> 558, 64 K keys x 16 x 1.4 KiB 362 -> 377 GiB/s:
+     * the key's 8 KiB H^1 table in global memory cost 32 lines per multiply) */
     const char *e = getenv("TLSREC_GCM_TREEMUL");
-    return e ? (uint32_t) atoi(e) & 3u : 1u;
+    return e ? (uint32_t) atoi(e) & 7u : (pair ? 7u : 1u);
 }
 
 /* paired wave passes (16 waves, two per key table) for small records of many
@@ -563,7 +568,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         /* coalesced calls wait on the lane tree: from the key's tables (one
          * L2 round trip per level) rather than table-free (~1 700 dependent
          * VALU ticks per level) */
-        a.tm = opt.coalesced ? 0u : gcm_tm();
+        a.tm = opt.coalesced ? 0u : gcm_tm(pair);
         a.skip = skip;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);

@@ -274,6 +274,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             __syncthreads();
         }
         const uint8_t *gp = WP ? reinterpret_cast<const uint8_t *>(a.ghtab + (size_t) s * KEY_TABLE_WORDS) : lds + LY::GH;
+        /* H as a value (wave passes, tm bit 2): the AAD fold and the final multiplies */
+        uint4 h1v = make_uint4(0, 0, 0, 0);
+        if constexpr (WP)
+            if (a.tm & 4u) __builtin_memcpy(&h1v, a.slots[s].h, 16);
         /* Round keys through the constant address space: scalar loads.  (Read
          * through a.slots they compile to vector loads + vmcnt(0) waits in
          * every round, since the kernel's own stores might alias the table.) */
@@ -341,8 +345,18 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
              * only the step with cc == 0 reads it. */
             uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + (PAIR ? wave * LY::FOLDN + g : wave * 64 + lane);
-            if (jb.run && (uint32_t) q == z % L)      /* the lane that holds block 0 (cc == 0) */
-                *fold = m ? gmul<0>(gp, jb.aadw) : jb.aadw;
+            /* the lane that holds block 0 (cc == 0) */
+            if (jb.run && (uint32_t) q == z % L) {
+                uint4 f = jb.aadw;
+                if (m) {
+                    if constexpr (WP)   /* tm bit 2: by H as a value -- the key's H^1 table is 8 KiB of
+                                         * global memory, and a multiply touches 32 lines of it */
+                        f = (a.tm & 4u) ? gf_mul_v(f, h1v) : gmul<0>(gp, f);
+                    else
+                        f = gmul<0>(gp, f);
+                }
+                *fold = f;
+            }
             /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
              * does not depend on step j's keystream, so its table reads share
              * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
@@ -469,9 +483,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 Y = gtree<L / 2>(gp, Y, lane, q);
             }
             if (q == 0) {                                            /* the group leader's sum */
-                Y = gmul<0>(gp, Y);                                  /* T */
                 uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
-                Y = gmul<0>(gp, xor4(Y, lenw));                      /* GHASH */
+                if (WP && (a.tm & 4u)) {
+                    Y = gf_mul_v(Y, h1v);                            /* T */
+                    Y = gf_mul_v(xor4(Y, lenw), h1v);                /* GHASH */
+                } else {
+                    Y = gmul<0>(gp, Y);                              /* T */
+                    Y = gmul<0>(gp, xor4(Y, lenw));                  /* GHASH */
+                }
             }
             if (!jb.run) continue;
             const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];

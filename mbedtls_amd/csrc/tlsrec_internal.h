@@ -68,7 +68,8 @@ struct GcmArgs {
     uint32_t capacity;
     uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM / _192_GCM */
     uint32_t g5;              /* host-side launch choice: 5-bit GHASH Horner table (8-lane, 16-wave kernel) */
-    uint32_t tm;              /* 16-lane wave passes: lane tree by table-free multiplies (tlsrec_clmul.h) */
+    uint32_t tm;              /* wave passes, table-free multiplies (tlsrec_clmul.h): bit 0 the 16-lane tree,
+                                 bit 1 the 2- / 4-lane tree, bit 2 the AAD fold and final multiplies */
     uint32_t skip;            /* test hook (tlsrec__test_skip_record): this record index is never reached */
 };
 
