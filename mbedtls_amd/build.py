@@ -29,7 +29,8 @@ C_FLAGS = ["-O2", "-fPIC", "-std=c11", "-Wall", "-Wextra", "-I" + INC, "-I" + CS
 
 HEADERS = ["tlsrec_device.h", "tlsrec_frame.h", "tlsrec_internal.h", "tlsrec_recdev.h", "tlsrec_gcm.h"]
 UNITS = [("gcm_dec.hip", "hip"), ("gcm_enc.hip", "hip"), ("gcm_alt_dec.hip", "hip"), ("gcm_alt_enc.hip", "hip"),
-         ("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("ccm.hip", "hip"), ("ticket.hip", "hip"), ("tlsrec_host.c", "c")]
+         ("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("ccm.hip", "hip"), ("ticket.hip", "hip"),
+         ("server.hip", "hip"), ("tlsrec_host.c", "c")]
 
 
 def _mtime(p):

@@ -968,6 +968,7 @@ static int engine_queue(uint32_t cipher, int dec)
 
 struct EnginePage {
     tlsrec_keytab *kt;
+    uint4 *d_hpw;                        /* H^1 .. H^64 per GCM slot (the record server's closing powers) */
     uint8_t used[ENGINE_PAGE_SLOTS];
     uint32_t nused;
     Combiner *co[ENGINE_QUEUES];
@@ -1025,6 +1026,8 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
                 r = TLSREC_ERR_SSL_ALLOC_FAILED;
             } else {
                 r = tlsrec_keytab_create(&g_pages[pg].kt, ENGINE_PAGE_SLOTS);
+                if (r == 0 && hipMalloc((void **) &g_pages[pg].d_hpw, sizeof(uint4) * 64 * ENGINE_PAGE_SLOTS) != hipSuccess)
+                    r = TLSREC_ERR_SSL_ALLOC_FAILED;
                 for (int q = 0; r == 0 && q < ENGINE_QUEUES; q++)
                     if (!(g_pages[pg].co[q] = combiner_new())) r = TLSREC_ERR_SSL_ALLOC_FAILED;
                 if (r != 0 && g_pages[pg].kt) {
@@ -1040,6 +1043,10 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
         for (int i = 0; i < ENGINE_PAGE_SLOTS; i++)
             if (!P.used[i]) { slot = i; break; }
         r = tlsrec_keytab_load(P.kt, (uint32_t) slot, 1, km, 0, g_load);
+        if (r == 0 && tlsrec_cipher_is_gcm(km->cipher) &&
+            tlsrec__launch_srv_hpow(P.kt->d_ghtab + (size_t) slot * KEY_TABLE_WORDS, P.d_hpw + (size_t) slot * 64,
+                                    g_load) != hipSuccess)
+            r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0 && hipStreamSynchronize(g_load) != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) {
             P.used[slot] = 1;
@@ -1178,10 +1185,19 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
     return rc;
 }
 
+/* server.hip: the resident record server (AES-GCM, ChaCha20-Poly1305) */
+extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const tlsrec_batch_rec *rec,
+                                  const void *slot_state, const void *ghtab, const void *hpw, unsigned char *buf,
+                                  size_t buf_len, uint32_t aead_pos, tlsrec_batch_res *out);
+
 /* Run one record through the kernels: host buffer -> device -> host.  A
- * decrypted record's CID (cid_len bytes) is staged right after the buffer. */
+ * decrypted record's CID (cid_len bytes) is staged right after the buffer.
+ * AES-GCM and ChaCha20-Poly1305 records of transforms without connection IDs
+ * go to the record server first (aead_pos: the plan's AEAD offset, which the
+ * server's staging aligns to 16 bytes); the coalescing launch path below takes
+ * every other record, and any the server does not take. */
 extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
-                                  const unsigned char *cid, tlsrec_batch_res *out)
+                                  const unsigned char *cid, uint32_t aead_pos, tlsrec_batch_res *out)
 {
     if (!g_ready) {
         pthread_mutex_lock(&g_mu);
@@ -1195,6 +1211,16 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
     const uint32_t cipher = kt->h_cipher[idx];
     if (cipher == 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
     if (buf_len > 0xffffffffu - 64) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if ((tlsrec_cipher_is_gcm((int) cipher) || cipher == TLSREC_CIPHER_CHACHA20_POLY1305) && !kt->has_cid &&
+        rec->cid_len == 0) {
+        tlsrec_batch_rec d = *rec;
+        d.slot = idx;
+        const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, kt->d_slots + idx,
+                                         kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS,
+                                         g_pages[rec->slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) idx * 64, buf,
+                                         buf_len, aead_pos, out);
+        if (r <= 0) return r;
+    }
     Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co[engine_queue(cipher, dec)];
     EngineReq me;
     me.dec = dec;

@@ -1,0 +1,742 @@
+/*
+ * server.hip -- the record server: a resident kernel that serves the
+ * single-record entry points (tlsrec_encrypt_buf / tlsrec_decrypt_buf, the
+ * drop-in for mbedtls_ssl_encrypt_buf / _decrypt_buf at ssl_msg.c:2697 and
+ * :3835) without a kernel launch, a copy-engine transfer or a stream sync
+ * per record.
+ *
+ * A call through the launch path costs ~10 us of launch + sync, ~12 us per
+ * copy-engine transfer and the kernel's own table staging:
+ * 33-41 us for a lone 1.4 KiB record.  Here each wave of a resident grid owns
+ * one request slot in pinned, host-mapped memory and polls it:
+ *
+ *   host thread                          server wave (slot i)
+ *   -----------                          --------------------
+ *   copy record into slot i, desc  ->
+ *   store hdr = (bytes, seq)       ->    sees hdr.seq != served (system-scope acquire)
+ *                                        one burst: descriptor + record -> LDS
+ *                                        AEAD in LDS (AES T-tables resident)
+ *                                        record + result -> slot i (posted writes)
+ *   spin on done == seq            <-    done = seq (system-scope release)
+ *   copy record out
+ *
+ * AES-128/192/256-GCM and ChaCha20-Poly1305 without connection IDs, records up
+ * to SRV_BUF bytes; everything else (CCM, ARIA, Camellia, CID transforms) stays
+ * on the coalescing launch path in engine.hip, which is also the fallback
+ * whenever the server cannot take a request.
+ *
+ * A record is served by one wave, 64 lanes, with the same framing plan and
+ * the same results as the batch kernels (tlsrec_recdev.h):
+ *   GCM: lane q takes the blocks j = q (mod 64) of the GHASH input A, C_1 ..
+ *        C_m, LEN (j = 0 the AAD, whose counter block J0 gives E_K(J0)), each
+ *        C block's keystream from the T-tables, a Horner chain per lane with
+ *        H^64 (the key's 4-bit table staged to LDS), then Y_q * H^(n - j_last)
+ *        (H^1 .. H^64 precomputed per key slot: tlsrec_srv_hpow_kernel) and an
+ *        XOR over the 64 lanes by DPP / permlane.
+ *   ChaCha20-Poly1305: lane q makes ChaCha20 block q (+ 64 k), block 0 being
+ *        the one-time Poly1305 key; Poly1305 runs the same lane-Horner form
+ *        with r^64 and r^1 .. r^64 built in LDS by doubling.
+ *
+ * Termination: a server grid lives `life` ticks of the device wall clock
+ * (TLSREC_SERVER_MS, default 20 ms) and at most `max_iter` polls, and leaves
+ * early on the set's stop word (process exit).  The host submits to a grid
+ * only inside its window minus a margin and launches the next grid on the
+ * other slot set when the window closes; a request the grid did not take
+ * (its kernel has ended) is withdrawn and runs on the launch path.
+ */
+#include <hip/hip_runtime.h>
+#include <atomic>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "tlsrec.h"
+#include "tlsrec_clmul.h"
+#include "tlsrec_device.h"
+#include "tlsrec_frame.h"
+#include "tlsrec_internal.h"
+#include "tlsrec_recdev.h"
+
+using namespace tlsrec;
+
+namespace {
+
+constexpr int SRV_WAVES = 2;                        /* waves (request slots) per workgroup */
+constexpr int SRV_GROUPS = 32;
+constexpr int SRV_SLOTS = SRV_WAVES * SRV_GROUPS;   /* 64 slots per set */
+constexpr uint32_t SRV_BUF = 17408;                 /* staged bytes per request (16 KiB record + room) */
+constexpr int SRV_TAB = 8192;                       /* per wave: H^64 table (GCM) / r^1..r^64 (ChaCha) */
+constexpr int SRV_WAVE_LDS = SRV_TAB + (int) SRV_BUF;
+constexpr int SRV_LDS = 65536 + SRV_WAVES * SRV_WAVE_LDS;
+static_assert(SRV_LDS <= 160 * 1024, "server LDS budget");
+static_assert(SRV_WAVE_LDS % 16 == 0, "16-byte aligned staging");
+
+/* Request descriptor, 96 bytes (read by lanes 0..5 as 16-byte chunks). */
+struct SrvDesc {
+    tlsrec_batch_rec d;       /* buf_off = alignment prefix, slot unused */
+    uint32_t dec, cipher, nr, pad;
+    uint64_t slot;            /* const SlotState * (device) */
+    uint64_t ghtab;           /* const uint4 *: the slot's GHASH tables (GCM) */
+    uint64_t hpw;             /* const uint4 *: H^1 .. H^64 (GCM) */
+    uint64_t pad2[2];
+};
+static_assert(sizeof(SrvDesc) == 96, "SrvDesc layout");
+
+/* One request slot in pinned host memory mapped into the device. */
+struct SrvReq {
+    uint64_t hdr;             /* seq (low 32) | staged bytes (high 32): one store posts the request */
+    uint8_t pad0[56];
+    uint32_t done;            /* seq of the last request served (device writes) */
+    uint8_t pad1[60];
+    SrvDesc desc;
+    tlsrec_batch_res res;
+    uint8_t pad2[16];
+    uint8_t buf[SRV_BUF];
+};
+static_assert(offsetof(SrvReq, done) == 64 && offsetof(SrvReq, desc) == 128 && offsetof(SrvReq, res) == 224 &&
+                  offsetof(SrvReq, buf) == 256 && sizeof(SrvReq) % 64 == 0,
+              "SrvReq layout");
+
+/* ---------------- LDS record access (16-byte aligned AEAD region) -------- */
+__device__ __forceinline__ uint4 lds16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+__device__ __forceinline__ void sts16(uint8_t *p, uint4 v) { *reinterpret_cast<uint4 *>(p) = v; }
+
+/* load_block (tlsrec_recdev.h) on the staged record */
+__device__ __forceinline__ uint4 srv_load_block(const uint8_t *src, uint32_t pos, uint32_t content_len,
+                                                uint32_t aead_len, uint8_t inner_type)
+{
+    uint4 v = lds16(src + pos);
+    if (pos + 16 <= content_len) return v;
+    v = mask_block(v, pos, content_len);
+    if (content_len >= pos && content_len < pos + 16 && content_len < aead_len) {
+        const uint32_t e = content_len - pos, sh = 8 * (e & 3), t = (uint32_t) inner_type << sh;
+        if ((e >> 2) == 0) v.x |= t;
+        else if ((e >> 2) == 1) v.y |= t;
+        else if ((e >> 2) == 2) v.z |= t;
+        else v.w |= t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void srv_store_block(uint8_t *dst, uint32_t pos, uint32_t len, uint4 v)
+{
+    if (pos + 16 <= len) {
+        sts16(dst + pos, v);
+        return;
+    }
+    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+        if (pos + i < len) dst[pos + i] = (uint8_t) (w[i >> 2] >> (8 * (i & 3)));
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i)
+{
+    const uint32_t w = (i >> 2) == 0 ? v.x : ((i >> 2) == 1 ? v.y : ((i >> 2) == 2 ? v.z : v.w));
+    return (w >> (8 * (i & 3))) & 0xffu;
+}
+
+__device__ __forceinline__ uint4 xor_all(uint4 v)
+{
+    auto x = [](uint32_t a, uint32_t b) { return a ^ b; };
+    return make_uint4(group_reduce<64>(v.x, x), group_reduce<64>(v.y, x), group_reduce<64>(v.z, x),
+                      group_reduce<64>(v.w, x));
+}
+
+/* x * y in GF(2^128) without tables (tlsrec_clmul.h) */
+__device__ __forceinline__ uint4 srv_gfmul(uint4 x, uint4 y)
+{
+    const uint32_t a[4] = { x.x, x.y, x.z, x.w }, b[4] = { y.x, y.y, y.z, y.w };
+    uint32_t r[4];
+    tlsrec_gf128_mul(a, b, r);
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+/* Everything a served record needs, uniform over the wave. */
+struct SrvJob {
+    tlsrec_batch_rec d;
+    const SlotState *st;
+    const uint4 *ghtab;
+    const uint4 *hpw;
+    tlsrec_key_material km;
+    uint8_t *rec;             /* the record's first byte in LDS (staging + d.buf_off) */
+};
+
+/* Result of a record whose plan stopped before the AEAD, or a finished one */
+__device__ __forceinline__ tlsrec_batch_res mk_res(int32_t status, const tlsrec_plan &p, uint8_t type, uint8_t cid_len)
+{
+    tlsrec_batch_res r;
+    r.status = status;
+    r.data_offset = p.data_offset;
+    r.data_len = p.data_len;
+    r.type = type;
+    r.cid_len = cid_len;
+    r.reserved[0] = r.reserved[1] = 0;
+    return r;
+}
+
+/* Tag handling shared by both AEADs: encrypt writes the tag and the explicit
+ * nonce, decrypt compares, wipes on a mismatch (PSA zeroes the output) and
+ * takes the TLS 1.3 inner type / length from the last non-zero byte. */
+template <bool DEC>
+__device__ __forceinline__ tlsrec_batch_res srv_finish(const SrvJob &J, const tlsrec_plan &p, uint4 tag, uint32_t nzkey,
+                                                       int lane)
+{
+    uint8_t *base = J.rec + p.aead_pos;
+    if (!DEC) {
+        if (lane < 16) base[p.aead_len + lane] = (uint8_t) byte_of(tag, (uint32_t) lane);
+        if (p.explicit_iv && p.post_status == 0 && lane < 8) {
+            uint32_t c[2];
+            __builtin_memcpy(c, J.d.ctr, 8);
+            J.rec[p.data_offset + lane] = (uint8_t) (c[lane >> 2] >> (8 * (lane & 3)));
+        }
+        return mk_res(p.post_status, p, p.type, p.cid_set ? p.cid_len : 0);
+    }
+    uint32_t diff = lane < 16 ? (base[p.aead_len + lane] ^ byte_of(tag, (uint32_t) lane)) : 0u;
+    diff = group_or<64>(diff);
+    const uint32_t key = group_max<64>(nzkey);
+    tlsrec_batch_res r = mk_res(0, p, J.d.type, 0);
+    if (diff != 0) {
+        for (uint32_t i = p.aead_pos + (uint32_t) lane; i < J.d.buf_len; i += 64) J.rec[i] = 0;
+        r.status = TLSREC_E_INVALID_MAC;
+    } else if (p.inner) {                                  /* ssl_msg.c:1809-1829 */
+        if (key == 0) {
+            r.status = TLSREC_E_INVALID_RECORD;
+        } else {
+            r.data_len = (key >> 8) - 1;
+            r.type = (uint8_t) (key & 0xff);
+        }
+    }
+    return r;
+}
+
+/* ---------------- AES-GCM, one record per wave ---------------------------- */
+template <int NR, bool DEC>
+__device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8_t *lds, uint8_t *tab, int lane)
+{
+    tlsrec_plan p;
+    make_plan<DEC, false>(p, J.d, J.km, J.st, J.rec - J.d.buf_off);
+    if (p.status != 0) {
+        tlsrec_batch_res r;
+        if (lane == 0) finish_early(p, J.d, J.rec - J.d.buf_off, &r);
+        r.status = __builtin_amdgcn_readfirstlane(r.status);
+        r.data_offset = __builtin_amdgcn_readfirstlane(r.data_offset);
+        r.data_len = __builtin_amdgcn_readfirstlane(r.data_len);
+        r.type = (uint8_t) __builtin_amdgcn_readfirstlane(r.type);
+        r.cid_len = (uint8_t) __builtin_amdgcn_readfirstlane(r.cid_len);
+        r.reserved[0] = r.reserved[1] = 0;
+        return r;
+    }
+    const int q = lane;
+    uint32_t nw[3];
+    nonce_words<DEC>(p, J.d, J.rec - J.d.buf_off, nw);
+    const uint32_t m = (p.aead_len + 15) >> 4;         /* C blocks */
+    const uint32_t n = m + 2;                          /* A, C_1 .. C_m, LEN */
+    const uint32_t K = (n + 63) >> 6;
+    const uint32_t content_len = DEC ? p.aead_len : p.content_len;
+    uint8_t *base = J.rec + p.aead_pos;
+
+    /* the key's H^64 table to LDS (the Horner multiplier), and this lane's
+     * closing power H^(n - j_last) */
+    const uint32_t kq = (uint32_t) q < n ? (n - 1 - (uint32_t) q) / 64 + 1 : 0;
+    const uint32_t dq = kq ? n - ((uint32_t) q + 64 * (kq - 1)) : 1;
+    const uint4 hd = J.hpw[dq - 1];
+    if (K > 1) {
+        const uint4 *src = J.ghtab + 6 * 512;
+#pragma unroll
+        for (int i = 0; i < 8; i++) sts16(tab + 16 * (lane + 64 * i), src[lane + 64 * i]);
+    }
+    /* round keys as uniform values (vector loads: the slot may be reloaded
+     * while the server runs, so nothing of it may sit in a scalar cache) */
+    uint32_t rk[60];
+    {
+        const uint32_t v = lane < 4 * (NR + 1) ? J.st->rkr[lane] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readlane(v, i);
+    }
+    const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
+    const uint4 aadw = aad_words(p);
+    const uint4 lenw = make_uint4(0, bswap32((uint32_t) p.aad_len * 8), 0, bswap32(p.aead_len * 8));
+    uint4 Y = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
+    uint32_t nzpos = 0;
+    for (uint32_t k = 0; k < K; k++) {
+        const uint32_t j = (uint32_t) q + 64 * k;
+        uint4 X = make_uint4(0, 0, 0, 0);
+        if (j <= m) {
+            const uint4 ks = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
+            if (j == 0) {
+                ej0 = ks;
+                X = aadw;
+            } else {
+                const uint32_t pos = (j - 1) * 16;
+                const uint4 blk = srv_load_block(base, pos, content_len, p.aead_len, p.inner_type);
+                const uint4 o = mask_block(xor4(blk, ks), pos, p.aead_len);
+                srv_store_block(base, pos, p.aead_len, o);
+                X = DEC ? blk : o;
+                if (DEC && p.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+            }
+        } else if (j == m + 1) {
+            X = lenw;
+        }
+        if (j < n) Y = k ? xor4(gmul<0>(tab, Y), X) : X;
+    }
+    if (kq) Y = srv_gfmul(Y, hd);
+    const uint4 S = xor_all(Y);
+    const uint4 e0 = make_uint4(__builtin_amdgcn_readlane(ej0.x, 0), __builtin_amdgcn_readlane(ej0.y, 0),
+                                __builtin_amdgcn_readlane(ej0.z, 0), __builtin_amdgcn_readlane(ej0.w, 0));
+    const uint4 tag = xor4(S, e0);
+    uint32_t nzkey = 0;
+    if (DEC && p.inner && nzpos) nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
+    return srv_finish<DEC>(J, p, tag, nzkey, lane);
+}
+
+/* ---------------- ChaCha20-Poly1305, one record per wave ------------------- */
+__device__ __forceinline__ P5 p_rd(const uint32_t *t) { P5 r; for (int i = 0; i < 5; i++) r.v[i] = t[i]; return r; }
+__device__ __forceinline__ void p_wr(uint32_t *t, const P5 &v) { for (int i = 0; i < 5; i++) t[i] = v.v[i]; }
+
+__device__ __forceinline__ P5 p_sum_all(P5 v, int lane)
+{
+    auto lvl = [&](auto sc) {
+        constexpr int S = decltype(sc)::value;
+        P5 w;
+#pragma unroll
+        for (int i = 0; i < 5; i++) w.v[i] = partner<S>(v.v[i], lane);
+        v = p_add(v, w);
+    };
+    lvl(std::integral_constant<int, 1>());
+    lvl(std::integral_constant<int, 2>());
+    lvl(std::integral_constant<int, 4>());
+    v = p_carry(v);                    /* 8 terms: limbs < 2^29 */
+    lvl(std::integral_constant<int, 8>());
+    lvl(std::integral_constant<int, 16>());
+    lvl(std::integral_constant<int, 32>());
+    return p_carry(v);
+}
+
+/* Poly1305 of A, C_1 .. C_M, LEN over the record's ciphertext in LDS:
+ * sum_j X_j r^(n - j), lane q taking j = q (mod 64) */
+__device__ __forceinline__ P5 srv_poly(const uint8_t *base, const tlsrec_plan &p, const uint32_t *rpow, int lane)
+{
+    const uint32_t M = (p.aead_len + 15) >> 4;
+    const uint32_t n = M + 2;
+    const uint32_t K = (n + 63) >> 6;
+    const P5 r64 = p_rd(rpow + 5 * 63);
+    const uint4 aadw = aad_words(p);
+    P5 Y = p_zero();
+    for (uint32_t k = 0; k < K; k++) {
+        const uint32_t j = (uint32_t) lane + 64 * k;
+        if (j >= n) break;
+        uint4 w;
+        if (j == 0) w = aadw;
+        else if (j <= M) w = mask_block(lds16(base + (j - 1) * 16), (j - 1) * 16, p.aead_len);
+        else w = make_uint4(p.aad_len, 0, p.aead_len, 0);
+        const P5 x = p_block(w);
+        Y = k ? p_add(p_mul(Y, r64), x) : x;
+    }
+    const uint32_t kq = (uint32_t) lane < n ? (n - 1 - (uint32_t) lane) / 64 + 1 : 0;
+    if (kq) Y = p_mul(Y, p_rd(rpow + 5 * (n - ((uint32_t) lane + 64 * (kq - 1)) - 1)));
+    else Y = p_zero();
+    return p_sum_all(Y, lane);
+}
+
+template <bool DEC>
+__device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, uint8_t *tab, int lane)
+{
+    tlsrec_plan p;
+    make_plan<DEC, false>(p, J.d, J.km, J.st, J.rec - J.d.buf_off);
+    if (p.status != 0) {
+        tlsrec_batch_res r;
+        if (lane == 0) finish_early(p, J.d, J.rec - J.d.buf_off, &r);
+        r.status = __builtin_amdgcn_readfirstlane(r.status);
+        r.data_offset = __builtin_amdgcn_readfirstlane(r.data_offset);
+        r.data_len = __builtin_amdgcn_readfirstlane(r.data_len);
+        r.type = (uint8_t) __builtin_amdgcn_readfirstlane(r.type);
+        r.cid_len = (uint8_t) __builtin_amdgcn_readfirstlane(r.cid_len);
+        r.reserved[0] = r.reserved[1] = 0;
+        return r;
+    }
+    uint32_t nw[3], key[8];
+    nonce_words<DEC>(p, J.d, J.rec - J.d.buf_off, nw);
+#pragma unroll
+    for (int i = 0; i < 8; i++) key[i] = ld_u32le(J.km.key + 4 * i);
+    const uint32_t B = (p.aead_len + 63) >> 6;         /* ChaCha20 blocks of data; counters 0 .. B */
+    const uint32_t KC = (B + 1 + 63) >> 6;
+    const uint32_t content_len = DEC ? p.aead_len : p.content_len;
+    uint8_t *base = J.rec + p.aead_pos;
+
+    /* step 0's keystream: lane q makes block q, lane 0 the one-time key */
+    uint32_t ks0[16];
+    chacha_block(key, (uint32_t) lane, nw, ks0);
+    uint32_t r0[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) r0[i] = __builtin_amdgcn_readlane(ks0[i], 0);
+    /* r^1 .. r^64 in LDS by doubling: after level t lanes < 2^(t+1) hold theirs */
+    uint32_t *rpow = reinterpret_cast<uint32_t *>(tab);
+    P5 rq = p_from_r(r0[0], r0[1], r0[2], r0[3]);
+    if (lane == 0) p_wr(rpow, rq);
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        const int s = 1 << t;
+        if (lane >= s && lane < 2 * s) {
+            rq = p_mul(p_rd(rpow + 5 * (lane - s)), p_rd(rpow + 5 * (s - 1)));
+            p_wr(rpow + 5 * lane, rq);
+        }
+        asm volatile("" ::: "memory");
+    }
+    P5 h = p_zero();
+    if (DEC) h = srv_poly(base, p, rpow, lane);        /* over the ciphertext, before it is replaced */
+    uint32_t nzpos = 0;
+    for (uint32_t k = 0; k < KC; k++) {
+        const uint32_t c = (uint32_t) lane + 64 * k;
+        uint32_t ks[16];
+        if (k == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) ks[i] = ks0[i];
+        } else if (c <= B) {
+            chacha_block(key, c, nw, ks);
+        }
+        if (c >= 1 && c <= B) {
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint32_t pos = (c - 1) * 64 + 16 * t;
+                if (pos < p.aead_len) {
+                    const uint4 blk = srv_load_block(base, pos, content_len, p.aead_len, p.inner_type);
+                    const uint4 o = mask_block(
+                        xor4(blk, make_uint4(ks[4 * t], ks[4 * t + 1], ks[4 * t + 2], ks[4 * t + 3])), pos, p.aead_len);
+                    srv_store_block(base, pos, p.aead_len, o);
+                    if (DEC && p.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                }
+            }
+        }
+    }
+    if (!DEC) h = srv_poly(base, p, rpow, lane);
+    const uint4 s = make_uint4(r0[4], r0[5], r0[6], r0[7]);
+    const uint4 tag = p_finish(h, s);
+    uint32_t nzkey = 0;
+    if (DEC && p.inner && nzpos) nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
+    return srv_finish<DEC>(J, p, tag, nzkey, lane);
+}
+
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* One request: descriptor + record -> LDS, the AEAD, record + result back. */
+__device__ __forceinline__ void srv_serve(SrvReq *rq, uint32_t bytes, uint8_t *lds, uint8_t *wl, int lane)
+{
+    uint8_t *tab = wl, *stage = wl + SRV_TAB;
+    const uint8_t *gsrc = rq->buf;
+    const uint32_t n16 = bytes > SRV_BUF ? 0u : (bytes + 15) / 16;
+    /* one burst: descriptor chunks (lanes 0..5) and every 16-byte chunk of the record */
+    const uint4 dc = lane < 6 ? gload16(reinterpret_cast<const uint8_t *>(&rq->desc) + 16 * lane) : make_uint4(0, 0, 0, 0);
+    constexpr int NCH = (int) (SRV_BUF / 16 + 63) / 64;
+    uint4 r[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const uint32_t i = (uint32_t) lane + 64u * k;
+        if (i < n16) r[k] = gload16(gsrc + 16 * i);
+    }
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const uint32_t i = (uint32_t) lane + 64u * k;
+        if (i < n16) sts16(stage + 16 * i, r[k]);
+    }
+    uint32_t w[24];
+#pragma unroll
+    for (int i = 0; i < 24; i++) {
+        const uint32_t c = (i & 3) == 0 ? dc.x : ((i & 3) == 1 ? dc.y : ((i & 3) == 2 ? dc.z : dc.w));
+        w[i] = __builtin_amdgcn_readlane(c, i >> 2);
+    }
+    SrvDesc D;
+    __builtin_memcpy(&D, w, sizeof(D));
+    SrvJob J;
+    J.d = D.d;
+    J.st = reinterpret_cast<const SlotState *>(D.slot);
+    J.ghtab = reinterpret_cast<const uint4 *>(D.ghtab);
+    J.hpw = reinterpret_cast<const uint4 *>(D.hpw);
+    J.rec = stage + D.d.buf_off;
+    {
+        const uint4 kv = lane < 4 ? gload16(reinterpret_cast<const uint8_t *>(&J.st->km) + 16 * lane) : make_uint4(0, 0, 0, 0);
+        uint32_t kw[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t c = (i & 3) == 0 ? kv.x : ((i & 3) == 1 ? kv.y : ((i & 3) == 2 ? kv.z : kv.w));
+            kw[i] = __builtin_amdgcn_readlane(c, i >> 2);
+        }
+        __builtin_memcpy(&J.km, kw, sizeof(J.km));
+    }
+    tlsrec_batch_res res;
+    res.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
+    res.data_offset = res.data_len = 0;
+    res.type = res.cid_len = 0;
+    res.reserved[0] = res.reserved[1] = 0;
+    /* the host checked these; a request outside them is refused, not served */
+    const bool ok = n16 != 0 && (uint64_t) D.d.buf_off + D.d.buf_len + 32 <= SRV_BUF && D.d.cid_len == 0 &&
+                    J.km.cipher == D.cipher && J.km.reserved[0] == 0;
+    if (ok) {
+        const uint32_t c = D.cipher;
+        if (c == TLSREC_CIPHER_CHACHA20_POLY1305)
+            res = D.dec ? srv_chachapoly<true>(J, tab, lane) : srv_chachapoly<false>(J, tab, lane);
+        else if (D.nr == 10 && c == TLSREC_CIPHER_AES_128_GCM)
+            res = D.dec ? srv_gcm<10, true>(J, lds, tab, lane) : srv_gcm<10, false>(J, lds, tab, lane);
+        else if (D.nr == 14 && c == TLSREC_CIPHER_AES_256_GCM)
+            res = D.dec ? srv_gcm<14, true>(J, lds, tab, lane) : srv_gcm<14, false>(J, lds, tab, lane);
+        else if (D.nr == 12 && c == TLSREC_CIPHER_AES_192_GCM)
+            res = D.dec ? srv_gcm<12, true>(J, lds, tab, lane) : srv_gcm<12, false>(J, lds, tab, lane);
+    }
+    /* the record (whole staged range) and the result back to the slot */
+    if (ok)
+        for (uint32_t i = (uint32_t) lane; i < n16; i += 64) gstore16(rq->buf + 16 * i, lds16(stage + 16 * i));
+    if (lane == 0) {
+        uint4 rv;
+        __builtin_memcpy(&rv, &res, sizeof(rv));
+        gstore16(reinterpret_cast<uint8_t *>(&rq->res), rv);
+    }
+}
+
+} /* namespace */
+
+/* The resident grid: wave w of workgroup b owns request slot b * SRV_WAVES + w. */
+__global__ __launch_bounds__(SRV_WAVES * 64) void tlsrec_server_kernel(SrvReq *reqs, const uint32_t *stop,
+                                                                       uint64_t life_ticks, uint32_t max_iter)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SRV_LDS];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    aes_fill_tables(lds, tid, SRV_WAVES * 64);
+    __syncthreads();
+    SrvReq *rq = reqs + blockIdx.x * SRV_WAVES + wave;
+    uint8_t *wl = lds + 65536 + wave * SRV_WAVE_LDS;
+    const uint64_t t0 = wall_clock64();
+    uint32_t served = __builtin_amdgcn_readfirstlane(ld_sys32(&rq->done));
+    for (uint32_t it = 0; it < max_iter; it++) {
+        const uint64_t h = __hip_atomic_load(&rq->hdr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t) h);
+        if (seq != served) {
+            srv_serve(rq, __builtin_amdgcn_readfirstlane((uint32_t) (h >> 32)), lds, wl, lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");    /* every lane's record stores, system scope */
+            if (lane == 0) __hip_atomic_store(&rq->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            served = seq;
+            continue;
+        }
+        if ((it & 15) == 0 && __builtin_amdgcn_readfirstlane(ld_sys32(stop)) != 0) break;
+        if ((uint64_t) (wall_clock64() - t0) > life_ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+/* H^1 .. H^64 of one GCM key slot, from its 4-bit tables H^(2^b): lane q
+ * multiplies the identity by H^(2^b) for the set bits b of q + 1. */
+__global__ __launch_bounds__(64) void tlsrec_srv_hpow_kernel(const uint4 *ghtab, uint4 *out)
+{
+    const uint8_t *g = reinterpret_cast<const uint8_t *>(ghtab);
+    const uint32_t e = threadIdx.x + 1;
+    uint4 x = make_uint4(0x80u, 0, 0, 0);                /* 1: the GCM string 80 00 .. 00 */
+    if (e & 1) x = gmul<0>(g, x);
+    if (e & 2) x = gmul<1>(g, x);
+    if (e & 4) x = gmul<2>(g, x);
+    if (e & 8) x = gmul<3>(g, x);
+    if (e & 16) x = gmul<4>(g, x);
+    if (e & 32) x = gmul<5>(g, x);
+    if (e & 64) x = gmul<6>(g, x);
+    out[threadIdx.x] = x;
+}
+
+/* ======================================================================
+ * Host side
+ * ==================================================================== */
+namespace {
+
+struct SrvSet {
+    SrvReq *h = nullptr, *d = nullptr;
+    uint32_t *stop_h = nullptr, *stop_d = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;
+    bool launched = false;
+    uint64_t t_launch = 0;
+    uint32_t seq[SRV_SLOTS] = {};
+    uint8_t busy[SRV_SLOTS] = {};
+    uint32_t nbusy = 0;
+};
+
+pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+SrvSet g_set[2];
+int g_cur = 0;
+int g_state = 0;                  /* 0 not yet set up, 1 ready, -1 unavailable */
+std::atomic<int> g_enabled{1};
+uint64_t g_submit_ns = 0, g_life_ticks = 0;
+uint32_t g_max_iter = 0;
+std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
+
+uint64_t now_ns()
+{
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t) t.tv_sec * 1000000000ull + (uint64_t) t.tv_nsec;
+}
+
+void srv_shutdown()
+{
+    pthread_mutex_lock(&g_mu);
+    for (auto &S : g_set)
+        if (S.launched) {
+            __atomic_store_n(S.stop_h, 1u, __ATOMIC_RELEASE);
+            (void) hipEventSynchronize(S.ev);
+            S.launched = false;
+        }
+    pthread_mutex_unlock(&g_mu);
+}
+
+int srv_setup_locked()
+{
+    if (g_state) return g_state;
+    g_state = -1;
+    const char *e = getenv("TLSREC_SERVER");
+    if (e && strcmp(e, "0") == 0) return g_state;
+    double ms = 20.0;
+    if (const char *m = getenv("TLSREC_SERVER_MS")) ms = atof(m);
+    if (!(ms >= 1.0)) ms = 1.0;
+    if (ms > 200.0) ms = 200.0;
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+        return g_state;
+    g_life_ticks = (uint64_t) (ms * khz);
+    g_max_iter = (uint32_t) (ms * 10000.0);          /* backstop: a poll (a PCIe read + s_sleep) is > 0.1 us */
+    const double margin = ms * 0.1 > 1.0 ? ms * 0.1 : 1.0;
+    g_submit_ns = (uint64_t) ((ms - margin) * 1e6);
+    for (auto &S : g_set) {
+        void *hd = nullptr, *sd = nullptr;
+        if (hipHostMalloc((void **) &S.h, sizeof(SrvReq) * SRV_SLOTS, hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess ||
+            hipHostGetDevicePointer(&hd, S.h, 0) != hipSuccess ||
+            hipHostMalloc((void **) &S.stop_h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(&sd, S.stop_h, 0) != hipSuccess ||
+            hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
+            return g_state;
+        memset(S.h, 0, sizeof(SrvReq) * SRV_SLOTS);
+        memset(S.stop_h, 0, 64);
+        S.d = (SrvReq *) hd;
+        S.stop_d = (uint32_t *) sd;
+    }
+    atexit(srv_shutdown);
+    g_state = 1;
+    return g_state;
+}
+
+bool kernel_done(SrvSet &S) { return !S.launched || hipEventQuery(S.ev) != hipErrorNotReady; }
+
+/* Under g_mu: the set to submit to, launching the next grid when the current
+ * one's window has closed; NULL = not now (the caller takes the launch path). */
+SrvSet *srv_current_locked(uint64_t now)
+{
+    SrvSet *S = &g_set[g_cur];
+    if (S->launched && now - S->t_launch < g_submit_ns) return S;
+    SrvSet *N = &g_set[g_cur ^ 1];
+    /* the other set must be drained: its grid ended, no host thread in it */
+    if (N->nbusy != 0 || !kernel_done(*N)) return nullptr;
+    __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d,
+                       (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(N->ev, N->st) != hipSuccess) {
+        g_state = -1;
+        return nullptr;
+    }
+    N->launched = true;
+    N->t_launch = now;
+    g_cur ^= 1;
+    g_launches++;
+    return N;
+}
+
+} /* namespace */
+
+extern "C" hipError_t tlsrec__launch_srv_hpow(const uint4 *ghtab_slot, uint4 *out, hipStream_t st)
+{
+    hipLaunchKernelGGL(tlsrec_srv_hpow_kernel, dim3(1), dim3(64), 0, st, ghtab_slot, out);
+    return hipGetLastError();
+}
+
+/* Serve one record.  Returns 0 with *out and buf filled in, 1 when the server
+ * did not take the request (the caller runs the launch path), or an error. */
+extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const tlsrec_batch_rec *rec,
+                                  const void *slot_state, const void *ghtab, const void *hpw, unsigned char *buf,
+                                  size_t buf_len, uint32_t aead_pos, tlsrec_batch_res *out)
+{
+    if (!g_enabled.load(std::memory_order_relaxed) || g_state < 0) return 1;
+    const uint32_t pre = (16u - (aead_pos & 15u)) & 15u;
+    if ((uint64_t) pre + buf_len + 32 > SRV_BUF) return 1;
+    pthread_mutex_lock(&g_mu);
+    if (srv_setup_locked() != 1) {
+        pthread_mutex_unlock(&g_mu);
+        return 1;
+    }
+    SrvSet *S = srv_current_locked(now_ns());
+    int i = -1;
+    if (S)
+        for (int k = 0; k < SRV_SLOTS; k++)
+            if (!S->busy[k]) { i = k; break; }
+    if (i < 0) {
+        pthread_mutex_unlock(&g_mu);
+        g_fallback++;
+        return 1;
+    }
+    S->busy[i] = 1;
+    S->nbusy++;
+    const uint32_t seq = ++S->seq[i];
+    pthread_mutex_unlock(&g_mu);
+
+    SrvReq *rq = &S->h[i];
+    if (buf_len) memcpy(rq->buf + pre, buf, buf_len);
+    SrvDesc &D = rq->desc;
+    D.d = *rec;
+    D.d.buf_off = pre;
+    D.d.slot = 0;
+    D.dec = (uint32_t) dec;
+    D.cipher = cipher;
+    D.nr = nr;
+    D.pad = 0;
+    D.slot = (uint64_t) (uintptr_t) slot_state;
+    D.ghtab = (uint64_t) (uintptr_t) ghtab;
+    D.hpw = (uint64_t) (uintptr_t) hpw;
+    const uint32_t bytes = (pre + (uint32_t) buf_len + 15u) & ~15u;
+    __atomic_store_n(&rq->hdr, ((uint64_t) bytes << 32) | seq, __ATOMIC_RELEASE);
+
+    int rc = 0;
+    for (uint32_t spins = 1;; spins++) {
+        if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
+        __builtin_ia32_pause();
+        if ((spins & 4095) == 0 && hipEventQuery(S->ev) != hipErrorNotReady) {
+            /* the grid has ended: served just before, or never taken */
+            if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
+            __atomic_store_n(&rq->done, seq, __ATOMIC_RELEASE);   /* withdraw: no later grid serves it */
+            rc = 1;
+            break;
+        }
+    }
+    if (rc == 0) {
+        *out = rq->res;
+        if (buf_len) memcpy(buf, rq->buf + pre, buf_len);
+        g_served++;
+    } else {
+        g_fallback++;
+    }
+    pthread_mutex_lock(&g_mu);
+    S->busy[i] = 0;
+    S->nbusy--;
+    pthread_mutex_unlock(&g_mu);
+    return rc;
+}
+
+/* tests: route single-record calls through the server (1) or never (0) */
+extern "C" void tlsrec__server_enable(int on) { g_enabled.store(on ? 1 : 0); }
+
+extern "C" void tlsrec__server_stats(uint64_t *served, uint64_t *fallback, uint64_t *launches)
+{
+    if (served) *served = g_served.load();
+    if (fallback) *fallback = g_fallback.load();
+    if (launches) *launches = g_launches.load();
+}

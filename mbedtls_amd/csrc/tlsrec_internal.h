@@ -159,6 +159,8 @@ hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_
  * tlsrec__scan_scratch_bytes(n) bytes, in and out may not alias */
 size_t tlsrec__scan_scratch_bytes(uint32_t n);
 hipError_t tlsrec__exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *scratch, hipStream_t st);
+/* server.hip: H^1 .. H^64 of one GCM key slot (64 uint4), from its GHASH tables */
+hipError_t tlsrec__launch_srv_hpow(const uint4 *ghtab_slot, uint4 *out, hipStream_t st);
 /* every result of a batch to INTERNAL_ERROR before its AEAD kernels (fail closed, kernels.hip) */
 hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st);
 }

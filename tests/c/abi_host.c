@@ -138,6 +138,20 @@ static int cmp_d(const void *a, const void *b)
     return (x > y) - (x < y);
 }
 
+/* libtlsrec internal: how many coalesced batches carried how many records,
+ * and the record server's requests (served, sent back to the launch path) and
+ * grid launches */
+void tlsrec__engine_stats(uint64_t *batches, uint64_t *records);
+void tlsrec__server_stats(uint64_t *served, uint64_t *fallback, uint64_t *launches);
+
+static void print_server_stats(void)
+{
+    uint64_t s = 0, f = 0, l = 0;
+    tlsrec__server_stats(&s, &f, &l);
+    printf(", \"server_served\": %llu, \"server_fallback\": %llu, \"server_launches\": %llu}\n",
+           (unsigned long long) s, (unsigned long long) f, (unsigned long long) l);
+}
+
 static int latency(char **a)
 {
     const int cipher = atoi(a[0]);
@@ -190,8 +204,9 @@ static int latency(char **a)
     const int i50 = iters / 2, i99 = (int) ((iters - 1) * 0.99);
     printf("{\"latency_us\": {\"cipher\": %d, \"tls\": \"%s\", \"content\": %zu, \"iters\": %d, "
            "\"encrypt_p50\": %.1f, \"encrypt_p99\": %.1f, \"encrypt_mean\": %.1f, "
-           "\"decrypt_p50\": %.1f, \"decrypt_p99\": %.1f, \"decrypt_mean\": %.1f}, \"bad\": %d}\n",
+           "\"decrypt_p50\": %.1f, \"decrypt_p99\": %.1f, \"decrypt_mean\": %.1f}, \"bad\": %d",
            cipher, a[1], content, iters, te[i50], te[i99], me / iters, td[i50], td[i99], md / iters, bad);
+    print_server_stats();
     tlsrec_transform_free(&t);
     free(buf);
     free(plain);
@@ -200,13 +215,15 @@ static int latency(char **a)
     return bad ? 1 : 0;
 }
 
-typedef struct { int id, records, bad; double us; pthread_barrier_t *go; } thr_job;
+typedef struct { int id, records, bad, mix; double us; pthread_barrier_t *go; } thr_job;
 
 static void *thr_main(void *arg)
 {
     thr_job *j = (thr_job *) arg;
+    /* mix: AES-256-GCM, ChaCha20-Poly1305 and AES-128-CCM threads (CCM runs on
+     * the launch path); otherwise the north star's two AEADs */
     const int ciphers[3] = { TLSREC_CIPHER_AES_256_GCM, TLSREC_CIPHER_CHACHA20_POLY1305, TLSREC_CIPHER_AES_128_CCM };
-    const int cipher = ciphers[j->id % 3];
+    const int cipher = ciphers[j->id % (j->mix ? 3 : 2)];
     unsigned char key[32], iv[16];
     for (int i = 0; i < 32; i++) key[i] = (unsigned char) (i + j->id * 17);
     for (int i = 0; i < 16; i++) iv[i] = (unsigned char) (i * 3 + j->id);
@@ -243,10 +260,7 @@ static void *thr_main(void *arg)
     return NULL;
 }
 
-/* libtlsrec internal: how many coalesced batches carried how many records */
-void tlsrec__engine_stats(uint64_t *batches, uint64_t *records);
-
-static int threads(char **a)
+static int threads(char **a, int mix)
 {
     const int nt = atoi(a[0]), records = atoi(a[1]);
     pthread_t tid[64];
@@ -255,7 +269,7 @@ static int threads(char **a)
     pthread_barrier_t go;
     pthread_barrier_init(&go, NULL, (unsigned) nt);
     for (int i = 0; i < nt; i++) {
-        jobs[i] = (thr_job) { i, records, 0, 0, &go };
+        jobs[i] = (thr_job) { i, records, 0, mix, 0, &go };
         pthread_create(&tid[i], NULL, thr_main, &jobs[i]);
     }
     int bad = 0;
@@ -268,9 +282,11 @@ static int threads(char **a)
     pthread_barrier_destroy(&go);
     uint64_t nb = 0, nr = 0;
     tlsrec__engine_stats(&nb, &nr);
-    printf("{\"threads\": %d, \"records_per_thread\": %d, \"round_trips_per_s\": %.0f, \"bad\": %d, "
-           "\"engine_batches\": %llu, \"engine_records\": %llu, \"records_per_batch\": %.2f}\n", nt, records,
-           1e6 * nt * records / us, bad, (unsigned long long) nb, (unsigned long long) nr, nb ? (double) nr / nb : 0.0);
+    printf("{\"threads\": %d, \"ciphers\": \"%s\", \"records_per_thread\": %d, \"round_trips_per_s\": %.0f, "
+           "\"bad\": %d, \"engine_batches\": %llu, \"engine_records\": %llu, \"records_per_batch\": %.2f",
+           nt, mix ? "gcm+chacha+ccm" : "gcm+chacha", records, 1e6 * nt * records / us, bad, (unsigned long long) nb,
+           (unsigned long long) nr, nb ? (double) nr / nb : 0.0);
+    print_server_stats();
     return bad ? 1 : 0;
 }
 
@@ -283,8 +299,9 @@ int main(int argc, char **argv)
     }
     if (argc == 10 && strcmp(argv[1], "kat") == 0) return kat(argv + 2);
     if (argc == 6 && strcmp(argv[1], "latency") == 0) return latency(argv + 2);
-    if (argc == 4 && strcmp(argv[1], "threads") == 0) return threads(argv + 2);
+    if (argc == 4 && strcmp(argv[1], "threads") == 0) return threads(argv + 2, 1);
+    if (argc == 5 && strcmp(argv[1], "threads") == 0) return threads(argv + 2, strcmp(argv[4], "mix") == 0);
     fprintf(stderr, "usage: abi_host layout | kat ... | latency <cipher> <1.2|1.3> <content> <iters> | "
-                    "threads <n> <records>\n");
+                    "threads <n> <records> [mix|gcm_chacha]\n");
     return 2;
 }

@@ -31,9 +31,23 @@ def _stats():
     return b.value, r.value
 
 
-def test_concurrent_calls_are_coalesced_and_exact():
+def _server_stats():
+    f = _abi.load().tlsrec__server_stats
+    f.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 3
+    s, fb, ln = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    f(ctypes.byref(s), ctypes.byref(fb), ctypes.byref(ln))
+    return s.value
+
+
+@pytest.mark.parametrize("server", [True, False], ids=["server", "launch_path"])
+def test_concurrent_calls_are_coalesced_and_exact(server):
+    """AES-GCM / ChaCha20-Poly1305 calls go to the record server (server.hip)
+    when it is on; the coalescing launch path carries the rest, and all of
+    them when it is off"""
+    _abi.load().tlsrec__server_enable(1 if server else 0)
     nthreads, per = 16, 40
     b0, r0 = _stats()
+    s0 = _server_stats()
     errors = []
 
     def worker(tid):
@@ -73,8 +87,11 @@ def test_concurrent_calls_are_coalesced_and_exact():
         th.start()
     for th in ths:
         th.join(timeout=300)
+    _abi.load().tlsrec__server_enable(1)
     assert not errors, errors[:5]
     b1, r1 = _stats()
     batches, records = b1 - b0, r1 - r0
-    assert records == 2 * nthreads * per
+    served = _server_stats() - s0
+    assert records + served == 2 * nthreads * per
     assert batches < records, "no call was coalesced with another"
+    assert (served > 0) == server
