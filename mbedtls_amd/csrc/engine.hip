@@ -1188,16 +1188,16 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
 /* server.hip: the resident record server (AES-GCM, ChaCha20-Poly1305) */
 extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const tlsrec_batch_rec *rec,
                                   const void *slot_state, const void *ghtab, const void *hpw, unsigned char *buf,
-                                  size_t buf_len, uint32_t aead_pos, tlsrec_batch_res *out);
+                                  size_t buf_len, const void *plan, tlsrec_batch_res *out);
 
 /* Run one record through the kernels: host buffer -> device -> host.  A
  * decrypted record's CID (cid_len bytes) is staged right after the buffer.
  * AES-GCM and ChaCha20-Poly1305 records of transforms without connection IDs
- * go to the record server first (aead_pos: the plan's AEAD offset, which the
- * server's staging aligns to 16 bytes); the coalescing launch path below takes
+ * go to the record server first (plan: the record's framing plan, as the
+ * host entry points computed it); the coalescing launch path below takes
  * every other record, and any the server does not take. */
 extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
-                                  const unsigned char *cid, uint32_t aead_pos, tlsrec_batch_res *out)
+                                  const unsigned char *cid, const void *plan, tlsrec_batch_res *out)
 {
     if (!g_ready) {
         pthread_mutex_lock(&g_mu);
@@ -1218,7 +1218,7 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
         const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, kt->d_slots + idx,
                                          kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS,
                                          g_pages[rec->slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) idx * 64, buf,
-                                         buf_len, aead_pos, out);
+                                         buf_len, plan, out);
         if (r <= 0) return r;
     }
     Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co[engine_queue(cipher, dec)];

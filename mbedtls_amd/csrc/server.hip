@@ -48,6 +48,7 @@
 #include <atomic>
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -73,30 +74,41 @@ constexpr int SRV_LDS = 65536 + SRV_WAVES * SRV_WAVE_LDS;
 static_assert(SRV_LDS <= 160 * 1024, "server LDS budget");
 static_assert(SRV_WAVE_LDS % 16 == 0, "16-byte aligned staging");
 
-/* Request descriptor, 96 bytes (read by lanes 0..5 as 16-byte chunks). */
+/* Request descriptor (lanes 0..8 read it as 16-byte chunks): the record's
+ * batch descriptor and the framing plan the host computed for it with the
+ * same code (tlsrec_frame.h; the explicit nonce of a TLS 1.2 GCM record
+ * filled in from the record), so the device goes straight to the AEAD. */
 struct SrvDesc {
     tlsrec_batch_rec d;       /* buf_off = alignment prefix, slot unused */
-    uint32_t dec, cipher, nr, pad;
-    uint64_t slot;            /* const SlotState * (device) */
-    uint64_t ghtab;           /* const uint4 *: the slot's GHASH tables (GCM) */
-    uint64_t hpw;             /* const uint4 *: H^1 .. H^64 (GCM) */
-    uint64_t pad2[2];
+    uint32_t pad[4];
+    tlsrec_plan p;
+    uint8_t pad2[144 - 56 - sizeof(tlsrec_plan)];
 };
-static_assert(sizeof(SrvDesc) == 96, "SrvDesc layout");
+static_assert(sizeof(SrvDesc) == 144, "SrvDesc layout");
+
+/* What one poll reads (four 8-byte loads in flight together):
+ *   w[0] = seq | staged bytes << 32 | cipher << 48 | dec << 56 | nr << 57
+ *   w[1] = the slot's SlotState, w[2] its GHASH tables, w[3] its H^1 .. H^64
+ *          (device addresses < 2^48), each | (seq & 0xffff) << 48
+ * The host writes w[1..3] before w[0] (release); a poll that sees a new seq
+ * in w[0] but an older one in w[1..3] read a request half-posted and polls
+ * again.  So the wave knows the key slot at once and its key loads go out
+ * with the record's. */
+constexpr uint64_t SRV_PTR_MASK = (1ull << 48) - 1;
 
 /* One request slot in pinned host memory mapped into the device. */
 struct SrvReq {
-    uint64_t hdr;             /* seq (low 32) | staged bytes (high 32): one store posts the request */
-    uint8_t pad0[56];
+    uint64_t w[4];
+    uint8_t pad0[32];
     uint32_t done;            /* seq of the last request served (device writes) */
     uint8_t pad1[60];
     SrvDesc desc;
     tlsrec_batch_res res;
-    uint8_t pad2[16];
+    uint8_t pad2[32];
     uint8_t buf[SRV_BUF];
 };
-static_assert(offsetof(SrvReq, done) == 64 && offsetof(SrvReq, desc) == 128 && offsetof(SrvReq, res) == 224 &&
-                  offsetof(SrvReq, buf) == 256 && sizeof(SrvReq) % 64 == 0,
+static_assert(offsetof(SrvReq, done) == 64 && offsetof(SrvReq, desc) == 128 && offsetof(SrvReq, res) == 272 &&
+                  offsetof(SrvReq, buf) == 320 && sizeof(SrvReq) % 64 == 0,
               "SrvReq layout");
 
 /* ---------------- LDS record access (16-byte aligned AEAD region) -------- */
@@ -154,37 +166,28 @@ __device__ __forceinline__ uint4 srv_gfmul(uint4 x, uint4 y)
     return make_uint4(r[0], r[1], r[2], r[3]);
 }
 
-/* Everything a served record needs, uniform over the wave. */
+/* Everything a served record needs, uniform over the wave (the AEAD's own
+ * per-lane inputs -- H^64 table, closing power, round keys -- are passed
+ * beside it). */
 struct SrvJob {
     tlsrec_batch_rec d;
-    const SlotState *st;
-    const uint4 *ghtab;
-    const uint4 *hpw;
-    tlsrec_key_material km;
+    tlsrec_plan p;
     uint8_t *rec;             /* the record's first byte in LDS (staging + d.buf_off) */
 };
-
-/* Result of a record whose plan stopped before the AEAD, or a finished one */
-__device__ __forceinline__ tlsrec_batch_res mk_res(int32_t status, const tlsrec_plan &p, uint8_t type, uint8_t cid_len)
-{
-    tlsrec_batch_res r;
-    r.status = status;
-    r.data_offset = p.data_offset;
-    r.data_len = p.data_len;
-    r.type = type;
-    r.cid_len = cid_len;
-    r.reserved[0] = r.reserved[1] = 0;
-    return r;
-}
 
 /* Tag handling shared by both AEADs: encrypt writes the tag and the explicit
  * nonce, decrypt compares, wipes on a mismatch (PSA zeroes the output) and
  * takes the TLS 1.3 inner type / length from the last non-zero byte. */
 template <bool DEC>
-__device__ __forceinline__ tlsrec_batch_res srv_finish(const SrvJob &J, const tlsrec_plan &p, uint4 tag, uint32_t nzkey,
-                                                       int lane)
+__device__ __forceinline__ tlsrec_batch_res srv_finish(const SrvJob &J, uint4 tag, uint32_t nzkey, int lane)
 {
+    const tlsrec_plan &p = J.p;
     uint8_t *base = J.rec + p.aead_pos;
+    tlsrec_batch_res r;
+    r.data_offset = p.data_offset;
+    r.data_len = p.data_len;
+    r.cid_len = 0;
+    r.reserved[0] = r.reserved[1] = 0;
     if (!DEC) {
         if (lane < 16) base[p.aead_len + lane] = (uint8_t) byte_of(tag, (uint32_t) lane);
         if (p.explicit_iv && p.post_status == 0 && lane < 8) {
@@ -192,12 +195,16 @@ __device__ __forceinline__ tlsrec_batch_res srv_finish(const SrvJob &J, const tl
             __builtin_memcpy(c, J.d.ctr, 8);
             J.rec[p.data_offset + lane] = (uint8_t) (c[lane >> 2] >> (8 * (lane & 3)));
         }
-        return mk_res(p.post_status, p, p.type, p.cid_set ? p.cid_len : 0);
+        r.status = p.post_status;
+        r.type = p.type;
+        r.cid_len = p.cid_set ? p.cid_len : 0;
+        return r;
     }
     uint32_t diff = lane < 16 ? (base[p.aead_len + lane] ^ byte_of(tag, (uint32_t) lane)) : 0u;
     diff = group_or<64>(diff);
     const uint32_t key = group_max<64>(nzkey);
-    tlsrec_batch_res r = mk_res(0, p, J.d.type, 0);
+    r.status = 0;
+    r.type = J.d.type;
     if (diff != 0) {
         for (uint32_t i = p.aead_pos + (uint32_t) lane; i < J.d.buf_len; i += 64) J.rec[i] = 0;
         r.status = TLSREC_E_INVALID_MAC;
@@ -212,75 +219,66 @@ __device__ __forceinline__ tlsrec_batch_res srv_finish(const SrvJob &J, const tl
     return r;
 }
 
-/* ---------------- AES-GCM, one record per wave ---------------------------- */
-template <int NR, bool DEC>
-__device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8_t *lds, uint8_t *tab, int lane)
+__device__ __forceinline__ void nonce_of(const tlsrec_plan &p, uint32_t nw[3])
 {
-    tlsrec_plan p;
-    make_plan<DEC, false>(p, J.d, J.km, J.st, J.rec - J.d.buf_off);
-    if (p.status != 0) {
-        tlsrec_batch_res r;
-        if (lane == 0) finish_early(p, J.d, J.rec - J.d.buf_off, &r);
-        r.status = __builtin_amdgcn_readfirstlane(r.status);
-        r.data_offset = __builtin_amdgcn_readfirstlane(r.data_offset);
-        r.data_len = __builtin_amdgcn_readfirstlane(r.data_len);
-        r.type = (uint8_t) __builtin_amdgcn_readfirstlane(r.type);
-        r.cid_len = (uint8_t) __builtin_amdgcn_readfirstlane(r.cid_len);
-        r.reserved[0] = r.reserved[1] = 0;
-        return r;
-    }
+    nw[0] = ld_u32le(p.nonce);
+    nw[1] = ld_u32le(p.nonce + 4);
+    nw[2] = ld_u32le(p.nonce + 8);
+}
+
+/* ---------------- AES-GCM, one record per wave ---------------------------- */
+/* tab: the key's H^64 table in LDS (the Horner multiplier); hd: this lane's
+ * closing power H^(n - j_last); rk: the round keys (rotated form). */
+template <int NR, bool DEC>
+__device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8_t *lds, const uint8_t *tab, uint4 hd,
+                                                    const uint32_t *rk, int lane)
+{
+    const tlsrec_plan &p = J.p;
     const int q = lane;
     uint32_t nw[3];
-    nonce_words<DEC>(p, J.d, J.rec - J.d.buf_off, nw);
+    nonce_of(p, nw);
     const uint32_t m = (p.aead_len + 15) >> 4;         /* C blocks */
     const uint32_t n = m + 2;                          /* A, C_1 .. C_m, LEN */
     const uint32_t K = (n + 63) >> 6;
     const uint32_t content_len = DEC ? p.aead_len : p.content_len;
     uint8_t *base = J.rec + p.aead_pos;
-
-    /* the key's H^64 table to LDS (the Horner multiplier), and this lane's
-     * closing power H^(n - j_last) */
     const uint32_t kq = (uint32_t) q < n ? (n - 1 - (uint32_t) q) / 64 + 1 : 0;
-    const uint32_t dq = kq ? n - ((uint32_t) q + 64 * (kq - 1)) : 1;
-    const uint4 hd = J.hpw[dq - 1];
-    if (K > 1) {
-        const uint4 *src = J.ghtab + 6 * 512;
-#pragma unroll
-        for (int i = 0; i < 8; i++) sts16(tab + 16 * (lane + 64 * i), src[lane + 64 * i]);
-    }
-    /* round keys as uniform values (vector loads: the slot may be reloaded
-     * while the server runs, so nothing of it may sit in a scalar cache) */
-    uint32_t rk[60];
-    {
-        const uint32_t v = lane < 4 * (NR + 1) ? J.st->rkr[lane] : 0u;
-#pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = __builtin_amdgcn_readlane(v, i);
-    }
     const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
     const uint4 aadw = aad_words(p);
     const uint4 lenw = make_uint4(0, bswap32((uint32_t) p.aad_len * 8), 0, bswap32(p.aead_len * 8));
     uint4 Y = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
     uint32_t nzpos = 0;
-    for (uint32_t k = 0; k < K; k++) {
+    auto block = [&](uint32_t k, uint4 ks) {
         const uint32_t j = (uint32_t) q + 64 * k;
         uint4 X = make_uint4(0, 0, 0, 0);
-        if (j <= m) {
-            const uint4 ks = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
-            if (j == 0) {
-                ej0 = ks;
-                X = aadw;
-            } else {
-                const uint32_t pos = (j - 1) * 16;
-                const uint4 blk = srv_load_block(base, pos, content_len, p.aead_len, p.inner_type);
-                const uint4 o = mask_block(xor4(blk, ks), pos, p.aead_len);
-                srv_store_block(base, pos, p.aead_len, o);
-                X = DEC ? blk : o;
-                if (DEC && p.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
-            }
+        if (j == 0) {
+            ej0 = ks;
+            X = aadw;
+        } else if (j <= m) {
+            const uint32_t pos = (j - 1) * 16;
+            const uint4 blk = srv_load_block(base, pos, content_len, p.aead_len, p.inner_type);
+            const uint4 o = mask_block(xor4(blk, ks), pos, p.aead_len);
+            srv_store_block(base, pos, p.aead_len, o);
+            X = DEC ? blk : o;
+            if (DEC && p.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
         } else if (j == m + 1) {
             X = lenw;
         }
         if (j < n) Y = k ? xor4(gmul<0>(tab, Y), X) : X;
+    };
+    /* two steps' counter blocks at a time: independent AES chains interleave
+     * (a lane's AES is a dependent LDS round trip per round) */
+    uint32_t k = 0;
+    for (; k + 1 < K; k += 2) {
+        const uint32_t j = (uint32_t) q + 64 * k;
+        const uint4 ks0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
+        const uint4 ks1 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 65)));
+        block(k, ks0);
+        block(k + 1, ks1);
+    }
+    if (k < K) {
+        const uint32_t j = (uint32_t) q + 64 * k;
+        block(k, aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1))));
     }
     if (kq) Y = srv_gfmul(Y, hd);
     const uint4 S = xor_all(Y);
@@ -288,8 +286,9 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
                                 __builtin_amdgcn_readlane(ej0.z, 0), __builtin_amdgcn_readlane(ej0.w, 0));
     const uint4 tag = xor4(S, e0);
     uint32_t nzkey = 0;
-    if (DEC && p.inner && nzpos) nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
-    return srv_finish<DEC>(J, p, tag, nzkey, lane);
+    if (DEC && p.inner && nzpos)
+        nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
+    return srv_finish<DEC>(J, tag, nzkey, lane);
 }
 
 /* ---------------- ChaCha20-Poly1305, one record per wave ------------------- */
@@ -342,25 +341,11 @@ __device__ __forceinline__ P5 srv_poly(const uint8_t *base, const tlsrec_plan &p
 }
 
 template <bool DEC>
-__device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, uint8_t *tab, int lane)
+__device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, const uint32_t *key, uint8_t *tab, int lane)
 {
-    tlsrec_plan p;
-    make_plan<DEC, false>(p, J.d, J.km, J.st, J.rec - J.d.buf_off);
-    if (p.status != 0) {
-        tlsrec_batch_res r;
-        if (lane == 0) finish_early(p, J.d, J.rec - J.d.buf_off, &r);
-        r.status = __builtin_amdgcn_readfirstlane(r.status);
-        r.data_offset = __builtin_amdgcn_readfirstlane(r.data_offset);
-        r.data_len = __builtin_amdgcn_readfirstlane(r.data_len);
-        r.type = (uint8_t) __builtin_amdgcn_readfirstlane(r.type);
-        r.cid_len = (uint8_t) __builtin_amdgcn_readfirstlane(r.cid_len);
-        r.reserved[0] = r.reserved[1] = 0;
-        return r;
-    }
-    uint32_t nw[3], key[8];
-    nonce_words<DEC>(p, J.d, J.rec - J.d.buf_off, nw);
-#pragma unroll
-    for (int i = 0; i < 8; i++) key[i] = ld_u32le(J.km.key + 4 * i);
+    const tlsrec_plan &p = J.p;
+    uint32_t nw[3];
+    nonce_of(p, nw);
     const uint32_t B = (p.aead_len + 63) >> 6;         /* ChaCha20 blocks of data; counters 0 .. B */
     const uint32_t KC = (B + 1 + 63) >> 6;
     const uint32_t content_len = DEC ? p.aead_len : p.content_len;
@@ -415,77 +400,104 @@ __device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, uint
     const uint4 s = make_uint4(r0[4], r0[5], r0[6], r0[7]);
     const uint4 tag = p_finish(h, s);
     uint32_t nzkey = 0;
-    if (DEC && p.inner && nzpos) nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
-    return srv_finish<DEC>(J, p, tag, nzkey, lane);
+    if (DEC && p.inner && nzpos)
+        nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
+    return srv_finish<DEC>(J, tag, nzkey, lane);
 }
 
-__device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p)
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-/* One request: descriptor + record -> LDS, the AEAD, record + result back. */
-__device__ __forceinline__ void srv_serve(SrvReq *rq, uint32_t bytes, uint8_t *lds, uint8_t *wl, int lane)
+__device__ __forceinline__ uint32_t comp(uint4 v, int i)
+{
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+/* One request: the record, its descriptor and the key slot's data in one
+ * burst of loads (record and descriptor over PCIe, key data from HBM), the
+ * AEAD in LDS, the record and result back to the slot. */
+__device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotState *st, const uint4 *ghtab,
+                                          const uint4 *hpw, const uint8_t *lds, uint8_t *wl, int lane)
 {
     uint8_t *tab = wl, *stage = wl + SRV_TAB;
-    const uint8_t *gsrc = rq->buf;
+    const uint32_t bytes = (uint32_t) (w0 >> 32) & 0xffffu;
+    const uint32_t cipher = (uint32_t) (w0 >> 48) & 0xffu;
+    const bool dec = (w0 >> 56) & 1u;
+    const uint32_t nr = (uint32_t) (w0 >> 57) & 0x1fu;
+    const bool gcm = cipher != TLSREC_CIPHER_CHACHA20_POLY1305;
     const uint32_t n16 = bytes > SRV_BUF ? 0u : (bytes + 15) / 16;
-    /* one burst: descriptor chunks (lanes 0..5) and every 16-byte chunk of the record */
-    const uint4 dc = lane < 6 ? gload16(reinterpret_cast<const uint8_t *>(&rq->desc) + 16 * lane) : make_uint4(0, 0, 0, 0);
+    /* descriptor chunks (lanes 0..8), slot chunks (lanes 0..3 the key
+     * material, 4..18 the rotated round keys at byte 304), the H^64 table and
+     * this lane's H^(lane+1) (GCM), every 16-byte chunk of the record */
+    const uint4 dc = lane < 9 ? gload16(reinterpret_cast<const uint8_t *>(&rq->desc) + 16 * lane) : make_uint4(0, 0, 0, 0);
+    const uint8_t *sp = reinterpret_cast<const uint8_t *>(st);
+    const uint4 sc = lane < 4 ? gload16(sp + 16 * lane)
+                     : (gcm && lane < 19) ? gload16(sp + offsetof(SlotState, rkr) + 16 * (lane - 4)) : make_uint4(0, 0, 0, 0);
+    uint4 hq = make_uint4(0, 0, 0, 0), ht[8];
+    if (gcm) {
+        hq = hpw[lane];
+#pragma unroll
+        for (int i = 0; i < 8; i++) ht[i] = ghtab[6 * 512 + lane + 64 * i];
+    }
     constexpr int NCH = (int) (SRV_BUF / 16 + 63) / 64;
     uint4 r[NCH];
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
         const uint32_t i = (uint32_t) lane + 64u * k;
-        if (i < n16) r[k] = gload16(gsrc + 16 * i);
+        if (i < n16) r[k] = gload16(rq->buf + 16 * i);
     }
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
         const uint32_t i = (uint32_t) lane + 64u * k;
         if (i < n16) sts16(stage + 16 * i, r[k]);
     }
-    uint32_t w[24];
+    if (gcm) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) {
-        const uint32_t c = (i & 3) == 0 ? dc.x : ((i & 3) == 1 ? dc.y : ((i & 3) == 2 ? dc.z : dc.w));
-        w[i] = __builtin_amdgcn_readlane(c, i >> 2);
+        for (int i = 0; i < 8; i++) sts16(tab + 16 * (lane + 64 * i), ht[i]);
     }
-    SrvDesc D;
-    __builtin_memcpy(&D, w, sizeof(D));
+    uint32_t w[36];
+#pragma unroll
+    for (int i = 0; i < 36; i++) w[i] = __builtin_amdgcn_readlane(comp(dc, i & 3), i >> 2);
     SrvJob J;
-    J.d = D.d;
-    J.st = reinterpret_cast<const SlotState *>(D.slot);
-    J.ghtab = reinterpret_cast<const uint4 *>(D.ghtab);
-    J.hpw = reinterpret_cast<const uint4 *>(D.hpw);
-    J.rec = stage + D.d.buf_off;
-    {
-        const uint4 kv = lane < 4 ? gload16(reinterpret_cast<const uint8_t *>(&J.st->km) + 16 * lane) : make_uint4(0, 0, 0, 0);
-        uint32_t kw[16];
+    __builtin_memcpy(&J.d, w, sizeof(J.d));
+    __builtin_memcpy(&J.p, w + 14, sizeof(J.p));
+    J.rec = stage + J.d.buf_off;
+    uint32_t kw[16];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const uint32_t c = (i & 3) == 0 ? kv.x : ((i & 3) == 1 ? kv.y : ((i & 3) == 2 ? kv.z : kv.w));
-            kw[i] = __builtin_amdgcn_readlane(c, i >> 2);
-        }
-        __builtin_memcpy(&J.km, kw, sizeof(J.km));
-    }
+    for (int i = 0; i < 16; i++) kw[i] = __builtin_amdgcn_readlane(comp(sc, i & 3), i >> 2);
+    const uint32_t km_cipher = kw[0] & 0xffu, km_cid = (kw[1] >> 8) & 0xffu;
     tlsrec_batch_res res;
     res.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
     res.data_offset = res.data_len = 0;
     res.type = res.cid_len = 0;
     res.reserved[0] = res.reserved[1] = 0;
     /* the host checked these; a request outside them is refused, not served */
-    const bool ok = n16 != 0 && (uint64_t) D.d.buf_off + D.d.buf_len + 32 <= SRV_BUF && D.d.cid_len == 0 &&
-                    J.km.cipher == D.cipher && J.km.reserved[0] == 0;
+    const bool ok = n16 != 0 && (uint64_t) J.d.buf_off + J.d.buf_len + 32 <= SRV_BUF && J.d.cid_len == 0 &&
+                    km_cipher == cipher && km_cid == 0 && J.p.status == 0 && J.p.cid_len == 0 &&
+                    (uint64_t) J.p.aead_pos + J.p.aead_len + 16 <= J.d.buf_len && ((J.d.buf_off + J.p.aead_pos) & 15) == 0;
     if (ok) {
-        const uint32_t c = D.cipher;
-        if (c == TLSREC_CIPHER_CHACHA20_POLY1305)
-            res = D.dec ? srv_chachapoly<true>(J, tab, lane) : srv_chachapoly<false>(J, tab, lane);
-        else if (D.nr == 10 && c == TLSREC_CIPHER_AES_128_GCM)
-            res = D.dec ? srv_gcm<10, true>(J, lds, tab, lane) : srv_gcm<10, false>(J, lds, tab, lane);
-        else if (D.nr == 14 && c == TLSREC_CIPHER_AES_256_GCM)
-            res = D.dec ? srv_gcm<14, true>(J, lds, tab, lane) : srv_gcm<14, false>(J, lds, tab, lane);
-        else if (D.nr == 12 && c == TLSREC_CIPHER_AES_192_GCM)
-            res = D.dec ? srv_gcm<12, true>(J, lds, tab, lane) : srv_gcm<12, false>(J, lds, tab, lane);
+        if (!gcm) {
+            const uint32_t *key = kw + 8;              /* tlsrec_key_material.key at byte 32 */
+            res = dec ? srv_chachapoly<true>(J, key, tab, lane) : srv_chachapoly<false>(J, key, tab, lane);
+        } else {
+            uint32_t rk[60];
+#pragma unroll
+            for (int i = 0; i < 60; i++) rk[i] = __builtin_amdgcn_readlane(comp(sc, i & 3), 4 + (i >> 2));
+            const tlsrec_plan &p = J.p;
+            const uint32_t n = ((p.aead_len + 15) >> 4) + 2;
+            const uint32_t kq = (uint32_t) lane < n ? (n - 1 - (uint32_t) lane) / 64 + 1 : 0;
+            const uint32_t dq = kq ? n - ((uint32_t) lane + 64 * (kq - 1)) : 1;   /* lane dq - 1 holds H^dq */
+            const uint4 hd = make_uint4(__shfl(hq.x, (int) dq - 1), __shfl(hq.y, (int) dq - 1),
+                                        __shfl(hq.z, (int) dq - 1), __shfl(hq.w, (int) dq - 1));
+            if (nr == 10 && cipher == TLSREC_CIPHER_AES_128_GCM)
+                res = dec ? srv_gcm<10, true>(J, lds, tab, hd, rk, lane) : srv_gcm<10, false>(J, lds, tab, hd, rk, lane);
+            else if (nr == 14 && cipher == TLSREC_CIPHER_AES_256_GCM)
+                res = dec ? srv_gcm<14, true>(J, lds, tab, hd, rk, lane) : srv_gcm<14, false>(J, lds, tab, hd, rk, lane);
+            else if (nr == 12 && cipher == TLSREC_CIPHER_AES_192_GCM)
+                res = dec ? srv_gcm<12, true>(J, lds, tab, hd, rk, lane) : srv_gcm<12, false>(J, lds, tab, hd, rk, lane);
+        }
     }
     /* the record (whole staged range) and the result back to the slot */
     if (ok)
@@ -510,20 +522,42 @@ __global__ __launch_bounds__(SRV_WAVES * 64) void tlsrec_server_kernel(SrvReq *r
     SrvReq *rq = reqs + blockIdx.x * SRV_WAVES + wave;
     uint8_t *wl = lds + 65536 + wave * SRV_WAVE_LDS;
     const uint64_t t0 = wall_clock64();
-    uint32_t served = __builtin_amdgcn_readfirstlane(ld_sys32(&rq->done));
+    uint32_t served = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&rq->done, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_SYSTEM));
+    uint32_t idle = 0;
     for (uint32_t it = 0; it < max_iter; it++) {
-        const uint64_t h = __hip_atomic_load(&rq->hdr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t) h);
+        const uint64_t h0 = ld_sys64(&rq->w[0]), h1 = ld_sys64(&rq->w[1]), h2 = ld_sys64(&rq->w[2]),
+                       h3 = ld_sys64(&rq->w[3]);
+        const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t) h0);
         if (seq != served) {
-            srv_serve(rq, __builtin_amdgcn_readfirstlane((uint32_t) (h >> 32)), lds, wl, lane);
+            const uint64_t tagw = (uint64_t) (seq & 0xffffu) << 48;
+            if (((h1 ^ tagw) | (h2 ^ tagw) | (h3 ^ tagw)) >> 48) continue;   /* half-posted: read again */
+            /* synchronizes with the host's release of w[0]: the record and
+             * descriptor it wrote before are visible to the loads below */
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            /* (readfirstlane returns int: widen through uint32_t, never sign-extend) */
+            auto uni = [](uint64_t h) {
+                return (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) h) |
+                       (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (h >> 32)) << 32;
+            };
+            const uint64_t a0 = uni(h0);
+            auto ptr = [&](uint64_t h) { return uni(h) & SRV_PTR_MASK; };
+            srv_serve(rq, a0, reinterpret_cast<const SlotState *>(ptr(h1)), reinterpret_cast<const uint4 *>(ptr(h2)),
+                      reinterpret_cast<const uint4 *>(ptr(h3)), lds, wl, lane);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");    /* every lane's record stores, system scope */
-            if (lane == 0) __hip_atomic_store(&rq->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) __hip_atomic_store(&rq->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             served = seq;
+            idle = 0;
             continue;
         }
-        if ((it & 15) == 0 && __builtin_amdgcn_readfirstlane(ld_sys32(stop)) != 0) break;
+        if ((it & 15) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(stop, __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_SYSTEM)) != 0)
+            break;
         if ((uint64_t) (wall_clock64() - t0) > life_ticks) break;
-        __builtin_amdgcn_s_sleep(8);
+        /* a slot idle for ~1 ms polls every few us instead of every ~2 us
+         * (the host hands out the lowest free slot, so busy slots stay hot) */
+        if (++idle > 512) __builtin_amdgcn_s_sleep(127);
+        else __builtin_amdgcn_s_sleep(8);
     }
 }
 
@@ -566,6 +600,7 @@ SrvSet g_set[2];
 int g_cur = 0;
 int g_state = 0;                  /* 0 not yet set up, 1 ready, -1 unavailable */
 std::atomic<int> g_enabled{1};
+int g_debug = 0;                  /* TLSREC_SERVER_DEBUG=1: one line per request on stderr */
 uint64_t g_submit_ns = 0, g_life_ticks = 0;
 uint32_t g_max_iter = 0;
 std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
@@ -583,7 +618,8 @@ void srv_shutdown()
     for (auto &S : g_set)
         if (S.launched) {
             __atomic_store_n(S.stop_h, 1u, __ATOMIC_RELEASE);
-            (void) hipEventSynchronize(S.ev);
+            const hipError_t e = hipEventSynchronize(S.ev);
+            if (g_debug) fprintf(stderr, "tlsrec server: shutdown, grid drained: %s\n", hipGetErrorString(e));
             S.launched = false;
         }
     pthread_mutex_unlock(&g_mu);
@@ -593,6 +629,7 @@ int srv_setup_locked()
 {
     if (g_state) return g_state;
     g_state = -1;
+    g_debug = getenv("TLSREC_SERVER_DEBUG") != nullptr;
     const char *e = getenv("TLSREC_SERVER");
     if (e && strcmp(e, "0") == 0) return g_state;
     double ms = 20.0;
@@ -639,9 +676,12 @@ SrvSet *srv_current_locked(uint64_t now)
     /* the other set must be drained: its grid ended, no host thread in it */
     if (N->nbusy != 0 || !kernel_done(*N)) return nullptr;
     __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
+    (void) hipGetLastError();         /* an earlier call's status (hipEventQuery's NotReady) is not the launch's */
     hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d,
                        (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter);
-    if (hipGetLastError() != hipSuccess || hipEventRecord(N->ev, N->st) != hipSuccess) {
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess || hipEventRecord(N->ev, N->st) != hipSuccess) {
+        if (g_debug) fprintf(stderr, "tlsrec server: launch failed: %s\n", hipGetErrorString(le));
         g_state = -1;
         return nullptr;
     }
@@ -660,14 +700,18 @@ extern "C" hipError_t tlsrec__launch_srv_hpow(const uint4 *ghtab_slot, uint4 *ou
     return hipGetLastError();
 }
 
-/* Serve one record.  Returns 0 with *out and buf filled in, 1 when the server
- * did not take the request (the caller runs the launch path), or an error. */
+/* Serve one record.  `plan` is the record's framing plan (tlsrec_frame.h, as
+ * tlsrec_encrypt_buf / _decrypt_buf computed it; status 0).  Returns 0 with
+ * *out and buf filled in, 1 when the server did not take the request (the
+ * caller runs the launch path), or an error. */
 extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const tlsrec_batch_rec *rec,
                                   const void *slot_state, const void *ghtab, const void *hpw, unsigned char *buf,
-                                  size_t buf_len, uint32_t aead_pos, tlsrec_batch_res *out)
+                                  size_t buf_len, const void *plan, tlsrec_batch_res *out)
 {
-    if (!g_enabled.load(std::memory_order_relaxed) || g_state < 0) return 1;
-    const uint32_t pre = (16u - (aead_pos & 15u)) & 15u;
+    if (!g_enabled.load(std::memory_order_relaxed) || g_state < 0 || plan == nullptr) return 1;
+    const tlsrec_plan *pl = (const tlsrec_plan *) plan;
+    if (pl->status != 0 || pl->cid_len != 0) return 1;
+    const uint32_t pre = (16u - (pl->aead_pos & 15u)) & 15u;
     if ((uint64_t) pre + buf_len + 32 > SRV_BUF) return 1;
     pthread_mutex_lock(&g_mu);
     if (srv_setup_locked() != 1) {
@@ -695,22 +739,30 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     D.d = *rec;
     D.d.buf_off = pre;
     D.d.slot = 0;
-    D.dec = (uint32_t) dec;
-    D.cipher = cipher;
-    D.nr = nr;
-    D.pad = 0;
-    D.slot = (uint64_t) (uintptr_t) slot_state;
-    D.ghtab = (uint64_t) (uintptr_t) ghtab;
-    D.hpw = (uint64_t) (uintptr_t) hpw;
+    D.p = *pl;
+    /* TLS 1.2 GCM decrypt: nonce bytes 4..11 are the record's explicit IV
+     * (ssl_msg.c:1352-1365, the kernels' nonce_words) */
+    if (dec && pl->explicit_iv) memcpy(D.p.nonce + 4, buf + rec->data_offset, 8);
+    const uint64_t tag = (uint64_t) (seq & 0xffffu) << 48;
+    if (g_debug)
+        fprintf(stderr, "tlsrec server: slot %d seq %u state %p ghtab %p hpw %p req %p\n", i, seq, slot_state, ghtab, hpw,
+                (void *) rq);
+    rq->w[1] = ((uint64_t) (uintptr_t) slot_state & SRV_PTR_MASK) | tag;
+    rq->w[2] = ((uint64_t) (uintptr_t) ghtab & SRV_PTR_MASK) | tag;
+    rq->w[3] = ((uint64_t) (uintptr_t) hpw & SRV_PTR_MASK) | tag;
     const uint32_t bytes = (pre + (uint32_t) buf_len + 15u) & ~15u;
-    __atomic_store_n(&rq->hdr, ((uint64_t) bytes << 32) | seq, __ATOMIC_RELEASE);
+    const uint64_t w0 = (uint64_t) seq | (uint64_t) bytes << 32 | (uint64_t) (cipher & 0xff) << 48 |
+                        (uint64_t) (dec ? 1 : 0) << 56 | (uint64_t) (nr & 0x1f) << 57;
+    __atomic_store_n(&rq->w[0], w0, __ATOMIC_RELEASE);
 
     int rc = 0;
     for (uint32_t spins = 1;; spins++) {
         if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
         __builtin_ia32_pause();
-        if ((spins & 4095) == 0 && hipEventQuery(S->ev) != hipErrorNotReady) {
+        hipError_t eq;
+        if ((spins & 4095) == 0 && (eq = hipEventQuery(S->ev)) != hipErrorNotReady) {
             /* the grid has ended: served just before, or never taken */
+            if (g_debug) fprintf(stderr, "tlsrec server: grid ended (%s) before seq %u\n", hipGetErrorString(eq), seq);
             if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
             __atomic_store_n(&rq->done, seq, __ATOMIC_RELEASE);   /* withdraw: no later grid serves it */
             rc = 1;

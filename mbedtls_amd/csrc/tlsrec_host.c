@@ -19,7 +19,7 @@
 int tlsrec__engine_slot_alloc(const tlsrec_key_material *km);
 void tlsrec__engine_slot_free(int slot);
 int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned char *buf, size_t buf_len,
-                       const unsigned char *cid, uint32_t aead_pos, tlsrec_batch_res *out);
+                       const unsigned char *cid, const void *plan, tlsrec_batch_res *out);
 int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, size_t cid_len);
 
 static void zeroize(void *p, size_t n)
@@ -139,7 +139,7 @@ static tlsrec_plan_key pkey(const tlsrec_transform *t, int dec)
     return k;
 }
 
-static int run(int dec, tlsrec_transform *t, tlsrec_record *rec, uint32_t aead_pos)
+static int run(int dec, tlsrec_transform *t, tlsrec_record *rec, const tlsrec_plan *p)
 {
     tlsrec_batch_rec d;
     tlsrec_batch_res res;
@@ -154,7 +154,7 @@ static int run(int dec, tlsrec_transform *t, tlsrec_record *rec, uint32_t aead_p
     d.ver[0] = rec->ver[0];
     d.ver[1] = rec->ver[1];
     d.cid_len = dec ? rec->cid_len : 0;
-    int r = tlsrec__engine_run(dec, &d, rec->buf, rec->buf_len, rec->cid, aead_pos, &res);
+    int r = tlsrec__engine_run(dec, &d, rec->buf, rec->buf_len, rec->cid, p, &res);
     if (r != 0) return r;
     /* no kernel reached the record: the staged INTERNAL_ERROR is returned and
      * rec is left as it was (ssl_msg.c:1260 / :1804, auth_done != 1) */
@@ -195,7 +195,7 @@ int tlsrec_encrypt_buf(void *ssl, tlsrec_transform *t, tlsrec_record *rec)
         return p.status;
     }
     if (t->slot_enc < 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
-    return run(0, t, rec, p.aead_pos);
+    return run(0, t, rec, &p);
 }
 
 /* mbedtls_ssl_decrypt_buf (ssl_msg.c:1270-1834), AEAD transforms */
@@ -216,7 +216,7 @@ int tlsrec_decrypt_buf(const void *ssl, tlsrec_transform *t, tlsrec_record *rec)
         return p.status;
     }
     if (t->slot_dec < 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
-    return run(1, t, rec, p.aead_pos);
+    return run(1, t, rec, &p);
 }
 
 int tlsrec_frame_check(int decrypt, const tlsrec_key_material *km, const tlsrec_batch_rec *rec,

@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -m pytest tests/test_server_gpu.py -x -v --timeout 1
 tail -2 $O/tests.txt
 : > $O/latency.jsonl
 for a in "2 1.3 16383" "2 1.3 1400" "3 1.3 1400" "1 1.2 1400" "2 1.3 100"; do
-  timeout -k 10 120 ./tests/c/abi_host latency $a 2000 >> $O/latency.jsonl || { echo "latency $a failed"; exit 1; }
+  TLSREC_SERVER_DEBUG=${SRV_DEBUG:-} timeout -k 10 120 ./tests/c/abi_host latency $a 2000 >> $O/latency.jsonl 2>> $O/stderr.txt || { echo "latency $a failed"; exit 1; }
 done
 for t in 1 16 32; do
   timeout -k 10 120 ./tests/c/abi_host threads $t 2000 gcm_chacha >> $O/latency.jsonl || { echo "threads $t failed"; exit 1; }
