@@ -266,9 +266,20 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
         }
         if (j < n) Y = k ? xor4(gmul<0>(tab, Y), X) : X;
     };
-    /* two steps' counter blocks at a time: independent AES chains interleave
-     * (a lane's AES is a dependent LDS round trip per round) */
+    /* four / two steps' counter blocks at a time: independent AES chains
+     * interleave (a lane's AES is a dependent LDS round trip per round) */
     uint32_t k = 0;
+    for (; k + 3 < K; k += 4) {
+        const uint32_t j = (uint32_t) q + 64 * k;
+        const uint4 ks0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
+        const uint4 ks1 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 65)));
+        const uint4 ks2 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 129)));
+        const uint4 ks3 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 193)));
+        block(k, ks0);
+        block(k + 1, ks1);
+        block(k + 2, ks2);
+        block(k + 3, ks3);
+    }
     for (; k + 1 < K; k += 2) {
         const uint32_t j = (uint32_t) q + 64 * k;
         const uint4 ks0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
