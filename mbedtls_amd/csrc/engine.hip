@@ -1188,7 +1188,7 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
 /* server.hip: the resident record server (AES-GCM, ChaCha20-Poly1305) */
 extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const tlsrec_batch_rec *rec,
                                   const void *slot_state, const void *ghtab, const void *hpw, unsigned char *buf,
-                                  size_t buf_len, const void *plan, tlsrec_batch_res *out);
+                                  size_t buf_len, const void *plan, int skip, tlsrec_batch_res *out);
 
 /* Run one record through the kernels: host buffer -> device -> host.  A
  * decrypted record's CID (cid_len bytes) is staged right after the buffer.
@@ -1218,7 +1218,7 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
         const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, kt->d_slots + idx,
                                          kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS,
                                          g_pages[rec->slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) idx * 64, buf,
-                                         buf_len, plan, out);
+                                         buf_len, plan, g_test_skip == 0, out);
         if (r <= 0) return r;
     }
     Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co[engine_queue(cipher, dec)];

@@ -87,7 +87,9 @@ struct SrvDesc {
 static_assert(sizeof(SrvDesc) == 144, "SrvDesc layout");
 
 /* What one poll reads (four 8-byte loads in flight together):
- *   w[0] = seq | staged bytes << 32 | cipher << 48 | dec << 56 | nr << 57
+ *   w[0] = seq | staged bytes << 32 | cipher << 48 | dec << 56 | nr << 57 | skip << 62
+ *          (skip: the test hook tlsrec__test_skip_record -- the request is
+ *          answered with its INTERNAL_ERROR result and nothing else)
  *   w[1] = the slot's SlotState, w[2] its GHASH tables, w[3] its H^1 .. H^64
  *          (device addresses < 2^48), each | (seq & 0xffff) << 48
  * The host writes w[1..3] before w[0] (release); a poll that sees a new seq
@@ -104,11 +106,12 @@ struct SrvReq {
     uint8_t pad1[60];
     SrvDesc desc;
     tlsrec_batch_res res;
-    uint8_t pad2[32];
+    uint64_t trace[10];       /* TLSREC_SERVER_TRACE: device wall-clock stamps of the request's phases */
+    uint8_t pad3[16];
     uint8_t buf[SRV_BUF];
 };
 static_assert(offsetof(SrvReq, done) == 64 && offsetof(SrvReq, desc) == 128 && offsetof(SrvReq, res) == 272 &&
-                  offsetof(SrvReq, buf) == 320 && sizeof(SrvReq) % 64 == 0,
+                  offsetof(SrvReq, buf) == 384 && sizeof(SrvReq) % 64 == 0,
               "SrvReq layout");
 
 /* ---------------- LDS record access (16-byte aligned AEAD region) -------- */
@@ -164,6 +167,107 @@ __device__ __forceinline__ uint4 srv_gfmul(uint4 x, uint4 y)
     uint32_t r[4];
     tlsrec_gf128_mul(a, b, r);
     return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+/* ---------------- compact AES / ChaCha20 for the server ------------------ *
+ * A served record runs its code once, so the request path's instruction
+ * footprint -- not its issue rate -- is the cost: the batch kernels' fully
+ * unrolled AES (14 rounds x 2-4 interleaved blocks) is tens of KiB of
+ * straight-line code that every request fetches again.  Here the rounds are
+ * a loop; the round keys sit one word per lane (lane i = word i of the
+ * rotated schedule) and each round takes its four with v_readlane. */
+struct LaneKeys {
+    uint32_t v;
+    __device__ __forceinline__ uint32_t operator[](int i) const { return (uint32_t) __builtin_amdgcn_readlane(v, i); }
+};
+
+/* All 16 T-table lookups of a round for every block, then one wait: with a
+ * single wave per SIMD nothing else hides the LDS latency, and left alone
+ * the compiler interleaves each lookup's XOR right behind it (a wait per
+ * couple of lookups).  The asm takes the lookups as operands, so every XOR
+ * comes after it, and its memory clobber keeps every read before it. */
+#define SRV_PIN16(t)                                                                                              \
+    asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),       \
+                      "+v"(t[7]), "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]), "+v"(t[12]), "+v"(t[13]),    \
+                      "+v"(t[14]), "+v"(t[15]) : : "memory")
+
+template <int NB>
+__device__ __forceinline__ void srv_lookups(const uint8_t *lds, uint32_t lb, const uint32_t (&s)[NB][4], int last,
+                                            uint32_t (&t)[NB][16])
+{
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            /* middle rounds: T0 / T1 alternating; last round: T0 only (S-box bytes) */
+            t[b][4 * c + 0] = tlook<0>(lds, s[b][c], lb, 0, 0);
+            t[b][4 * c + 1] = tlook<0>(lds, s[b][(c + 1) & 3], lb, 1, last ? 0 : 1);
+            t[b][4 * c + 2] = tlook<0>(lds, s[b][(c + 2) & 3], lb, 2, 0);
+            t[b][4 * c + 3] = tlook<0>(lds, s[b][(c + 3) & 3], lb, 3, last ? 0 : 1);
+        }
+#pragma unroll
+    for (int b = 0; b < NB; b++) SRV_PIN16(t[b]);
+}
+
+template <int NR, int NB>
+__device__ __forceinline__ void srv_aes(const uint8_t *lds, uint32_t lb, LaneKeys rk, const uint4 (&in)[NB],
+                                        uint4 (&out)[NB])
+{
+    uint32_t s[NB][4], t[NB][16];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        s[b][0] = in[b].x ^ rk[0];
+        s[b][1] = in[b].y ^ rk[1];
+        s[b][2] = in[b].z ^ rk[2];
+        s[b][3] = in[b].w ^ rk[3];
+    }
+#pragma unroll 1
+    for (int r = 1; r < NR; r++) {
+        const uint32_t k[4] = { rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3] };
+        srv_lookups<NB>(lds, lb, s, 0, t);
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)     /* rotated round keys: see aes_encrypt */
+                s[b][c] = xor3(t[b][4 * c], t[b][4 * c + 1], rotl16(xor3(t[b][4 * c + 2], t[b][4 * c + 3], k[c])));
+    }
+    srv_lookups<NB>(lds, lb, s, 1, t);
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        uint32_t o[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {          /* last round: S[x] is byte 1 (and byte 2) of T0[x] */
+            const uint32_t lo = __builtin_amdgcn_perm(t[b][4 * c + 1], t[b][4 * c], 0x0C0C0501u);
+            const uint32_t hi = __builtin_amdgcn_perm(t[b][4 * c + 3], t[b][4 * c + 2], 0x06020C0Cu);
+            o[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);
+        }
+        out[b] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+/* chacha_block (tlsrec_device.h) with the double rounds as a loop */
+__device__ __forceinline__ void srv_chacha_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3],
+                                                 uint32_t out[16])
+{
+    const uint32_t in[16] = { 0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                              key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                              counter, nonce[0], nonce[1], nonce[2] };
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = in[i];
+#pragma unroll 1
+    for (int i = 0; i < 10; i++) {
+        TLSREC_QR(x[0], x[4], x[8], x[12]);
+        TLSREC_QR(x[1], x[5], x[9], x[13]);
+        TLSREC_QR(x[2], x[6], x[10], x[14]);
+        TLSREC_QR(x[3], x[7], x[11], x[15]);
+        TLSREC_QR(x[0], x[5], x[10], x[15]);
+        TLSREC_QR(x[1], x[6], x[11], x[12]);
+        TLSREC_QR(x[2], x[7], x[8], x[13]);
+        TLSREC_QR(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
 }
 
 /* Everything a served record needs, uniform over the wave (the AEAD's own
@@ -231,7 +335,7 @@ __device__ __forceinline__ void nonce_of(const tlsrec_plan &p, uint32_t nw[3])
  * closing power H^(n - j_last); rk: the round keys (rotated form). */
 template <int NR, bool DEC>
 __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8_t *lds, const uint8_t *tab, uint4 hd,
-                                                    const uint32_t *rk, int lane)
+                                                    LaneKeys rk, int lane, uint64_t *tst)
 {
     const tlsrec_plan &p = J.p;
     const int q = lane;
@@ -264,34 +368,41 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
         } else if (j == m + 1) {
             X = lenw;
         }
-        if (j < n) Y = k ? xor4(gmul<0>(tab, Y), X) : X;
+        if (j < n) Y = k ? xor4(gmul<0, 1>(tab, Y), X) : X;   /* one wait for all 32 table reads */
     };
     /* four / two steps' counter blocks at a time: independent AES chains
      * interleave (a lane's AES is a dependent LDS round trip per round) */
+    auto ctrb = [&](uint32_t c) { return make_uint4(nw[0], nw[1], nw[2], bswap32(c)); };
     uint32_t k = 0;
+#pragma unroll 1
     for (; k + 3 < K; k += 4) {
         const uint32_t j = (uint32_t) q + 64 * k;
-        const uint4 ks0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
-        const uint4 ks1 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 65)));
-        const uint4 ks2 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 129)));
-        const uint4 ks3 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 193)));
-        block(k, ks0);
-        block(k + 1, ks1);
-        block(k + 2, ks2);
-        block(k + 3, ks3);
+        const uint4 x[4] = { ctrb(j + 1), ctrb(j + 65), ctrb(j + 129), ctrb(j + 193) };
+        uint4 ks[4];
+        srv_aes<NR, 4>(lds, lanebase, rk, x, ks);
+        block(k, ks[0]);
+        block(k + 1, ks[1]);
+        block(k + 2, ks[2]);
+        block(k + 3, ks[3]);
     }
-    for (; k + 1 < K; k += 2) {
+    if (k + 1 < K) {
         const uint32_t j = (uint32_t) q + 64 * k;
-        const uint4 ks0 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1)));
-        const uint4 ks1 = aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 65)));
-        block(k, ks0);
-        block(k + 1, ks1);
+        const uint4 x[2] = { ctrb(j + 1), ctrb(j + 65) };
+        uint4 ks[2];
+        srv_aes<NR, 2>(lds, lanebase, rk, x, ks);
+        block(k, ks[0]);
+        block(k + 1, ks[1]);
+        k += 2;
     }
     if (k < K) {
-        const uint32_t j = (uint32_t) q + 64 * k;
-        block(k, aes_encrypt<NR, 0>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(j + 1))));
+        const uint4 x[1] = { ctrb((uint32_t) q + 64 * k + 1) };
+        uint4 ks[1];
+        srv_aes<NR, 1>(lds, lanebase, rk, x, ks);
+        block(k, ks[0]);
     }
+    if (tst) tst[0] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.y)) == 0x5bd1e995u ? 0 : wall_clock64();
     if (kq) Y = srv_gfmul(Y, hd);
+    if (tst) tst[1] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.y)) == 0x5bd1e995u ? 0 : wall_clock64();
     const uint4 S = xor_all(Y);
     const uint4 e0 = make_uint4(__builtin_amdgcn_readlane(ej0.x, 0), __builtin_amdgcn_readlane(ej0.y, 0),
                                 __builtin_amdgcn_readlane(ej0.z, 0), __builtin_amdgcn_readlane(ej0.w, 0));
@@ -364,7 +475,7 @@ __device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, cons
 
     /* step 0's keystream: lane q makes block q, lane 0 the one-time key */
     uint32_t ks0[16];
-    chacha_block(key, (uint32_t) lane, nw, ks0);
+    srv_chacha_block(key, (uint32_t) lane, nw, ks0);
     uint32_t r0[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) r0[i] = __builtin_amdgcn_readlane(ks0[i], 0);
@@ -391,7 +502,7 @@ __device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, cons
 #pragma unroll
             for (int i = 0; i < 16; i++) ks[i] = ks0[i];
         } else if (c <= B) {
-            chacha_block(key, c, nw, ks);
+            srv_chacha_block(key, c, nw, ks);
         }
         if (c >= 1 && c <= B) {
 #pragma unroll
@@ -430,13 +541,18 @@ __device__ __forceinline__ uint32_t comp(uint4 v, int i)
  * burst of loads (record and descriptor over PCIe, key data from HBM), the
  * AEAD in LDS, the record and result back to the slot. */
 __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotState *st, const uint4 *ghtab,
-                                          const uint4 *hpw, const uint8_t *lds, uint8_t *wl, int lane)
+                                          const uint4 *hpw, const uint8_t *lds, uint8_t *wl, int lane, uint32_t trace)
 {
+    const uint64_t ts0 = trace ? wall_clock64() : 0;
+    const uint64_t cy0 = trace ? __builtin_readcyclecounter() : 0;
+    uint64_t tsx[2] = { 0, 0 };
+    uint64_t *tst = trace ? tsx : nullptr;
     uint8_t *tab = wl, *stage = wl + SRV_TAB;
     const uint32_t bytes = (uint32_t) (w0 >> 32) & 0xffffu;
     const uint32_t cipher = (uint32_t) (w0 >> 48) & 0xffu;
     const bool dec = (w0 >> 56) & 1u;
     const uint32_t nr = (uint32_t) (w0 >> 57) & 0x1fu;
+    const bool skip = (w0 >> 62) & 1u;
     const bool gcm = cipher != TLSREC_CIPHER_CHACHA20_POLY1305;
     const uint32_t n16 = bytes > SRV_BUF ? 0u : (bytes + 15) / 16;
     /* descriptor chunks (lanes 0..8), slot chunks (lanes 0..3 the key
@@ -444,8 +560,9 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
      * this lane's H^(lane+1) (GCM), every 16-byte chunk of the record */
     const uint4 dc = lane < 9 ? gload16(reinterpret_cast<const uint8_t *>(&rq->desc) + 16 * lane) : make_uint4(0, 0, 0, 0);
     const uint8_t *sp = reinterpret_cast<const uint8_t *>(st);
-    const uint4 sc = lane < 4 ? gload16(sp + 16 * lane)
-                     : (gcm && lane < 19) ? gload16(sp + offsetof(SlotState, rkr) + 16 * (lane - 4)) : make_uint4(0, 0, 0, 0);
+    const uint4 sc = lane < 4 ? gload16(sp + 16 * lane) : make_uint4(0, 0, 0, 0);
+    LaneKeys rk;
+    rk.v = (gcm && lane < 60) ? st->rkr[lane] : 0u;
     uint4 hq = make_uint4(0, 0, 0, 0), ht[8];
     if (gcm) {
         hq = hpw[lane];
@@ -471,6 +588,8 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
     uint32_t w[36];
 #pragma unroll
     for (int i = 0; i < 36; i++) w[i] = __builtin_amdgcn_readlane(comp(dc, i & 3), i >> 2);
+    if (trace) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   /* tracing: every load landed */
+    const uint64_t ts1 = trace ? wall_clock64() : 0;
     SrvJob J;
     __builtin_memcpy(&J.d, w, sizeof(J.d));
     __builtin_memcpy(&J.p, w + 14, sizeof(J.p));
@@ -485,7 +604,7 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
     res.type = res.cid_len = 0;
     res.reserved[0] = res.reserved[1] = 0;
     /* the host checked these; a request outside them is refused, not served */
-    const bool ok = n16 != 0 && (uint64_t) J.d.buf_off + J.d.buf_len + 32 <= SRV_BUF && J.d.cid_len == 0 &&
+    const bool ok = !skip && n16 != 0 && (uint64_t) J.d.buf_off + J.d.buf_len + 32 <= SRV_BUF && J.d.cid_len == 0 &&
                     km_cipher == cipher && km_cid == 0 && J.p.status == 0 && J.p.cid_len == 0 &&
                     (uint64_t) J.p.aead_pos + J.p.aead_len + 16 <= J.d.buf_len && ((J.d.buf_off + J.p.aead_pos) & 15) == 0;
     if (ok) {
@@ -493,9 +612,6 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
             const uint32_t *key = kw + 8;              /* tlsrec_key_material.key at byte 32 */
             res = dec ? srv_chachapoly<true>(J, key, tab, lane) : srv_chachapoly<false>(J, key, tab, lane);
         } else {
-            uint32_t rk[60];
-#pragma unroll
-            for (int i = 0; i < 60; i++) rk[i] = __builtin_amdgcn_readlane(comp(sc, i & 3), 4 + (i >> 2));
             const tlsrec_plan &p = J.p;
             const uint32_t n = ((p.aead_len + 15) >> 4) + 2;
             const uint32_t kq = (uint32_t) lane < n ? (n - 1 - (uint32_t) lane) / 64 + 1 : 0;
@@ -503,12 +619,22 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
             const uint4 hd = make_uint4(__shfl(hq.x, (int) dq - 1), __shfl(hq.y, (int) dq - 1),
                                         __shfl(hq.z, (int) dq - 1), __shfl(hq.w, (int) dq - 1));
             if (nr == 10 && cipher == TLSREC_CIPHER_AES_128_GCM)
-                res = dec ? srv_gcm<10, true>(J, lds, tab, hd, rk, lane) : srv_gcm<10, false>(J, lds, tab, hd, rk, lane);
+                res = dec ? srv_gcm<10, true>(J, lds, tab, hd, rk, lane, tst) : srv_gcm<10, false>(J, lds, tab, hd, rk, lane, tst);
             else if (nr == 14 && cipher == TLSREC_CIPHER_AES_256_GCM)
-                res = dec ? srv_gcm<14, true>(J, lds, tab, hd, rk, lane) : srv_gcm<14, false>(J, lds, tab, hd, rk, lane);
+                res = dec ? srv_gcm<14, true>(J, lds, tab, hd, rk, lane, tst) : srv_gcm<14, false>(J, lds, tab, hd, rk, lane, tst);
             else if (nr == 12 && cipher == TLSREC_CIPHER_AES_192_GCM)
-                res = dec ? srv_gcm<12, true>(J, lds, tab, hd, rk, lane) : srv_gcm<12, false>(J, lds, tab, hd, rk, lane);
+                res = dec ? srv_gcm<12, true>(J, lds, tab, hd, rk, lane, tst) : srv_gcm<12, false>(J, lds, tab, hd, rk, lane, tst);
         }
+    }
+    const uint64_t ts2 = trace ? wall_clock64() : 0;
+    const uint64_t cy2 = trace ? __builtin_readcyclecounter() : 0;
+    if (trace && lane == 0) {
+        rq->trace[0] = ts0;
+        rq->trace[1] = ts1;
+        rq->trace[2] = ts2;
+        rq->trace[4] = tsx[0];
+        rq->trace[5] = tsx[1];
+        rq->trace[6] = cy2 - cy0;
     }
     /* the record (whole staged range) and the result back to the slot */
     if (ok)
@@ -522,9 +648,14 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
 
 } /* namespace */
 
-/* The resident grid: wave w of workgroup b owns request slot b * SRV_WAVES + w. */
-__global__ __launch_bounds__(SRV_WAVES * 64) void tlsrec_server_kernel(SrvReq *reqs, const uint32_t *stop,
-                                                                       uint64_t life_ticks, uint32_t max_iter)
+/* The resident grid: wave w of workgroup b owns request slot b * SRV_WAVES + w.
+ * One wave per SIMD at most (the LDS holds one workgroup per CU): nothing
+ * hides a wave's latency, so the compiler is told to schedule for one wave
+ * per EU -- all lookups of an AES round in flight together, not the few its
+ * occupancy-first scheduling keeps in flight between waits. */
+__global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tlsrec_server_kernel(SrvReq *reqs, const uint32_t *stop,
+                                                                       uint64_t life_ticks, uint32_t max_iter,
+                                                                       uint32_t trace)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SRV_LDS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -554,8 +685,12 @@ __global__ __launch_bounds__(SRV_WAVES * 64) void tlsrec_server_kernel(SrvReq *r
             const uint64_t a0 = uni(h0);
             auto ptr = [&](uint64_t h) { return uni(h) & SRV_PTR_MASK; };
             srv_serve(rq, a0, reinterpret_cast<const SlotState *>(ptr(h1)), reinterpret_cast<const uint4 *>(ptr(h2)),
-                      reinterpret_cast<const uint4 *>(ptr(h3)), lds, wl, lane);
+                      reinterpret_cast<const uint4 *>(ptr(h3)), lds, wl, lane, trace);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");    /* every lane's record stores, system scope */
+            if (trace && lane == 0) {
+                rq->trace[3] = wall_clock64();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            }
             if (lane == 0) __hip_atomic_store(&rq->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             served = seq;
             idle = 0;
@@ -612,6 +747,9 @@ int g_cur = 0;
 int g_state = 0;                  /* 0 not yet set up, 1 ready, -1 unavailable */
 std::atomic<int> g_enabled{1};
 int g_debug = 0;                  /* TLSREC_SERVER_DEBUG=1: one line per request on stderr */
+int g_trace = 0;                  /* TLSREC_SERVER_TRACE=1: device phase times, summed, printed at exit */
+uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr_gcm = 0, g_tr_cyc = 0;
+double g_tick_ns = 10.0;
 uint64_t g_submit_ns = 0, g_life_ticks = 0;
 uint32_t g_max_iter = 0;
 std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
@@ -633,6 +771,16 @@ void srv_shutdown()
             if (g_debug) fprintf(stderr, "tlsrec server: shutdown, grid drained: %s\n", hipGetErrorString(e));
             S.launched = false;
         }
+    if (g_trace && g_tr_n)
+        fprintf(stderr, "{\"server_trace\": {\"requests\": %llu, \"load_us\": %.2f, \"aead_us\": %.2f, "
+                        "\"writeback_us\": %.2f}}\n",
+                (unsigned long long) g_tr_n, g_tr_sum[0] * g_tick_ns / 1e3 / g_tr_n,
+                g_tr_sum[1] * g_tick_ns / 1e3 / g_tr_n, g_tr_sum[2] * g_tick_ns / 1e3 / g_tr_n);
+    if (g_trace && g_tr_n)
+        fprintf(stderr, "{\"server_trace_detail\": {\"gcm_to_horner_end_us\": %.2f, \"gcm_final_mul_us\": %.2f, "
+                        "\"clock_ghz\": %.3f}}\n",
+                g_tr_gcm ? g_tr_aes * g_tick_ns / 1e3 / g_tr_gcm : 0.0, g_tr_gcm ? g_tr_mul * g_tick_ns / 1e3 / g_tr_gcm : 0.0,
+                (double) g_tr_cyc / ((double) (g_tr_sum[0] + g_tr_sum[1]) * g_tick_ns));
     pthread_mutex_unlock(&g_mu);
 }
 
@@ -641,6 +789,7 @@ int srv_setup_locked()
     if (g_state) return g_state;
     g_state = -1;
     g_debug = getenv("TLSREC_SERVER_DEBUG") != nullptr;
+    g_trace = getenv("TLSREC_SERVER_TRACE") != nullptr;
     const char *e = getenv("TLSREC_SERVER");
     if (e && strcmp(e, "0") == 0) return g_state;
     double ms = 20.0;
@@ -652,6 +801,7 @@ int srv_setup_locked()
         hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
         return g_state;
     g_life_ticks = (uint64_t) (ms * khz);
+    g_tick_ns = 1e6 / khz;
     g_max_iter = (uint32_t) (ms * 10000.0);          /* backstop: a poll (a PCIe read + s_sleep) is > 0.1 us */
     const double margin = ms * 0.1 > 1.0 ? ms * 0.1 : 1.0;
     g_submit_ns = (uint64_t) ((ms - margin) * 1e6);
@@ -689,7 +839,7 @@ SrvSet *srv_current_locked(uint64_t now)
     __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
     (void) hipGetLastError();         /* an earlier call's status (hipEventQuery's NotReady) is not the launch's */
     hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d,
-                       (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter);
+                       (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter, (uint32_t) g_trace);
     const hipError_t le = hipGetLastError();
     if (le != hipSuccess || hipEventRecord(N->ev, N->st) != hipSuccess) {
         if (g_debug) fprintf(stderr, "tlsrec server: launch failed: %s\n", hipGetErrorString(le));
@@ -717,7 +867,7 @@ extern "C" hipError_t tlsrec__launch_srv_hpow(const uint4 *ghtab_slot, uint4 *ou
  * caller runs the launch path), or an error. */
 extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const tlsrec_batch_rec *rec,
                                   const void *slot_state, const void *ghtab, const void *hpw, unsigned char *buf,
-                                  size_t buf_len, const void *plan, tlsrec_batch_res *out)
+                                  size_t buf_len, const void *plan, int skip, tlsrec_batch_res *out)
 {
     if (!g_enabled.load(std::memory_order_relaxed) || g_state < 0 || plan == nullptr) return 1;
     const tlsrec_plan *pl = (const tlsrec_plan *) plan;
@@ -763,7 +913,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     rq->w[3] = ((uint64_t) (uintptr_t) hpw & SRV_PTR_MASK) | tag;
     const uint32_t bytes = (pre + (uint32_t) buf_len + 15u) & ~15u;
     const uint64_t w0 = (uint64_t) seq | (uint64_t) bytes << 32 | (uint64_t) (cipher & 0xff) << 48 |
-                        (uint64_t) (dec ? 1 : 0) << 56 | (uint64_t) (nr & 0x1f) << 57;
+                        (uint64_t) (dec ? 1 : 0) << 56 | (uint64_t) (nr & 0x1f) << 57 | (uint64_t) (skip ? 1 : 0) << 62;
     __atomic_store_n(&rq->w[0], w0, __ATOMIC_RELEASE);
 
     int rc = 0;
@@ -782,8 +932,21 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     }
     if (rc == 0) {
         *out = rq->res;
-        if (buf_len) memcpy(buf, rq->buf + pre, buf_len);
+        /* a request the server refused comes back untouched (fail closed) */
+        if (buf_len && out->status != TLSREC_ERR_SSL_INTERNAL_ERROR) memcpy(buf, rq->buf + pre, buf_len);
         g_served++;
+        if (g_trace) {
+            pthread_mutex_lock(&g_mu);
+            g_tr_n++;
+            for (int k = 0; k < 3; k++) g_tr_sum[k] += rq->trace[k + 1] - rq->trace[k];
+            if (rq->trace[4] && rq->trace[5]) {
+                g_tr_gcm++;
+                g_tr_aes += rq->trace[4] - rq->trace[1];
+                g_tr_mul += rq->trace[5] - rq->trace[4];
+            }
+            g_tr_cyc += rq->trace[6];
+            pthread_mutex_unlock(&g_mu);
+        }
     } else {
         g_fallback++;
     }
