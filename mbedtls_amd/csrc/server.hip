@@ -380,10 +380,12 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
         const uint4 x[4] = { ctrb(j + 1), ctrb(j + 65), ctrb(j + 129), ctrb(j + 193) };
         uint4 ks[4];
         srv_aes<NR, 4>(lds, lanebase, rk, x, ks);
+        if (tst && k == 0) tst[2] = __builtin_amdgcn_readfirstlane((uint32_t) (ks[0].x ^ ks[3].y)) == 0x5bd1e995u ? 0 : wall_clock64();
         block(k, ks[0]);
         block(k + 1, ks[1]);
         block(k + 2, ks[2]);
         block(k + 3, ks[3]);
+        if (tst && k == 0) tst[3] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.w)) == 0x5bd1e995u ? 0 : wall_clock64();
     }
     if (k + 1 < K) {
         const uint32_t j = (uint32_t) q + 64 * k;
@@ -398,7 +400,9 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
         const uint4 x[1] = { ctrb((uint32_t) q + 64 * k + 1) };
         uint4 ks[1];
         srv_aes<NR, 1>(lds, lanebase, rk, x, ks);
+        if (tst && k == 0) tst[2] = __builtin_amdgcn_readfirstlane((uint32_t) (ks[0].x ^ ks[0].y)) == 0x5bd1e995u ? 0 : wall_clock64();
         block(k, ks[0]);
+        if (tst && k == 0) tst[3] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.w)) == 0x5bd1e995u ? 0 : wall_clock64();
     }
     if (tst) tst[0] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.y)) == 0x5bd1e995u ? 0 : wall_clock64();
     if (kq) Y = srv_gfmul(Y, hd);
@@ -545,7 +549,7 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
 {
     const uint64_t ts0 = trace ? wall_clock64() : 0;
     const uint64_t cy0 = trace ? __builtin_readcyclecounter() : 0;
-    uint64_t tsx[2] = { 0, 0 };
+    uint64_t tsx[4] = { 0, 0, 0, 0 };
     uint64_t *tst = trace ? tsx : nullptr;
     uint8_t *tab = wl, *stage = wl + SRV_TAB;
     const uint32_t bytes = (uint32_t) (w0 >> 32) & 0xffffu;
@@ -635,6 +639,8 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
         rq->trace[4] = tsx[0];
         rq->trace[5] = tsx[1];
         rq->trace[6] = cy2 - cy0;
+        rq->trace[7] = tsx[2] ? tsx[2] - ts1 : 0;
+        rq->trace[8] = tsx[3] ? tsx[3] - tsx[2] : 0;
     }
     /* the record (whole staged range) and the result back to the slot */
     if (ok)
@@ -748,7 +754,8 @@ int g_state = 0;                  /* 0 not yet set up, 1 ready, -1 unavailable *
 std::atomic<int> g_enabled{1};
 int g_debug = 0;                  /* TLSREC_SERVER_DEBUG=1: one line per request on stderr */
 int g_trace = 0;                  /* TLSREC_SERVER_TRACE=1: device phase times, summed, printed at exit */
-uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr_gcm = 0, g_tr_cyc = 0;
+uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr_gcm = 0, g_tr_cyc = 0, g_tr_a1 = 0,
+         g_tr_b1 = 0;
 double g_tick_ns = 10.0;
 uint64_t g_submit_ns = 0, g_life_ticks = 0;
 uint32_t g_max_iter = 0;
@@ -778,8 +785,9 @@ void srv_shutdown()
                 g_tr_sum[1] * g_tick_ns / 1e3 / g_tr_n, g_tr_sum[2] * g_tick_ns / 1e3 / g_tr_n);
     if (g_trace && g_tr_n)
         fprintf(stderr, "{\"server_trace_detail\": {\"gcm_to_horner_end_us\": %.2f, \"gcm_final_mul_us\": %.2f, "
-                        "\"clock_ghz\": %.3f}}\n",
+                        "\"first_aes_call_us\": %.2f, \"first_blocks_us\": %.2f, \"clock_ghz\": %.3f}}\n",
                 g_tr_gcm ? g_tr_aes * g_tick_ns / 1e3 / g_tr_gcm : 0.0, g_tr_gcm ? g_tr_mul * g_tick_ns / 1e3 / g_tr_gcm : 0.0,
+                g_tr_gcm ? g_tr_a1 * g_tick_ns / 1e3 / g_tr_gcm : 0.0, g_tr_gcm ? g_tr_b1 * g_tick_ns / 1e3 / g_tr_gcm : 0.0,
                 (double) g_tr_cyc / ((double) (g_tr_sum[0] + g_tr_sum[1]) * g_tick_ns));
     pthread_mutex_unlock(&g_mu);
 }
@@ -945,6 +953,8 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
                 g_tr_mul += rq->trace[5] - rq->trace[4];
             }
             g_tr_cyc += rq->trace[6];
+            g_tr_a1 += rq->trace[7];
+            g_tr_b1 += rq->trace[8];
             pthread_mutex_unlock(&g_mu);
         }
     } else {
