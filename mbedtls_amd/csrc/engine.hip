@@ -970,6 +970,7 @@ struct EnginePage {
     tlsrec_keytab *kt;
     uint4 *d_hpw;                        /* H^1 .. H^64 per GCM slot (the record server's closing powers) */
     uint8_t used[ENGINE_PAGE_SLOTS];
+    uint8_t cid[ENGINE_PAGE_SLOTS];      /* the slot has a DTLS connection ID (the record server takes none) */
     uint32_t nused;
     Combiner *co[ENGINE_QUEUES];
 };
@@ -1050,6 +1051,7 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
         if (r == 0 && hipStreamSynchronize(g_load) != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) {
             P.used[slot] = 1;
+            P.cid[slot] = 0;
             P.nused++;
             slot += pg * ENGINE_PAGE_SLOTS;
         }
@@ -1086,6 +1088,7 @@ extern "C" int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, s
     tlsrec_keytab *kt = slot_table(slot, &i);
     int r = kt && g_pages[slot / ENGINE_PAGE_SLOTS].used[i] ? tlsrec_keytab_set_cid(kt, i, cid, cid_len, g_load)
                                                             : TLSREC_ERR_SSL_INTERNAL_ERROR;
+    if (r == 0) g_pages[slot / ENGINE_PAGE_SLOTS].cid[i] = cid_len != 0;
     pthread_mutex_unlock(&g_mu);
     return r;
 }
@@ -1211,8 +1214,10 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
     const uint32_t cipher = kt->h_cipher[idx];
     if (cipher == 0) return TLSREC_ERR_SSL_INTERNAL_ERROR;
     if (buf_len > 0xffffffffu - 64) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    if ((tlsrec_cipher_is_gcm((int) cipher) || cipher == TLSREC_CIPHER_CHACHA20_POLY1305) && !kt->has_cid &&
-        rec->cid_len == 0) {
+    /* per slot, not the page's has_cid: one CID connection must not take the
+     * server away from the page's other 4095 slots */
+    if ((tlsrec_cipher_is_gcm((int) cipher) || cipher == TLSREC_CIPHER_CHACHA20_POLY1305) &&
+        !g_pages[rec->slot / ENGINE_PAGE_SLOTS].cid[idx] && rec->cid_len == 0) {
         tlsrec_batch_rec d = *rec;
         d.slot = idx;
         const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, kt->d_slots + idx,
