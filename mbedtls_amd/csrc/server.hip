@@ -545,8 +545,9 @@ __device__ __forceinline__ uint32_t comp(uint4 v, int i)
  * burst of loads (record and descriptor over PCIe, key data from HBM), the
  * AEAD in LDS, the record and result back to the slot. */
 __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotState *st, const uint4 *ghtab,
-                                          const uint4 *hpw, const uint8_t *lds, uint8_t *wl, int lane, uint32_t trace)
+                                          const uint4 *hpw, const uint8_t *lds, uint8_t *wl, int lane, uint32_t flags)
 {
+    const uint32_t trace = flags & 1u;
     const uint64_t ts0 = trace ? wall_clock64() : 0;
     const uint64_t cy0 = trace ? __builtin_readcyclecounter() : 0;
     uint64_t tsx[4] = { 0, 0, 0, 0 };
@@ -661,7 +662,7 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
  * occupancy-first scheduling keeps in flight between waits. */
 __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tlsrec_server_kernel(SrvReq *reqs, const uint32_t *stop,
                                                                        uint64_t life_ticks, uint32_t max_iter,
-                                                                       uint32_t trace)
+                                                                       uint32_t flags)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SRV_LDS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -691,9 +692,9 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
             const uint64_t a0 = uni(h0);
             auto ptr = [&](uint64_t h) { return uni(h) & SRV_PTR_MASK; };
             srv_serve(rq, a0, reinterpret_cast<const SlotState *>(ptr(h1)), reinterpret_cast<const uint4 *>(ptr(h2)),
-                      reinterpret_cast<const uint4 *>(ptr(h3)), lds, wl, lane, trace);
+                      reinterpret_cast<const uint4 *>(ptr(h3)), lds, wl, lane, flags);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");    /* every lane's record stores, system scope */
-            if (trace && lane == 0) {
+            if ((flags & 1u) && lane == 0) {
                 rq->trace[3] = wall_clock64();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             }
