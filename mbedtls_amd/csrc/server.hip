@@ -170,12 +170,16 @@ __device__ __forceinline__ uint4 srv_gfmul(uint4 x, uint4 y)
 }
 
 /* ---------------- compact AES / ChaCha20 for the server ------------------ *
- * A served record runs its code once, so the request path's instruction
- * footprint -- not its issue rate -- is the cost: the batch kernels' fully
- * unrolled AES (14 rounds x 2-4 interleaved blocks) is tens of KiB of
- * straight-line code that every request fetches again.  Here the rounds are
- * a loop; the round keys sit one word per lane (lane i = word i of the
- * rotated schedule) and each round takes its four with v_readlane. */
+ * A served record is one wave on a SIMD with nothing else to run, so its
+ * time is latency: a wave keeps at most 15 LDS requests in flight (lgkmcnt),
+ * and on the box an AES-256 block took 2.3 us for one block per lane and 6.7
+ * us for four interleaved (TLSREC_SERVER_TRACE) -- the LDS request rate of
+ * one wave, not VALU issue.  So the rounds are a loop (a smaller request
+ * path: same-box A/B against the batch kernels' unrolled AES, 1.4 KiB p50
+ * 11.4-11.9 vs 12.0-13.2 us, 16 threads 387-406 K vs 282-335 K round trips/s,
+ * profiles/r03m_server/ab_rolled_vs_unrolled.txt), each round's lookups all
+ * issue before one wait, and the round keys sit one word per lane (lane i =
+ * word i of the rotated schedule), four v_readlane per round. */
 struct LaneKeys {
     uint32_t v;
     __device__ __forceinline__ uint32_t operator[](int i) const { return (uint32_t) __builtin_amdgcn_readlane(v, i); }
