@@ -26,5 +26,5 @@ row keysched 300 python3 tools/bench_keysched.py && cat $O/keysched.json &&
 : > $O/latency.jsonl &&
 for a in "2 1.3 16383" "2 1.3 1400" "3 1.3 1400" "1 1.2 1400" "2 1.3 100"; do
   timeout -k 10 120 ./tests/c/abi_host latency $a 2000 >> $O/latency.jsonl || exit 1
-done && for t in 1 16 32; do timeout -k 10 120 ./tests/c/abi_host threads $t 2000 >> $O/latency.jsonl || exit 1; done &&
+done && for t in 1 16 32; do timeout -k 10 120 ./tests/c/abi_host threads $t 2000 gcm_chacha >> $O/latency.jsonl || exit 1; done &&
 cat $O/latency.jsonl
