@@ -163,18 +163,25 @@ TLSREC_HD uint8_t tlsrec__aad(uint8_t aad[16], int tls13, const uint8_t ctr[8], 
      * TLS 1.3: type || ver || len(TLSCiphertext)        (:671-677, :727-731)
      * TLS 1.2: seq  || type || ver || len(plaintext)    (:700-703, :727-731)
      * DTLS 1.2 + CID: tlsrec_cid_aad_byte; aad[] keeps its first 16 bytes */
-    uint8_t n = 0;
     for (int i = 0; i < 16; i++) aad[i] = 0;
     if (!tls13 && cid_len != 0) return tlsrec__cid_aad_head(aad, ctr, type, ver, len_field, cid, cid_len);
+    /* constant positions in each branch: a runtime offset would make the
+     * kernels keep the whole plan in scratch memory */
     if (!tls13) {
-        for (int i = 0; i < 8; i++) aad[n++] = ctr[i];
+        for (int i = 0; i < 8; i++) aad[i] = ctr[i];
+        aad[8] = type;
+        aad[9] = ver[0];
+        aad[10] = ver[1];
+        aad[11] = (uint8_t) (len_field >> 8);
+        aad[12] = (uint8_t) len_field;
+        return 13;
     }
-    aad[n++] = type;
-    aad[n++] = ver[0];
-    aad[n++] = ver[1];
-    aad[n++] = (uint8_t) (len_field >> 8);
-    aad[n++] = (uint8_t) len_field;
-    return n;
+    aad[0] = type;
+    aad[1] = ver[0];
+    aad[2] = ver[1];
+    aad[3] = (uint8_t) (len_field >> 8);
+    aad[4] = (uint8_t) len_field;
+    return 5;
 }
 
 /* mbedtls_ssl_encrypt_buf, AEAD mode.  buf_len/data_offset/data_len are the
