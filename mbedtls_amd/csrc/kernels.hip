@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     }
     __syncthreads();
     if (!gcm) return;
-    if (tid < 3) {                      /* H^2, H^4, H^8 for the table-free lane tree */
+    if (tid < 4) {                      /* H^2, H^4, H^8, H^16 for the table-free lane tree */
         const uint4 w = g_to_words(pw[tid + 1]);
         st->hpow[tid][0] = w.x; st->hpow[tid][1] = w.y; st->hpow[tid][2] = w.z; st->hpow[tid][3] = w.w;
     }

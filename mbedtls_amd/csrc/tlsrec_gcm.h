@@ -123,9 +123,9 @@ __device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, cons
 }
 
 /* The lane tree with table-free multiplies (tlsrec_clmul.h) by the powers
- * P[k] = H^(2^k) held as values: for the wave passes, whose per-record tables
- * otherwise come from HBM (a key's H^8, H^4, H^2 tables, 24 KiB, for 4
- * records of 16 KiB at L = 16). */
+ * P[k] = H^(2^k) held as values (k <= 4: L <= 32): for the wave passes, whose
+ * per-record tables otherwise come from HBM (a key's H^8, H^4, H^2 tables, 24
+ * KiB, for 4 records of 16 KiB at L = 16). */
 __device__ __forceinline__ uint4 gf_mul_v(uint4 x, uint4 p)
 {
     const uint32_t a[4] = { x.x, x.y, x.z, x.w }, b[4] = { p.x, p.y, p.z, p.w };
@@ -135,7 +135,7 @@ __device__ __forceinline__ uint4 gf_mul_v(uint4 x, uint4 p)
 }
 
 template <int SH>
-__device__ __forceinline__ uint4 gtree_v(const uint4 (&P)[4], uint4 Y, int lane, int q)
+__device__ __forceinline__ uint4 gtree_v(const uint4 (&P)[5], uint4 Y, int lane, int q)
 {
     if constexpr (SH >= 1) {
         uint4 o = from_up4<SH>(Y, lane);
@@ -466,15 +466,19 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
             }
             /* tree: sum_q Y_q H^(L-q) */
-            if constexpr (WP && (L == 16 || L == 4 || L == 2)) {
+            /* L = 8 and 32 (the paired passes of DTLS / stream records, 16 per
+             * key, and of k4) too: their tree read the key's H^1 .. H^16 tables
+             * from HBM, 8 KiB each, for a handful of records per key */
+            if constexpr (WP && L >= 2 && L <= 32) {
                 if (a.tm & (L == 16 ? 1u : 2u)) {
                     const SlotState &ss = a.slots[s];
                     uint4 h1;
                     __builtin_memcpy(&h1, ss.h, 16);                 /* H: bytes at a 4-byte-aligned offset */
-                    const uint4 P[4] = { h1,
+                    const uint4 P[5] = { h1,
                                          make_uint4(ss.hpow[0][0], ss.hpow[0][1], ss.hpow[0][2], ss.hpow[0][3]),
                                          make_uint4(ss.hpow[1][0], ss.hpow[1][1], ss.hpow[1][2], ss.hpow[1][3]),
-                                         make_uint4(ss.hpow[2][0], ss.hpow[2][1], ss.hpow[2][2], ss.hpow[2][3]) };
+                                         make_uint4(ss.hpow[2][0], ss.hpow[2][1], ss.hpow[2][2], ss.hpow[2][3]),
+                                         make_uint4(ss.hpow[3][0], ss.hpow[3][1], ss.hpow[3][2], ss.hpow[3][3]) };
                     Y = gtree_v<L / 2>(P, Y, lane, q);
                 } else {
                     Y = gtree<L / 2>(gp, Y, lane, q);

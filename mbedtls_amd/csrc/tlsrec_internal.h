@@ -41,8 +41,8 @@ struct SlotState {
     uint8_t pad0[3];
     uint32_t ark[68];         /* ARIA: the nr + 1 round keys ek1.. (RFC 5794 2.2), 16 B each as LE words;
                                  Camellia: the 26 / 34 64-bit subkeys as (high, low) words */
-    uint32_t hpow[3][4];      /* GCM: H^2, H^4, H^8 as GCM-string words (the table-free lane tree) */
-    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16 - 33 - 3 - 272 - 48];
+    uint32_t hpow[4][4];      /* GCM: H^2, H^4, H^8, H^16 as GCM-string words (the table-free lane tree) */
+    uint8_t pad[1024 - 64 - 240 - 240 - 4 - 16 - 33 - 3 - 272 - 64];
 };
 static_assert(sizeof(SlotState) == 1024, "SlotState layout");
 static_assert(sizeof(tlsrec_key_material) == 64, "key material layout");
@@ -69,7 +69,7 @@ struct GcmArgs {
     uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM / _192_GCM */
     uint32_t g5;              /* host-side launch choice: 5-bit GHASH Horner table (8-lane, 16-wave kernel) */
     uint32_t tm;              /* wave passes, table-free multiplies (tlsrec_clmul.h): bit 0 the 16-lane tree,
-                                 bit 1 the 2- / 4-lane tree, bit 2 the AAD fold and final multiplies */
+                                 bit 1 the 2- / 4- / 8- / 32-lane tree, bit 2 the AAD fold and final multiplies */
     uint32_t skip;            /* test hook (tlsrec__test_skip_record): this record index is never reached */
 };
 
