@@ -64,15 +64,17 @@ using namespace tlsrec;
 
 namespace {
 
-constexpr int SRV_WAVES = 2;                        /* waves (request slots) per workgroup */
-constexpr int SRV_GROUPS = 32;
-constexpr int SRV_SLOTS = SRV_WAVES * SRV_GROUPS;   /* 64 slots per set */
+constexpr int SRV_WAVES = 2;                        /* waves per workgroup: both serve its one request slot */
+constexpr int SRV_GROUPS = 64;
+constexpr int SRV_SLOTS = SRV_GROUPS;               /* 64 slots per set */
+constexpr int SRV_LANES = SRV_WAVES * 64;           /* lanes per record */
 constexpr uint32_t SRV_BUF = 17408;                 /* staged bytes per request (16 KiB record + room) */
-constexpr int SRV_TAB = 8192;                       /* per wave: H^64 table (GCM) / r^1..r^64 (ChaCha) */
-constexpr int SRV_WAVE_LDS = SRV_TAB + (int) SRV_BUF;
-constexpr int SRV_LDS = 65536 + SRV_WAVES * SRV_WAVE_LDS;
+constexpr int SRV_TAB_OFF = 65536;                  /* H^64 table (GCM, 8 KiB) / r^1..r^128 (ChaCha, 2.5 KiB) */
+constexpr int SRV_STAGE_OFF = SRV_TAB_OFF + 8192;   /* the record */
+constexpr int SRV_XCH_OFF = SRV_STAGE_OFF + (int) SRV_BUF;   /* wave 1 -> wave 0 partial sums, poll decisions */
+constexpr int SRV_LDS = SRV_XCH_OFF + 256;
 static_assert(SRV_LDS <= 160 * 1024, "server LDS budget");
-static_assert(SRV_WAVE_LDS % 16 == 0, "16-byte aligned staging");
+static_assert(SRV_STAGE_OFF % 16 == 0 && SRV_XCH_OFF % 16 == 0, "16-byte aligned staging");
 
 /* Request descriptor (lanes 0..8 read it as 16-byte chunks): the record's
  * batch descriptor and the framing plan the host computed for it with the
@@ -334,30 +336,38 @@ __device__ __forceinline__ void nonce_of(const tlsrec_plan &p, uint32_t nw[3])
     nw[2] = ld_u32le(p.nonce + 8);
 }
 
-/* ---------------- AES-GCM, one record per wave ---------------------------- */
-/* tab: the key's H^64 table in LDS (the Horner multiplier); hd: this lane's
- * closing power H^(n - j_last); rk: the round keys (rotated form). */
+/* ---------------- AES-GCM, one record per workgroup (2 waves) -------------- */
+/* Lane g = 64 wave + lane of the workgroup takes the blocks j = g (mod 128)
+ * of A, C_1 .. C_m, LEN.  tab: the key's H^64 table in LDS (the Horner
+ * multiplier H^128 is two multiplies by it); hq: lane i of each wave holds
+ * H^(i+1); rk: the round keys (rotated form); xch: wave 1's partial sums. */
 template <int NR, bool DEC>
-__device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8_t *lds, const uint8_t *tab, uint4 hd,
-                                                    LaneKeys rk, int lane, uint64_t *tst)
+__device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8_t *lds, const uint8_t *tab, uint4 hq,
+                                                    LaneKeys rk, int wave, int lane, uint8_t *xch, uint64_t *tst)
 {
     const tlsrec_plan &p = J.p;
-    const int q = lane;
+    const uint32_t g = (uint32_t) (wave * 64 + lane);
     uint32_t nw[3];
     nonce_of(p, nw);
     const uint32_t m = (p.aead_len + 15) >> 4;         /* C blocks */
     const uint32_t n = m + 2;                          /* A, C_1 .. C_m, LEN */
-    const uint32_t K = (n + 63) >> 6;
+    const uint32_t K = (n + SRV_LANES - 1) / SRV_LANES;
     const uint32_t content_len = DEC ? p.aead_len : p.content_len;
     uint8_t *base = J.rec + p.aead_pos;
-    const uint32_t kq = (uint32_t) q < n ? (n - 1 - (uint32_t) q) / 64 + 1 : 0;
+    /* this lane's chain ends at j_last; it closes with H^d, d = n - j_last in
+     * 1 .. 128: H^d = H^(d-64) * H^64 above 64 */
+    const uint32_t kq = g < n ? (n - 1 - g) / SRV_LANES + 1 : 0;
+    const uint32_t d = kq ? n - (g + SRV_LANES * (kq - 1)) : 1;
+    const uint32_t dl = d > 64 ? d - 64 : d;
+    const uint4 hd = make_uint4(__shfl(hq.x, (int) dl - 1), __shfl(hq.y, (int) dl - 1), __shfl(hq.z, (int) dl - 1),
+                                __shfl(hq.w, (int) dl - 1));
     const uint32_t lanebase = (uint32_t) (lane & 31) << 2;
     const uint4 aadw = aad_words(p);
     const uint4 lenw = make_uint4(0, bswap32((uint32_t) p.aad_len * 8), 0, bswap32(p.aead_len * 8));
     uint4 Y = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
     uint32_t nzpos = 0;
     auto block = [&](uint32_t k, uint4 ks) {
-        const uint32_t j = (uint32_t) q + 64 * k;
+        const uint32_t j = g + SRV_LANES * k;
         uint4 X = make_uint4(0, 0, 0, 0);
         if (j == 0) {
             ej0 = ks;
@@ -372,7 +382,8 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
         } else if (j == m + 1) {
             X = lenw;
         }
-        if (j < n) Y = k ? xor4(gmul<0, 1>(tab, Y), X) : X;   /* one wait for all 32 table reads */
+        /* Horner by H^128 (one wait per table multiply) */
+        if (j < n) Y = k ? xor4(gmul<0, 1>(tab, gmul<0, 1>(tab, Y)), X) : X;
     };
     /* four / two steps' counter blocks at a time: independent AES chains
      * interleave (a lane's AES is a dependent LDS round trip per round) */
@@ -380,20 +391,19 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
     uint32_t k = 0;
 #pragma unroll 1
     for (; k + 3 < K; k += 4) {
-        const uint32_t j = (uint32_t) q + 64 * k;
-        const uint4 x[4] = { ctrb(j + 1), ctrb(j + 65), ctrb(j + 129), ctrb(j + 193) };
+        const uint32_t j = g + SRV_LANES * k;
+        const uint4 x[4] = { ctrb(j + 1), ctrb(j + 1 + SRV_LANES), ctrb(j + 1 + 2 * SRV_LANES),
+                             ctrb(j + 1 + 3 * SRV_LANES) };
         uint4 ks[4];
         srv_aes<NR, 4>(lds, lanebase, rk, x, ks);
-        if (tst && k == 0) tst[2] = __builtin_amdgcn_readfirstlane((uint32_t) (ks[0].x ^ ks[3].y)) == 0x5bd1e995u ? 0 : wall_clock64();
         block(k, ks[0]);
         block(k + 1, ks[1]);
         block(k + 2, ks[2]);
         block(k + 3, ks[3]);
-        if (tst && k == 0) tst[3] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.w)) == 0x5bd1e995u ? 0 : wall_clock64();
     }
     if (k + 1 < K) {
-        const uint32_t j = (uint32_t) q + 64 * k;
-        const uint4 x[2] = { ctrb(j + 1), ctrb(j + 65) };
+        const uint32_t j = g + SRV_LANES * k;
+        const uint4 x[2] = { ctrb(j + 1), ctrb(j + 1 + SRV_LANES) };
         uint4 ks[2];
         srv_aes<NR, 2>(lds, lanebase, rk, x, ks);
         block(k, ks[0]);
@@ -401,27 +411,43 @@ __device__ __forceinline__ tlsrec_batch_res srv_gcm(const SrvJob &J, const uint8
         k += 2;
     }
     if (k < K) {
-        const uint4 x[1] = { ctrb((uint32_t) q + 64 * k + 1) };
+        const uint4 x[1] = { ctrb(g + SRV_LANES * k + 1) };
         uint4 ks[1];
         srv_aes<NR, 1>(lds, lanebase, rk, x, ks);
-        if (tst && k == 0) tst[2] = __builtin_amdgcn_readfirstlane((uint32_t) (ks[0].x ^ ks[0].y)) == 0x5bd1e995u ? 0 : wall_clock64();
+        if (tst && k == 0) tst[2] = __builtin_amdgcn_readfirstlane((uint32_t) (ks[0].x ^ ks[0].y)) == 0x5bd1e995u
+                                        ? 0 : wall_clock64();
         block(k, ks[0]);
-        if (tst && k == 0) tst[3] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.w)) == 0x5bd1e995u ? 0 : wall_clock64();
     }
     if (tst) tst[0] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.y)) == 0x5bd1e995u ? 0 : wall_clock64();
-    if (kq) Y = srv_gfmul(Y, hd);
+    if (kq) {
+        Y = srv_gfmul(Y, hd);
+        if (d > 64) Y = gmul<0, 1>(tab, Y);
+    }
     if (tst) tst[1] = __builtin_amdgcn_readfirstlane((uint32_t) (Y.x ^ Y.y)) == 0x5bd1e995u ? 0 : wall_clock64();
-    const uint4 S = xor_all(Y);
-    const uint4 e0 = make_uint4(__builtin_amdgcn_readlane(ej0.x, 0), __builtin_amdgcn_readlane(ej0.y, 0),
-                                __builtin_amdgcn_readlane(ej0.z, 0), __builtin_amdgcn_readlane(ej0.w, 0));
-    const uint4 tag = xor4(S, e0);
+    uint4 S = xor_all(Y);
     uint32_t nzkey = 0;
     if (DEC && p.inner && nzpos)
         nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
-    return srv_finish<DEC>(J, tag, nzkey, lane);
+    nzkey = group_max<64>(nzkey);
+    uint32_t *x = reinterpret_cast<uint32_t *>(xch);
+    if (wave == 1 && lane == 0) {
+        x[0] = S.x; x[1] = S.y; x[2] = S.z; x[3] = S.w;
+        x[4] = nzkey;
+    }
+    __syncthreads();
+    tlsrec_batch_res r = {};
+    if (wave == 0) {
+        S = xor4(S, make_uint4(x[0], x[1], x[2], x[3]));
+        nzkey = max(nzkey, x[4]);
+        const uint4 e0 = make_uint4(__builtin_amdgcn_readlane(ej0.x, 0), __builtin_amdgcn_readlane(ej0.y, 0),
+                                    __builtin_amdgcn_readlane(ej0.z, 0), __builtin_amdgcn_readlane(ej0.w, 0));
+        r = srv_finish<DEC>(J, xor4(S, e0), nzkey, lane);
+    }
+    __syncthreads();                                   /* wave 0's tag / wipe land before the copy-out */
+    return r;
 }
 
-/* ---------------- ChaCha20-Poly1305, one record per wave ------------------- */
+/* ---------------- ChaCha20-Poly1305, one record per workgroup --------------- */
 __device__ __forceinline__ P5 p_rd(const uint32_t *t) { P5 r; for (int i = 0; i < 5; i++) r.v[i] = t[i]; return r; }
 __device__ __forceinline__ void p_wr(uint32_t *t, const P5 &v) { for (int i = 0; i < 5; i++) t[i] = v.v[i]; }
 
@@ -445,66 +471,81 @@ __device__ __forceinline__ P5 p_sum_all(P5 v, int lane)
 }
 
 /* Poly1305 of A, C_1 .. C_M, LEN over the record's ciphertext in LDS:
- * sum_j X_j r^(n - j), lane q taking j = q (mod 64) */
-__device__ __forceinline__ P5 srv_poly(const uint8_t *base, const tlsrec_plan &p, const uint32_t *rpow, int lane)
+ * sum_j X_j r^(n - j), lane g taking j = g (mod 128); this wave's part */
+__device__ __forceinline__ P5 srv_poly(const uint8_t *base, const tlsrec_plan &p, const uint32_t *rpow, uint32_t g,
+                                       int lane)
 {
     const uint32_t M = (p.aead_len + 15) >> 4;
     const uint32_t n = M + 2;
-    const uint32_t K = (n + 63) >> 6;
-    const P5 r64 = p_rd(rpow + 5 * 63);
+    const uint32_t K = (n + SRV_LANES - 1) / SRV_LANES;
+    const P5 r128 = p_rd(rpow + 5 * (SRV_LANES - 1));
     const uint4 aadw = aad_words(p);
     P5 Y = p_zero();
     for (uint32_t k = 0; k < K; k++) {
-        const uint32_t j = (uint32_t) lane + 64 * k;
+        const uint32_t j = g + SRV_LANES * k;
         if (j >= n) break;
         uint4 w;
         if (j == 0) w = aadw;
         else if (j <= M) w = mask_block(lds16(base + (j - 1) * 16), (j - 1) * 16, p.aead_len);
         else w = make_uint4(p.aad_len, 0, p.aead_len, 0);
         const P5 x = p_block(w);
-        Y = k ? p_add(p_mul(Y, r64), x) : x;
+        Y = k ? p_add(p_mul(Y, r128), x) : x;
     }
-    const uint32_t kq = (uint32_t) lane < n ? (n - 1 - (uint32_t) lane) / 64 + 1 : 0;
-    if (kq) Y = p_mul(Y, p_rd(rpow + 5 * (n - ((uint32_t) lane + 64 * (kq - 1)) - 1)));
+    const uint32_t kq = g < n ? (n - 1 - g) / SRV_LANES + 1 : 0;
+    if (kq) Y = p_mul(Y, p_rd(rpow + 5 * (n - (g + SRV_LANES * (kq - 1)) - 1)));
     else Y = p_zero();
     return p_sum_all(Y, lane);
 }
 
 template <bool DEC>
-__device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, const uint32_t *key, uint8_t *tab, int lane)
+__device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, const uint32_t *key, uint8_t *tab,
+                                                           int wave, int lane, uint8_t *xch)
 {
     const tlsrec_plan &p = J.p;
+    const uint32_t g = (uint32_t) (wave * 64 + lane);
     uint32_t nw[3];
     nonce_of(p, nw);
     const uint32_t B = (p.aead_len + 63) >> 6;         /* ChaCha20 blocks of data; counters 0 .. B */
-    const uint32_t KC = (B + 1 + 63) >> 6;
+    const uint32_t KC = (B + 1 + SRV_LANES - 1) / SRV_LANES;
     const uint32_t content_len = DEC ? p.aead_len : p.content_len;
     uint8_t *base = J.rec + p.aead_pos;
+    uint32_t *x = reinterpret_cast<uint32_t *>(xch);
 
-    /* step 0's keystream: lane q makes block q, lane 0 the one-time key */
+    /* step 0's keystream: lane g makes block g, g = 0 the one-time key */
     uint32_t ks0[16];
-    srv_chacha_block(key, (uint32_t) lane, nw, ks0);
-    uint32_t r0[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) r0[i] = __builtin_amdgcn_readlane(ks0[i], 0);
-    /* r^1 .. r^64 in LDS by doubling: after level t lanes < 2^(t+1) hold theirs */
+    srv_chacha_block(key, g, nw, ks0);
+    /* r^1 .. r^128 in LDS: wave 0 doubles up to r^64, wave 1 multiplies by r^64 */
     uint32_t *rpow = reinterpret_cast<uint32_t *>(tab);
-    P5 rq = p_from_r(r0[0], r0[1], r0[2], r0[3]);
-    if (lane == 0) p_wr(rpow, rq);
+    if (wave == 0) {
+        uint32_t r0[8];
 #pragma unroll
-    for (int t = 0; t < 6; t++) {
-        const int s = 1 << t;
-        if (lane >= s && lane < 2 * s) {
-            rq = p_mul(p_rd(rpow + 5 * (lane - s)), p_rd(rpow + 5 * (s - 1)));
-            p_wr(rpow + 5 * lane, rq);
+        for (int i = 0; i < 8; i++) r0[i] = __builtin_amdgcn_readlane(ks0[i], 0);
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < 8; i++) x[8 + i] = r0[i];
+        P5 rq = p_from_r(r0[0], r0[1], r0[2], r0[3]);
+        if (lane == 0) p_wr(rpow, rq);
+#pragma unroll
+        for (int t = 0; t < 6; t++) {
+            const int s = 1 << t;
+            if (lane >= s && lane < 2 * s) {
+                rq = p_mul(p_rd(rpow + 5 * (lane - s)), p_rd(rpow + 5 * (s - 1)));
+                p_wr(rpow + 5 * lane, rq);
+            }
+            asm volatile("" ::: "memory");
         }
-        asm volatile("" ::: "memory");
     }
+    __syncthreads();
+    if (wave == 1) p_wr(rpow + 5 * g, p_mul(p_rd(rpow + 5 * lane), p_rd(rpow + 5 * 63)));   /* r^(g+1) */
+    __syncthreads();
     P5 h = p_zero();
-    if (DEC) h = srv_poly(base, p, rpow, lane);        /* over the ciphertext, before it is replaced */
+    if (DEC) {
+        h = srv_poly(base, p, rpow, g, lane);          /* over the ciphertext, before it is replaced */
+        __syncthreads();
+    }
     uint32_t nzpos = 0;
     for (uint32_t k = 0; k < KC; k++) {
-        const uint32_t c = (uint32_t) lane + 64 * k;
+        const uint32_t c = g + SRV_LANES * k;
         uint32_t ks[16];
         if (k == 0) {
 #pragma unroll
@@ -526,13 +567,28 @@ __device__ __forceinline__ tlsrec_batch_res srv_chachapoly(const SrvJob &J, cons
             }
         }
     }
-    if (!DEC) h = srv_poly(base, p, rpow, lane);
-    const uint4 s = make_uint4(r0[4], r0[5], r0[6], r0[7]);
-    const uint4 tag = p_finish(h, s);
+    if (!DEC) {
+        __syncthreads();                               /* the whole ciphertext in LDS */
+        h = srv_poly(base, p, rpow, g, lane);
+    }
     uint32_t nzkey = 0;
     if (DEC && p.inner && nzpos)
         nzkey = last_nonzero_key(mask_block(lds16(base + nzpos - 1), nzpos - 1, p.aead_len), nzpos - 1);
-    return srv_finish<DEC>(J, tag, nzkey, lane);
+    nzkey = group_max<64>(nzkey);
+    if (wave == 1 && lane == 0) {
+        p_wr(x, h);
+        x[5] = nzkey;
+    }
+    __syncthreads();
+    tlsrec_batch_res r = {};
+    if (wave == 0) {
+        h = p_carry(p_add(h, p_rd(x)));
+        nzkey = max(nzkey, x[5]);
+        const uint4 s = make_uint4(x[12], x[13], x[14], x[15]);
+        r = srv_finish<DEC>(J, p_finish(h, s), nzkey, lane);
+    }
+    __syncthreads();                                   /* wave 0's tag / wipe land before the copy-out */
+    return r;
 }
 
 __device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p)
@@ -545,18 +601,21 @@ __device__ __forceinline__ uint32_t comp(uint4 v, int i)
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
-/* One request: the record, its descriptor and the key slot's data in one
- * burst of loads (record and descriptor over PCIe, key data from HBM), the
- * AEAD in LDS, the record and result back to the slot. */
+/* One request, both waves: the record, its descriptor and the key slot's data
+ * in one burst of loads (record and descriptor over PCIe, key data from HBM),
+ * the AEAD in LDS, the record and result back to the slot.  Called by both
+ * waves with the same arguments: every branch around a barrier is uniform. */
 __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotState *st, const uint4 *ghtab,
-                                          const uint4 *hpw, const uint8_t *lds, uint8_t *wl, int lane, uint32_t flags)
+                                          const uint4 *hpw, const uint8_t *lds, int wave, int lane, uint32_t flags)
 {
     const uint32_t trace = flags & 1u;
     const uint64_t ts0 = trace ? wall_clock64() : 0;
     const uint64_t cy0 = trace ? __builtin_readcyclecounter() : 0;
     uint64_t tsx[4] = { 0, 0, 0, 0 };
-    uint64_t *tst = trace ? tsx : nullptr;
-    uint8_t *tab = wl, *stage = wl + SRV_TAB;
+    uint64_t *tst = (trace && wave == 0) ? tsx : nullptr;
+    uint8_t *L = const_cast<uint8_t *>(lds);
+    uint8_t *tab = L + SRV_TAB_OFF, *stage = L + SRV_STAGE_OFF, *xch = L + SRV_XCH_OFF;
+    const uint32_t g = (uint32_t) (wave * 64 + lane);
     const uint32_t bytes = (uint32_t) (w0 >> 32) & 0xffffu;
     const uint32_t cipher = (uint32_t) (w0 >> 48) & 0xffu;
     const bool dec = (w0 >> 56) & 1u;
@@ -564,41 +623,40 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
     const bool skip = (w0 >> 62) & 1u;
     const bool gcm = cipher != TLSREC_CIPHER_CHACHA20_POLY1305;
     const uint32_t n16 = bytes > SRV_BUF ? 0u : (bytes + 15) / 16;
-    /* descriptor chunks (lanes 0..8), slot chunks (lanes 0..3 the key
-     * material, 4..18 the rotated round keys at byte 304), the H^64 table and
-     * this lane's H^(lane+1) (GCM), every 16-byte chunk of the record */
+    /* descriptor chunks (lanes 0..8) and key material (lanes 0..3) in each
+     * wave; the rotated round keys one word per lane, this lane's H^(lane+1),
+     * half of the H^64 table per wave (GCM); every 16-byte chunk of the
+     * record, split over the two waves */
     const uint4 dc = lane < 9 ? gload16(reinterpret_cast<const uint8_t *>(&rq->desc) + 16 * lane) : make_uint4(0, 0, 0, 0);
     const uint8_t *sp = reinterpret_cast<const uint8_t *>(st);
     const uint4 sc = lane < 4 ? gload16(sp + 16 * lane) : make_uint4(0, 0, 0, 0);
     LaneKeys rk;
     rk.v = (gcm && lane < 60) ? st->rkr[lane] : 0u;
-    uint4 hq = make_uint4(0, 0, 0, 0), ht[8];
+    uint4 hq = make_uint4(0, 0, 0, 0), ht[4];
     if (gcm) {
         hq = hpw[lane];
 #pragma unroll
-        for (int i = 0; i < 8; i++) ht[i] = ghtab[6 * 512 + lane + 64 * i];
+        for (int i = 0; i < 4; i++) ht[i] = ghtab[6 * 512 + g + SRV_LANES * i];
     }
-    constexpr int NCH = (int) (SRV_BUF / 16 + 63) / 64;
+    constexpr int NCH = (int) (SRV_BUF / 16 + SRV_LANES - 1) / SRV_LANES;
     uint4 r[NCH];
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
-        const uint32_t i = (uint32_t) lane + 64u * k;
+        const uint32_t i = g + (uint32_t) SRV_LANES * k;
         if (i < n16) r[k] = gload16(rq->buf + 16 * i);
     }
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
-        const uint32_t i = (uint32_t) lane + 64u * k;
+        const uint32_t i = g + (uint32_t) SRV_LANES * k;
         if (i < n16) sts16(stage + 16 * i, r[k]);
     }
     if (gcm) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) sts16(tab + 16 * (lane + 64 * i), ht[i]);
+        for (int i = 0; i < 4; i++) sts16(tab + 16 * (g + SRV_LANES * i), ht[i]);
     }
     uint32_t w[36];
 #pragma unroll
     for (int i = 0; i < 36; i++) w[i] = __builtin_amdgcn_readlane(comp(dc, i & 3), i >> 2);
-    if (trace) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   /* tracing: every load landed */
-    const uint64_t ts1 = trace ? wall_clock64() : 0;
     SrvJob J;
     __builtin_memcpy(&J.d, w, sizeof(J.d));
     __builtin_memcpy(&J.p, w + 14, sizeof(J.p));
@@ -612,32 +670,38 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
     res.data_offset = res.data_len = 0;
     res.type = res.cid_len = 0;
     res.reserved[0] = res.reserved[1] = 0;
-    /* the host checked these; a request outside them is refused, not served */
-    const bool ok = !skip && n16 != 0 && (uint64_t) J.d.buf_off + J.d.buf_len + 32 <= SRV_BUF && J.d.cid_len == 0 &&
-                    km_cipher == cipher && km_cid == 0 && J.p.status == 0 && J.p.cid_len == 0 &&
-                    (uint64_t) J.p.aead_pos + J.p.aead_len + 16 <= J.d.buf_len && ((J.d.buf_off + J.p.aead_pos) & 15) == 0;
+    /* the host checked these; a request outside them is refused, not served.
+     * Wave 0's verdict goes to both waves through LDS: the AEAD below has
+     * barriers, so the branch must be the same in both */
+    uint32_t *x = reinterpret_cast<uint32_t *>(xch);
+    if (wave == 0 && lane == 0)
+        x[20] = (!skip && n16 != 0 && (uint64_t) J.d.buf_off + J.d.buf_len + 32 <= SRV_BUF && J.d.cid_len == 0 &&
+                 km_cipher == cipher && km_cid == 0 && J.p.status == 0 && J.p.cid_len == 0 &&
+                 (uint64_t) J.p.aead_pos + J.p.aead_len + 16 <= J.d.buf_len &&
+                 ((J.d.buf_off + J.p.aead_pos) & 15) == 0) ? 1u : 0u;
+    if (trace) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   /* tracing: every load landed */
+    const uint64_t ts1 = trace ? wall_clock64() : 0;
+    __syncthreads();                                   /* the staged record and table, both halves; the verdict */
+    const bool ok = __builtin_amdgcn_readfirstlane(x[20]) != 0;
     if (ok) {
         if (!gcm) {
             const uint32_t *key = kw + 8;              /* tlsrec_key_material.key at byte 32 */
-            res = dec ? srv_chachapoly<true>(J, key, tab, lane) : srv_chachapoly<false>(J, key, tab, lane);
-        } else {
-            const tlsrec_plan &p = J.p;
-            const uint32_t n = ((p.aead_len + 15) >> 4) + 2;
-            const uint32_t kq = (uint32_t) lane < n ? (n - 1 - (uint32_t) lane) / 64 + 1 : 0;
-            const uint32_t dq = kq ? n - ((uint32_t) lane + 64 * (kq - 1)) : 1;   /* lane dq - 1 holds H^dq */
-            const uint4 hd = make_uint4(__shfl(hq.x, (int) dq - 1), __shfl(hq.y, (int) dq - 1),
-                                        __shfl(hq.z, (int) dq - 1), __shfl(hq.w, (int) dq - 1));
-            if (nr == 10 && cipher == TLSREC_CIPHER_AES_128_GCM)
-                res = dec ? srv_gcm<10, true>(J, lds, tab, hd, rk, lane, tst) : srv_gcm<10, false>(J, lds, tab, hd, rk, lane, tst);
-            else if (nr == 14 && cipher == TLSREC_CIPHER_AES_256_GCM)
-                res = dec ? srv_gcm<14, true>(J, lds, tab, hd, rk, lane, tst) : srv_gcm<14, false>(J, lds, tab, hd, rk, lane, tst);
-            else if (nr == 12 && cipher == TLSREC_CIPHER_AES_192_GCM)
-                res = dec ? srv_gcm<12, true>(J, lds, tab, hd, rk, lane, tst) : srv_gcm<12, false>(J, lds, tab, hd, rk, lane, tst);
+            res = dec ? srv_chachapoly<true>(J, key, tab, wave, lane, xch)
+                      : srv_chachapoly<false>(J, key, tab, wave, lane, xch);
+        } else if (nr == 10 && cipher == TLSREC_CIPHER_AES_128_GCM) {
+            res = dec ? srv_gcm<10, true>(J, lds, tab, hq, rk, wave, lane, xch, tst)
+                      : srv_gcm<10, false>(J, lds, tab, hq, rk, wave, lane, xch, tst);
+        } else if (nr == 14 && cipher == TLSREC_CIPHER_AES_256_GCM) {
+            res = dec ? srv_gcm<14, true>(J, lds, tab, hq, rk, wave, lane, xch, tst)
+                      : srv_gcm<14, false>(J, lds, tab, hq, rk, wave, lane, xch, tst);
+        } else if (nr == 12 && cipher == TLSREC_CIPHER_AES_192_GCM) {
+            res = dec ? srv_gcm<12, true>(J, lds, tab, hq, rk, wave, lane, xch, tst)
+                      : srv_gcm<12, false>(J, lds, tab, hq, rk, wave, lane, xch, tst);
         }
     }
     const uint64_t ts2 = trace ? wall_clock64() : 0;
     const uint64_t cy2 = trace ? __builtin_readcyclecounter() : 0;
-    if (trace && lane == 0) {
+    if (trace && wave == 0 && lane == 0) {
         rq->trace[0] = ts0;
         rq->trace[1] = ts1;
         rq->trace[2] = ts2;
@@ -645,76 +709,104 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
         rq->trace[5] = tsx[1];
         rq->trace[6] = cy2 - cy0;
         rq->trace[7] = tsx[2] ? tsx[2] - ts1 : 0;
-        rq->trace[8] = tsx[3] ? tsx[3] - tsx[2] : 0;
+        rq->trace[8] = 0;
     }
-    /* the record (whole staged range) and the result back to the slot */
+    /* the record (whole staged range, both halves) and the result back to the slot */
     if (ok)
-        for (uint32_t i = (uint32_t) lane; i < n16; i += 64) gstore16(rq->buf + 16 * i, lds16(stage + 16 * i));
-    if (lane == 0) {
+        for (uint32_t i = g; i < n16; i += SRV_LANES) gstore16(rq->buf + 16 * i, lds16(stage + 16 * i));
+    if (wave == 0 && lane == 0) {
         uint4 rv;
         __builtin_memcpy(&rv, &res, sizeof(rv));
         gstore16(reinterpret_cast<uint8_t *>(&rq->res), rv);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      /* this wave's record stores, system scope */
+    __syncthreads();                                   /* ... and the other wave's */
 }
 
 } /* namespace */
 
-/* The resident grid: wave w of workgroup b owns request slot b * SRV_WAVES + w.
- * One wave per SIMD at most (the LDS holds one workgroup per CU): nothing
- * hides a wave's latency, so the compiler is told to schedule for one wave
- * per EU -- all lookups of an AES round in flight together, not the few its
- * occupancy-first scheduling keeps in flight between waits. */
-__global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tlsrec_server_kernel(SrvReq *reqs, const uint32_t *stop,
-                                                                       uint64_t life_ticks, uint32_t max_iter,
-                                                                       uint32_t flags)
+/* The resident grid: workgroup b (two waves, one per SIMD pair) owns request
+ * slot b.  Wave 0 polls; every poll's verdict goes to wave 1 through LDS
+ * (double-buffered by poll parity) behind one barrier, so both waves leave
+ * the loop together.  At most one wave per SIMD (the LDS holds one workgroup
+ * per CU): the compiler is told to schedule for one wave per EU -- all
+ * lookups of an AES round in flight together. */
+__global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tlsrec_server_kernel(
+    SrvReq *reqs, const uint32_t *stop, uint64_t life_ticks, uint32_t max_iter, uint32_t flags)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SRV_LDS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     aes_fill_tables(lds, tid, SRV_WAVES * 64);
+    SrvReq *rq = reqs + blockIdx.x;
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(lds + SRV_XCH_OFF + 128);   /* [2][10] poll verdicts */
     __syncthreads();
-    SrvReq *rq = reqs + blockIdx.x * SRV_WAVES + wave;
-    uint8_t *wl = lds + 65536 + wave * SRV_WAVE_LDS;
     const uint64_t t0 = wall_clock64();
     uint32_t served = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&rq->done, __ATOMIC_RELAXED,
                                                                        __HIP_MEMORY_SCOPE_SYSTEM));
     uint32_t idle = 0;
-    for (uint32_t it = 0; it < max_iter; it++) {
-        const uint64_t h0 = ld_sys64(&rq->w[0]), h1 = ld_sys64(&rq->w[1]), h2 = ld_sys64(&rq->w[2]),
-                       h3 = ld_sys64(&rq->w[3]);
-        const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t) h0);
-        if (seq != served) {
-            const uint64_t tagw = (uint64_t) (seq & 0xffffu) << 48;
-            if (((h1 ^ tagw) | (h2 ^ tagw) | (h3 ^ tagw)) >> 48) continue;   /* half-posted: read again */
+    for (uint32_t it = 0;; it++) {
+        uint32_t *c = ctl + (it & 1) * 10;
+        if (wave == 0) {
+            /* verdict: 0 idle, 1 serve, 2 leave, 3 poll again at once */
+            uint32_t v = 2;
+            uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+            if (it < max_iter) {
+                h0 = ld_sys64(&rq->w[0]);
+                h1 = ld_sys64(&rq->w[1]);
+                h2 = ld_sys64(&rq->w[2]);
+                h3 = ld_sys64(&rq->w[3]);
+                const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t) h0);
+                if (seq != served) {
+                    const uint64_t tagw = (uint64_t) (seq & 0xffffu) << 48;
+                    v = (((h1 ^ tagw) | (h2 ^ tagw) | (h3 ^ tagw)) >> 48) ? 3u : 1u;   /* half-posted: again */
+                    v = __builtin_amdgcn_readfirstlane(v);
+                } else if ((it & 15) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                                 stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0) {
+                    v = 2;
+                } else {
+                    v = (uint64_t) (wall_clock64() - t0) > life_ticks ? 2u : 0u;
+                }
+            }
+            if (lane == 0) {
+                c[0] = v;
+                c[1] = (uint32_t) h0; c[2] = (uint32_t) (h0 >> 32);
+                c[3] = (uint32_t) h1; c[4] = (uint32_t) (h1 >> 32);
+                c[5] = (uint32_t) h2; c[6] = (uint32_t) (h2 >> 32);
+                c[7] = (uint32_t) h3; c[8] = (uint32_t) (h3 >> 32);
+            }
+        }
+        __syncthreads();
+        const uint32_t v = __builtin_amdgcn_readfirstlane(c[0]);
+        if (v == 2) break;
+        if (v == 1) {
+            /* (readfirstlane returns int: widen through uint32_t, never sign-extend) */
+            auto u64 = [&](int i) {
+                return (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane(c[i]) |
+                       (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane(c[i + 1]) << 32;
+            };
+            const uint64_t a0 = u64(1);
             /* synchronizes with the host's release of w[0]: the record and
              * descriptor it wrote before are visible to the loads below */
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            /* (readfirstlane returns int: widen through uint32_t, never sign-extend) */
-            auto uni = [](uint64_t h) {
-                return (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) h) |
-                       (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (h >> 32)) << 32;
-            };
-            const uint64_t a0 = uni(h0);
-            auto ptr = [&](uint64_t h) { return uni(h) & SRV_PTR_MASK; };
-            srv_serve(rq, a0, reinterpret_cast<const SlotState *>(ptr(h1)), reinterpret_cast<const uint4 *>(ptr(h2)),
-                      reinterpret_cast<const uint4 *>(ptr(h3)), lds, wl, lane, flags);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");    /* every lane's record stores, system scope */
-            if ((flags & 1u) && lane == 0) {
-                rq->trace[3] = wall_clock64();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            srv_serve(rq, a0, reinterpret_cast<const SlotState *>(u64(3) & SRV_PTR_MASK),
+                      reinterpret_cast<const uint4 *>(u64(5) & SRV_PTR_MASK),
+                      reinterpret_cast<const uint4 *>(u64(7) & SRV_PTR_MASK), lds, wave, lane, flags);
+            const uint32_t seq = (uint32_t) a0;
+            if (wave == 0 && lane == 0) {
+                if (flags & 1u) {
+                    rq->trace[3] = wall_clock64();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                }
+                __hip_atomic_store(&rq->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            if (lane == 0) __hip_atomic_store(&rq->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             served = seq;
             idle = 0;
-            continue;
+        } else if (v == 0 && wave == 0) {
+            /* a slot idle for ~1 ms polls every few us instead of every ~2 us
+             * (the host hands out the lowest free slot, so busy slots stay hot) */
+            if (++idle > 512) __builtin_amdgcn_s_sleep(127);
+            else __builtin_amdgcn_s_sleep(8);
         }
-        if ((it & 15) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(stop, __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_SYSTEM)) != 0)
-            break;
-        if ((uint64_t) (wall_clock64() - t0) > life_ticks) break;
-        /* a slot idle for ~1 ms polls every few us instead of every ~2 us
-         * (the host hands out the lowest free slot, so busy slots stay hot) */
-        if (++idle > 512) __builtin_amdgcn_s_sleep(127);
-        else __builtin_amdgcn_s_sleep(8);
     }
 }
 
