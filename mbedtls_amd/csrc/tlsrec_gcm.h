@@ -20,6 +20,10 @@
 #include "tlsrec_internal.h"
 #include "tlsrec_recdev.h"
 
+#ifndef TLSREC_GCM_LINE_GROUPS
+#define TLSREC_GCM_LINE_GROUPS 1
+#endif
+
 namespace tlsrec {
 
 /* ======================================================================
@@ -430,6 +434,36 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 {
                     const uint8_t *sp = jb.src + (size_t) (BL * j + q - z) * 16;
                     uint8_t *dp = jb.dst + (size_t) (BL * j + q - z) * 16;
+                    /* 2 / 4 lanes per record (the paired passes over small
+                     * records): a record's 128-byte line spans G = 128 / (16 L)
+                     * steps, and 32 records per wave keep 4 MiB of such lines
+                     * live per XCD -- the L2's size -- so lines were fetched
+                     * and written back part-used.  Load G steps' blocks
+                     * together and store them together: each line is touched
+                     * once per direction. */
+                    if constexpr (PAIR && L <= 4 && B == 1 && TLSREC_GCM_LINE_GROUPS) {
+                        constexpr int G = 128 / (16 * L);
+                        for (; j + G <= jh; j += G) {
+                            uint4 blk[G], out[G];
+#pragma unroll
+                            for (int t = 0; t < G; t++) blk[t] = gload16(sp + 16 * BL * t);
+#pragma unroll
+                            for (int t = 0; t < G; t++) {
+                                const int32_t cc = (int32_t) (BL * (j + t) + q) - (int32_t) z;
+                                uint4 ks, Zn;
+                                crypt(cc, xor4(Z, Xp), ks, Zn);
+                                out[t] = xor4(blk[t], ks);
+                                if (DEC && jb.inner && (out[t].x | out[t].y | out[t].z | out[t].w))
+                                    nzpos = (uint32_t) cc * 16 + 1;
+                                Z = Zn;
+                                Xp = DEC ? blk[t] : out[t];
+                            }
+#pragma unroll
+                            for (int t = 0; t < G; t++) gstore16(dp + 16 * BL * t, out[t]);
+                            sp += 16 * BL * G;
+                            dp += 16 * BL * G;
+                        }
+                    }
                     for (; j < jh; j++) {
 #pragma unroll
                         for (int b = 0; b < B; b++) {
