@@ -443,6 +443,22 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                      * once per direction. */
                     if constexpr (PAIR && L <= 4 && B == 1 && TLSREC_GCM_LINE_GROUPS) {
                         constexpr int G = 128 / (16 * L);
+                        /* single steps up to a group boundary: groups then
+                         * start on a line for records without front padding
+                         * (z = 0: whole-block AEAD lengths, 128-byte slots) */
+                        for (; j < jh && j % G != 0; j++) {
+                            const int32_t cc = (int32_t) (BL * j + q) - (int32_t) z;
+                            const uint4 blk = gload16(sp);
+                            uint4 ks, Zn;
+                            crypt(cc, xor4(Z, Xp), ks, Zn);
+                            const uint4 o = xor4(blk, ks);
+                            gstore16(dp, o);
+                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
+                            Z = Zn;
+                            Xp = DEC ? blk : o;
+                            sp += 16 * BL;
+                            dp += 16 * BL;
+                        }
                         for (; j + G <= jh; j += G) {
                             uint4 blk[G], out[G];
 #pragma unroll
