@@ -8,9 +8,13 @@ tlsrec_batch_decrypt call over the whole batch (one kernel launch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
 
-Multi-GPU (driver): torchrun ... bench.py --gpus N.  Records shard by
-contiguous range (2^20 per rank, weak scaling); the only collective is the
-RCCL broadcast of the key table from rank 0 (plus the max-time reduction).
+Multi-GPU: `python bench.py --gpus N` starts N rank processes itself (one per
+GPU, before any GPU call in the parent; launch_ranks), or runs as one rank of
+an external `torch.distributed.run ... bench.py --gpus N`.  Either way every
+rank checks that the process group really has N ranks.  Records shard by
+contiguous range (2^20 per rank, weak scaling: BASELINE configs[4] = 8 M x
+16 KiB over 8 GPUs at N = 8); the only collective is the RCCL broadcast of the
+key table from rank 0 (plus the max-time reduction).
 
 Prints ONE JSON line on rank 0.
 """
@@ -98,6 +102,61 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def rank_env(base, rank, world, port):
+    """The environment of rank `rank` of a `world`-rank job on this node (the
+    variables torch.distributed.run would set)."""
+    e = dict(base)
+    e.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+             GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return e
+
+
+def launch_ranks(world, argv, script=None, env=None, poll_s=0.2):
+    """Start `world` rank processes of `script` (this file) with `argv` and
+    wait for them.  Children, never an exec: the parent has made no GPU call.
+    Rank 0's JSON line reaches stdout directly (the children inherit it).  The
+    first rank that fails ends the others (by their own PIDs) and its exit
+    code is returned; a signal to the parent is passed on to the ranks."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = script or os.path.abspath(__file__)
+    base = dict(os.environ if env is None else env)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=rank_env(base, r, world, port))
+             for r in range(world)]
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = {sig: signal.signal(sig, lambda s, f: (stop(), sys.exit(128 + s))) for sig in (signal.SIGTERM, signal.SIGINT)}
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    log(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks")
+                    stop()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        stop()
+        for p in procs:
+            p.wait()
+        for sig, h in old.items():
+            signal.signal(sig, h)
+    return rc
+
+
 def inner_len(content, tls):
     if tls == "TLS1.3":
         return content + 1 + (16 - (content + 1) % 16) % 16
@@ -106,11 +165,24 @@ def inner_len(content, tls):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # this process is the launcher: count the devices (no GPU context is
+        # made by device_count on this image) and start one rank per GPU
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            log(f"bench.py: --gpus {args.gpus} needs {args.gpus} HIP devices, {have} visible; "
+                f"refusing to report a {have}-GPU run as {args.gpus} GPUs")
+            sys.exit(2)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     import torch
     import torch.distributed as dist
     import mbedtls_amd as M
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"bench.py: WORLD_SIZE {world} but --gpus {args.gpus}")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -119,6 +191,7 @@ def main():
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     cname, tls, direction, content, n_default, nkeys, workload = CONFIGS[args.config]
     n = args.records or n_default

@@ -197,3 +197,46 @@ def load():
         f.argtypes = args
     _lib = L
     return L
+
+
+TEST_LIB_PATH = os.path.join(PKG, "libtlsrec_test.so")
+_test_lib = None
+
+
+def test_library():
+    """The test-hooks build (tests/ only), loaded once, with the ABI's
+    signatures bound."""
+    global _test_lib
+    if _test_lib is None:
+        if not os.path.exists(TEST_LIB_PATH):
+            raise ImportError(f"{TEST_LIB_PATH} is missing: build it with `python -m mbedtls_amd.build`")
+        load()                       # torch first, as load() does
+        L = ctypes.CDLL(TEST_LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _test_lib = L
+    return _test_lib
+
+
+class use_library:
+    """Context manager for tests/: route every binding to another in-tree
+    build of the same ABI for the duration -- the test-hooks build
+    libtlsrec_test.so (-DTLSREC_TEST_HOOKS, the only one exporting
+    tlsrec__test_*).  Objects (KeyTable, Transform) keep the library they were
+    created with, so create them inside the block."""
+
+    def __init__(self):
+        self.saved = None
+
+    def __enter__(self):
+        global _lib
+        L = test_library()
+        self.saved, _lib = _lib, L
+        return L
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.saved
+        return False

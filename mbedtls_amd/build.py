@@ -5,6 +5,12 @@
 
 The shared library lands next to this file (mbedtls_amd/libtlsrec.so) so
 that it travels with a gpurun snapshot; objects go to build/.
+
+Beside it, libtlsrec_test.so: the same library compiled with
+-DTLSREC_TEST_HOOKS (the reference's MBEDTLS_TEST_HOOKS, ssl_misc.h:2685) --
+the tlsrec__test_* entry points and the kernels' unreached-record compare
+exist only there.  Only tests/ load it (tests/test_fail_closed_gpu.py through
+mbedtls_amd._abi.use_library); units that hold no hook share their objects.
 """
 from __future__ import annotations
 
@@ -18,6 +24,8 @@ CSRC = os.path.join(PKG, "csrc")
 INC = os.path.join(ROOT, "include")
 OBJ = os.path.join(ROOT, "build")
 LIB = os.path.join(PKG, "libtlsrec.so")
+TEST_LIB = os.path.join(PKG, "libtlsrec_test.so")
+TEST_OBJ = os.path.join(OBJ, "test_hooks")
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # parallel compiles: the box exports MAX_JOBS=16; here 8 CPUs (and ~2 GB per hipcc)
@@ -31,6 +39,9 @@ HEADERS = ["tlsrec_device.h", "tlsrec_frame.h", "tlsrec_internal.h", "tlsrec_rec
 UNITS = [("gcm_dec.hip", "hip"), ("gcm_enc.hip", "hip"), ("gcm_alt_dec.hip", "hip"), ("gcm_alt_enc.hip", "hip"),
          ("kernels.hip", "hip"), ("engine.hip", "hip"), ("keysched.hip", "hip"), ("stream.hip", "hip"), ("ccm.hip", "hip"), ("ticket.hip", "hip"),
          ("server.hip", "hip"), ("tlsrec_host.c", "c")]
+# units whose code changes under TLSREC_TEST_HOOKS (TLSREC_HOOK_SKIP, the hook entry points)
+HOOK_UNITS = {"gcm_dec.hip", "gcm_enc.hip", "gcm_alt_dec.hip", "gcm_alt_enc.hip", "kernels.hip", "engine.hip",
+              "ccm.hip", "server.hip"}
 
 
 def _mtime(p):
@@ -43,19 +54,26 @@ def _deps():
 
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(TEST_OBJ, exist_ok=True)
     dep_time = max(_mtime(p) for p in _deps())
-    objs, cmds = [], []
+    objs, test_objs, cmds = [], [], []
     for src, kind in UNITS:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src.rsplit(".", 1)[0] + ".o")
-        objs.append(o)
-        if not force and _mtime(o) > max(_mtime(s), dep_time):
-            continue
-        if kind == "hip":
-            cmds.append([HIPCC] + HIP_FLAGS + ["-c", s, "-o", o])
-        else:
-            cmds.append(["gcc"] + C_FLAGS + ["-c", s, "-o", o])
-    # translation units compile in parallel (kernels.hip dominates)
+        stem = src.rsplit(".", 1)[0] + ".o"
+        variants = [(os.path.join(OBJ, stem), [])]
+        if src in HOOK_UNITS:
+            variants.append((os.path.join(TEST_OBJ, stem), ["-DTLSREC_TEST_HOOKS"]))
+        objs.append(variants[0][0])
+        test_objs.append(variants[-1][0])
+        for o, extra in variants:
+            if not force and _mtime(o) > max(_mtime(s), dep_time):
+                continue
+            if kind == "hip":
+                cmds.append([HIPCC] + HIP_FLAGS + extra + ["-c", s, "-o", o])
+            else:
+                cmds.append(["gcc"] + C_FLAGS + extra + ["-c", s, "-o", o])
+    # translation units compile in parallel, the slowest first (the GCM units dominate)
+    cmds.sort(key=lambda c: 0 if any("gcm_" in x for x in c) else (1 if any("kernels" in x for x in c) else 2))
     from concurrent.futures import ThreadPoolExecutor
     def run(cmd):
         if verbose:
@@ -63,11 +81,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
         subprocess.run(cmd, check=True)
     with ThreadPoolExecutor(max_workers=min(JOBS, max(1, len(cmds)))) as ex:
         list(ex.map(run, cmds))
-    if force or _mtime(LIB) < max(_mtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+    for lib, lib_objs in ((LIB, objs), (TEST_LIB, test_objs)):
+        if force or _mtime(lib) < max(_mtime(o) for o in lib_objs):
+            cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib] + lib_objs
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
     return LIB
 
 

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
             const uint32_t s = a.recs[my_rec].slot;
             const bool usable = s < a.capacity && a.slots[s].km.cipher != 0;
             const int c = usable ? a.slots[s].km.cipher : 0;   /* no read past the table */
-            if (my_rec == a.skip) {
+            if (TLSREC_HOOK_SKIP(my_rec, a.skip)) {
                 /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
             } else if (usable && (ARIA ? tlsrec_cipher_is_alt_ccm(c) && tlsrec_cipher_alt_nr(c) == NR
                                 : tlsrec_cipher_is_ccm(c) && tlsrec_cipher_nr(c) == NR))

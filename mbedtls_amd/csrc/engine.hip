@@ -301,6 +301,42 @@ struct ScratchEntry {
 static pthread_mutex_t g_scratch_mu = PTHREAD_MUTEX_INITIALIZER;
 static ScratchEntry *g_scratch = nullptr;
 
+/* hipStreamPerThread entries belong to their thread: freed when it exits, so
+ * a server whose connections come and go on short-lived threads does not
+ * accumulate device memory */
+static pthread_key_t g_scratch_key;
+static pthread_once_t g_scratch_once = PTHREAD_ONCE_INIT;
+
+static void scratch_thread_exit(void *)
+{
+    const uintptr_t me = (uintptr_t) pthread_self();
+    ScratchEntry *mine = nullptr;
+    pthread_mutex_lock(&g_scratch_mu);
+    for (ScratchEntry **pp = &g_scratch; *pp;) {
+        ScratchEntry *e = *pp;
+        if (e->thread == me) {
+            *pp = e->next;
+            e->next = mine;
+            mine = e;
+        } else {
+            pp = &e->next;
+        }
+    }
+    pthread_mutex_unlock(&g_scratch_mu);
+    while (mine) {
+        ScratchEntry *nx = mine->next;
+        if (mine->mem) {
+            hipStreamSynchronize(hipStreamPerThread);    /* this thread's own stream */
+            hipFree(mine->mem);
+        }
+        pthread_mutex_destroy(&mine->mu);
+        free(mine);
+        mine = nx;
+    }
+}
+
+static void scratch_key_init(void) { pthread_key_create(&g_scratch_key, scratch_thread_exit); }
+
 extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, tlsrec_scratch_lease *lease)
 {
     int dev = 0;
@@ -326,6 +362,10 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
         pthread_mutex_init(&e->mu, NULL);
         e->next = g_scratch;
         g_scratch = e;
+        if (thr) {
+            pthread_once(&g_scratch_once, scratch_key_init);
+            pthread_setspecific(g_scratch_key, (void *) 1);   /* non-NULL: the destructor runs */
+        }
     }
     pthread_mutex_unlock(&g_scratch_mu);
     pthread_mutex_lock(&e->mu);
@@ -348,6 +388,21 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
     lease->mem = e->mem;
     lease->entry = e;
     return 0;
+}
+
+/* diagnostics (tests): scratch entries alive, and their device bytes */
+extern "C" uint32_t tlsrec__scratch_entries(uint64_t *bytes)
+{
+    uint32_t n = 0;
+    uint64_t b = 0;
+    pthread_mutex_lock(&g_scratch_mu);
+    for (ScratchEntry *e = g_scratch; e; e = e->next) {
+        n++;
+        b += e->bytes;
+    }
+    pthread_mutex_unlock(&g_scratch_mu);
+    if (bytes) *bytes = b;
+    return n;
 }
 
 extern "C" void tlsrec__scratch_release(tlsrec_scratch_lease *lease)
@@ -412,11 +467,32 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
 /* avg_bytes: mean record size when the caller knows it (the stream / DTLS
  * layers and the host pipeline do; 0 = unknown) -- it decides the GCM launch
  * for many keys with little work each (below). */
-/* test hook (tlsrec__test_skip_record): the AEAD kernels leave this record
- * index unreached, so a test can show that its result stays INTERNAL_ERROR */
+/* Test hooks (tlsrec_internal.h TLSREC_HOOK_SKIP; the test build only, as the
+ * reference compiles its own under MBEDTLS_TEST_HOOKS, ssl_misc.h:2685):
+ *   tlsrec__test_skip_record   the AEAD kernels leave this record index
+ *                              unreached, so a test can show that its result
+ *                              stays INTERNAL_ERROR
+ *   tlsrec__test_fail_staging  the next n staging-area allocations of the
+ *                              single-record engine fail (ALLOC_FAILED path)
+ *   tlsrec__test_server_shadow served records read their key state from
+ *                              copies at addresses whose low 32 bits have bit
+ *                              31 set (the readfirstlane sign-extension case) */
+#ifdef TLSREC_TEST_HOOKS
 static volatile uint32_t g_test_skip = 0xffffffffu;
+static volatile int g_test_fail_staging = 0;
+static uint8_t *g_test_shadow = nullptr;
+static size_t g_test_shadow_bytes = 0;
 
 extern "C" void tlsrec__test_skip_record(uint32_t index) { g_test_skip = index; }
+extern "C" void tlsrec__test_fail_staging(int n) { g_test_fail_staging = n; }
+extern "C" void tlsrec__test_server_shadow(void *dev, size_t bytes)
+{
+    g_test_shadow = (uint8_t *) dev;
+    g_test_shadow_bytes = dev ? bytes : 0;
+}
+#else
+static constexpr uint32_t g_test_skip = 0xffffffffu;
+#endif
 
 /* Launch options of one batch:
  *   only_mask  launch only these ciphers' kernels (1 << TLSREC_CIPHER_*; the
@@ -990,6 +1066,22 @@ static int engine_init_locked(void)
     return 0;
 }
 
+static void combiner_free(Combiner *c)
+{
+    if (!c) return;
+    for (int i = 0; i < ENGINE_SETS; i++) {
+        if (c->set[i].st) {
+            hipStreamSynchronize(c->set[i].st);
+            hipStreamDestroy(c->set[i].st);
+        }
+        if (c->set[i].h) hipHostFree(c->set[i].h);
+        if (c->set[i].d) hipFree(c->set[i].d);
+    }
+    pthread_cond_destroy(&c->cv);
+    pthread_mutex_destroy(&c->mu);
+    free(c);
+}
+
 static Combiner *combiner_new(void)
 {
     Combiner *c = (Combiner *) calloc(1, sizeof(Combiner));
@@ -998,7 +1090,8 @@ static Combiner *combiner_new(void)
     pthread_cond_init(&c->cv, NULL);
     for (int i = 0; i < ENGINE_SETS; i++)
         if (hipStreamCreateWithFlags(&c->set[i].st, hipStreamNonBlocking) != hipSuccess) {
-            free(c);
+            c->set[i].st = NULL;
+            combiner_free(c);      /* the streams created before this one */
             return NULL;
         }
     return c;
@@ -1026,14 +1119,24 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
             if (pg == ENGINE_MAX_PAGES) {
                 r = TLSREC_ERR_SSL_ALLOC_FAILED;
             } else {
-                r = tlsrec_keytab_create(&g_pages[pg].kt, ENGINE_PAGE_SLOTS);
-                if (r == 0 && hipMalloc((void **) &g_pages[pg].d_hpw, sizeof(uint4) * 64 * ENGINE_PAGE_SLOTS) != hipSuccess)
+                EnginePage &N = g_pages[pg];
+                r = tlsrec_keytab_create(&N.kt, ENGINE_PAGE_SLOTS);
+                if (r == 0 && hipMalloc((void **) &N.d_hpw, sizeof(uint4) * 64 * ENGINE_PAGE_SLOTS) != hipSuccess) {
+                    N.d_hpw = NULL;
                     r = TLSREC_ERR_SSL_ALLOC_FAILED;
+                }
                 for (int q = 0; r == 0 && q < ENGINE_QUEUES; q++)
-                    if (!(g_pages[pg].co[q] = combiner_new())) r = TLSREC_ERR_SSL_ALLOC_FAILED;
-                if (r != 0 && g_pages[pg].kt) {
-                    tlsrec_keytab_free(g_pages[pg].kt);
-                    g_pages[pg].kt = NULL;
+                    if (!(N.co[q] = combiner_new())) r = TLSREC_ERR_SSL_ALLOC_FAILED;
+                if (r != 0) {
+                    /* unwind the partial page: nothing of it stays allocated or pointed at */
+                    for (int q = 0; q < ENGINE_QUEUES; q++) {
+                        combiner_free(N.co[q]);
+                        N.co[q] = NULL;
+                    }
+                    if (N.d_hpw) hipFree(N.d_hpw);
+                    N.d_hpw = NULL;
+                    if (N.kt) tlsrec_keytab_free(N.kt);
+                    N.kt = NULL;
                 }
                 if (r == 0) g_npages = pg + 1;
             }
@@ -1072,6 +1175,8 @@ extern "C" void tlsrec__engine_slot_free(int slot)
         hipMemsetAsync(kt->d_slots + i, 0, sizeof(SlotState), g_load);
         hipMemsetAsync(kt->d_cipher + i, 0, 1, g_load);
         hipMemsetAsync(kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS, 0, sizeof(uint4) * KEY_TABLE_WORDS, g_load);
+        /* the record server's H^1..H^64 of the slot (key-derived, like H) */
+        hipMemsetAsync(P->d_hpw + (size_t) i * 64, 0, sizeof(uint4) * 64, g_load);
         hipStreamSynchronize(g_load);
         kt->h_cipher[i] = 0;
         kt->nloaded--;
@@ -1080,6 +1185,26 @@ extern "C" void tlsrec__engine_slot_free(int slot)
     }
     pthread_mutex_unlock(&g_mu);
 }
+
+#ifdef TLSREC_TEST_HOOKS
+/* test hook: the device bytes of an engine slot -- its SlotState (1024 B),
+ * the first 1024 B of its GHASH tables and its 64 record-server powers
+ * (1024 B) -- copied to host, to show what slot_free leaves behind */
+extern "C" int tlsrec__test_engine_slot_dump(int slot, void *state, void *ghtab, void *hpw)
+{
+    pthread_mutex_lock(&g_mu);
+    uint32_t i = 0;
+    tlsrec_keytab *kt = slot_table(slot, &i);
+    int r = kt ? 0 : TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    if (!r && (hipMemcpy(state, kt->d_slots + i, sizeof(SlotState), hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(ghtab, kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS, 1024, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(hpw, g_pages[slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) i * 64, 1024,
+                         hipMemcpyDeviceToHost) != hipSuccess))
+        r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}
+#endif
 
 extern "C" int tlsrec__engine_slot_set_cid(int slot, const unsigned char *cid, size_t cid_len)
 {
@@ -1116,17 +1241,31 @@ static int run_batch(tlsrec_keytab *kt, EngineSet &S, EngineReq *first, uint32_t
         used = al(used + v[i]->buf_len + v[i]->d.cid_len + 16, ENGINE_ALIGN);
     }
     const size_t need = off_arena + used + ENGINE_ALIGN;
-    if (S.cap < need) {
+    bool fail_alloc = false;
+#ifdef TLSREC_TEST_HOOKS
+    if (g_test_fail_staging > 0) {
+        g_test_fail_staging--;
+        fail_alloc = true;
+    }
+#endif
+    if (S.cap < need || fail_alloc) {
         hipStreamSynchronize(S.st);
         hipHostFree(S.h);
         hipFree(S.d);
         S.h = S.hd = S.d = NULL;
         S.cap = 0;
         const size_t want = need > (1u << 20) ? need + need / 2 : (1u << 20);
-        if (hipHostMalloc((void **) &S.h, want, hipHostMallocMapped) != hipSuccess ||
+        if (fail_alloc || hipHostMalloc((void **) &S.h, want, hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void **) &S.hd, S.h, 0) != hipSuccess ||
-            hipMalloc((void **) &S.d, want) != hipSuccess)
+            hipMalloc((void **) &S.d, want) != hipSuccess) {
+            /* no request of this batch ran: each caller gets the error, never
+             * the unfilled result (ssl_msg.c:1260 / :1804) */
+            if (S.h) hipHostFree(S.h);
+            if (S.d) hipFree(S.d);
+            S.h = S.hd = S.d = NULL;
+            for (uint32_t i = 0; i < n; i++) v[i]->rc = TLSREC_ERR_SSL_ALLOC_FAILED;
             return TLSREC_ERR_SSL_ALLOC_FAILED;
+        }
         S.cap = want;
     }
     tlsrec_batch_rec *hd = (tlsrec_batch_rec *) S.h;
@@ -1220,10 +1359,38 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
         !g_pages[rec->slot / ENGINE_PAGE_SLOTS].cid[idx] && rec->cid_len == 0) {
         tlsrec_batch_rec d = *rec;
         d.slot = idx;
-        const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, kt->d_slots + idx,
-                                         kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS,
-                                         g_pages[rec->slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) idx * 64, buf,
-                                         buf_len, plan, g_test_skip == 0, out);
+        const void *p_state = kt->d_slots + idx;
+        const void *p_ghtab = kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS;
+        const void *p_hpw = g_pages[rec->slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) idx * 64;
+#ifdef TLSREC_TEST_HOOKS
+        if (g_test_shadow) {
+            /* copies at the first address of the test's buffer whose low word
+             * has bit 31 set, all three inside that half of the 4 GiB window */
+            const size_t sz[3] = { sizeof(SlotState), sizeof(uint4) * KEY_TABLE_WORDS, sizeof(uint4) * 64 };
+            const size_t tot = sz[0] + sz[1] + sz[2];
+            const uintptr_t b0 = (uintptr_t) g_test_shadow, end = b0 + g_test_shadow_bytes;
+            uintptr_t at = (b0 + 255) & ~(uintptr_t) 255;
+            if (!(at & 0x80000000u) || (at & 0xffffffffu) + tot > 0x100000000ull)
+                at = ((at & 0xffffffffu) + tot > 0x100000000ull ? (at | 0xffffffffull) + 1 : at & ~(uintptr_t) 0xffffffffu) |
+                     0x80000000u;
+            if (at + tot > end) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+            const void *src[3] = { p_state, p_ghtab, p_hpw };
+            uint8_t *dst = (uint8_t *) at;
+            const void *dsts[3];
+            for (int k = 0; k < 3; k++) {
+                if (hipMemcpyAsync(dst, src[k], sz[k], hipMemcpyDeviceToDevice, g_load) != hipSuccess)
+                    return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                dsts[k] = dst;
+                dst += sz[k];
+            }
+            if (hipStreamSynchronize(g_load) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+            p_state = dsts[0];
+            p_ghtab = dsts[1];
+            p_hpw = dsts[2];
+        }
+#endif
+        const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, p_state, p_ghtab, p_hpw,
+                                         buf, buf_len, plan, g_test_skip == 0, out);
         if (r <= 0) return r;
     }
     Combiner *co = g_pages[rec->slot / ENGINE_PAGE_SLOTS].co[engine_queue(cipher, dec)];
@@ -1235,7 +1402,11 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
     me.buf = buf;
     me.buf_len = buf_len;
     me.cid = cid;
-    me.rc = 0;
+    /* fail closed: a request no batch filled in reads as an error, never as
+     * the success its zeroed result would say */
+    me.rc = TLSREC_ERR_SSL_INTERNAL_ERROR;
+    memset(&me.res, 0, sizeof(me.res));
+    me.res.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
     me.done = 0;
     me.next = NULL;
     pthread_mutex_lock(&co->mu);

@@ -662,7 +662,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const tlsrec_batch_rec d = a.recs[my_rec];
-            const bool reach = my_rec != a.skip;   /* test hook: the guard's INTERNAL_ERROR stays */
+            const bool reach = !TLSREC_HOOK_SKIP(my_rec, a.skip);   /* test hook: the guard's INTERNAL_ERROR stays */
             if (reach && !a.perm && !(d.slot < a.capacity && a.slots[d.slot].km.cipher != 0))
                 bad_slot_result(d, &a.res[my_rec]);
             if (reach && d.slot < a.capacity && a.slots[d.slot].km.cipher == TLSREC_CIPHER_CHACHA20_POLY1305) {
@@ -1125,6 +1125,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void tlsrec_scan_apply_kernel(const u
     }
 }
 
+#ifdef TLSREC_TEST_HOOKS
 /* Self-test of the cross-lane helpers (tlsrec_recdev.h) for
  * tests/test_lane_ops_gpu.py: one wave, lane i holds v_i = (i * 37 + 11) & 63
  * plus 100 * i; rows of 64 words:
@@ -1167,6 +1168,7 @@ extern "C" int tlsrec__test_lane_ops(uint32_t *host_out /* 17 x 64 words */)
     hipFree(d);
     return e == hipSuccess ? 0 : -1;
 }
+#endif /* TLSREC_TEST_HOOKS */
 
 extern "C" size_t tlsrec__scan_scratch_bytes(uint32_t n)
 {
@@ -1183,6 +1185,7 @@ extern "C" hipError_t tlsrec__exclusive_scan(const uint32_t *in, uint32_t *out, 
     return hipGetLastError();
 }
 
+#ifdef TLSREC_TEST_HOOKS
 /* tests/test_scan_gpu.py: the scan over host arrays (copies in, scans, copies out) */
 extern "C" int tlsrec__test_scan(const uint32_t *host_in, uint32_t n, uint32_t *host_out)
 {
@@ -1195,6 +1198,7 @@ extern "C" int tlsrec__test_scan(const uint32_t *host_in, uint32_t n, uint32_t *
     hipFree(d);
     return e == hipSuccess ? 0 : -1;
 }
+#endif /* TLSREC_TEST_HOOKS */
 
 extern "C" hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st)
 {

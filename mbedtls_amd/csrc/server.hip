@@ -620,7 +620,7 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
     const uint32_t cipher = (uint32_t) (w0 >> 48) & 0xffu;
     const bool dec = (w0 >> 56) & 1u;
     const uint32_t nr = (uint32_t) (w0 >> 57) & 0x1fu;
-    const bool skip = (w0 >> 62) & 1u;
+    const bool skip = TLSREC_HOOK_SKIP(1u, (uint32_t) (w0 >> 62) & 1u);
     const bool gcm = cipher != TLSREC_CIPHER_CHACHA20_POLY1305;
     const uint32_t n16 = bytes > SRV_BUF ? 0u : (bytes + 15) / 16;
     /* descriptor chunks (lanes 0..8) and key material (lanes 0..3) in each

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
             const uint32_t s = a.recs[my_rec].slot;
-            if (my_rec == a.skip) {
+            if (TLSREC_HOOK_SKIP(my_rec, a.skip)) {
                 /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
             } else if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
                 my_slot = s;

@@ -11,7 +11,17 @@
 
 namespace tlsrec {
 
-constexpr int KEY_TABLES = 7;                       /* H^1, H^2, ..., H^64 (4-bit position tables) */
+/* Test hooks, the reference's MBEDTLS_TEST_HOOKS (ssl_misc.h:2685): only the
+ * test build (libtlsrec_test.so, -DTLSREC_TEST_HOOKS, tests/ only) can leave a
+ * record unreached by the kernels; in the release library the compare is
+ * compiled out and no entry point sets it. */
+#ifdef TLSREC_TEST_HOOKS
+#define TLSREC_HOOK_SKIP(rec, skip) ((rec) == (skip))
+#else
+#define TLSREC_HOOK_SKIP(rec, skip) false
+#endif
+
+constexpr int KEY_TABLES = 7;                      /* H^1, H^2, ..., H^64 (4-bit position tables) */
 /* plus H^8 as 5-bit position tables read in 8-byte halves (gmul5 in
  * tlsrec_device.h): 26 windows x 512 B, the 8-lane Horner multiplier */
 constexpr int KEY_G5_POWER = 3;                     /* H^(2^3) */

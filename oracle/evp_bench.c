@@ -178,7 +178,10 @@ double evp_bench_records(int cipher, int tls13, const uint8_t *key, const uint8_
         jobs[i] = (eb_job) { cipher, tls13, dir, key, iv, arena, stride, data_len,
                              n * (uint64_t) i / (uint64_t) threads, n * (uint64_t) (i + 1) / (uint64_t) threads,
                              seq0, status };
-        if (pthread_create(&tid[i], NULL, eb_worker, &jobs[i]) != 0) return -1.0;
+        if (pthread_create(&tid[i], NULL, eb_worker, &jobs[i]) != 0) {
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);   /* started workers use the caller's buffers */
+            return -1.0;
+        }
     }
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &b);
@@ -257,7 +260,10 @@ eb_mixed *evp_mixed_create(uint32_t nconn, const uint8_t *ciphers, const uint8_t
     int ok = 1;
     for (int i = 0; i < threads; i++) {
         st[i] = (eb_setup) { m, i, 0 };
-        if (pthread_create(&tid[i], NULL, eb_setup_worker, &st[i]) != 0) return evp_mixed_free(m), NULL;
+        if (pthread_create(&tid[i], NULL, eb_setup_worker, &st[i]) != 0) {
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);   /* started workers use the caller's buffers */
+            return evp_mixed_free(m), NULL;
+        }
     }
     for (int i = 0; i < threads; i++) {
         pthread_join(tid[i], NULL);
@@ -317,7 +323,10 @@ double evp_mixed_records(const eb_mixed *m, int dir, uint8_t *arena, size_t stri
     clock_gettime(CLOCK_MONOTONIC, &a);
     for (int i = 0; i < threads; i++) {
         jobs[i] = (eb_mjob) { m, dir, i, threads, arena, stride, data_len, n, status };
-        if (pthread_create(&tid[i], NULL, eb_mworker, &jobs[i]) != 0) return -1.0;
+        if (pthread_create(&tid[i], NULL, eb_mworker, &jobs[i]) != 0) {
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);   /* started workers use the caller's buffers */
+            return -1.0;
+        }
     }
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &b);
@@ -440,7 +449,12 @@ int evp_check_records(int mode, int cipher, int tls13, uint32_t nkeys, const uin
     for (int i = 0; i < threads; i++) {
         jobs[i] = (eb_vjob) { mode, cipher, tls13, i, threads, nkeys, keys, ivs, n, keyidx, len, seq, off, plain, got,
                               result };
-        if (pthread_create(&tid[i], NULL, eb_vworker, &jobs[i]) != 0) return -1;
+        if (pthread_create(&tid[i], NULL, eb_vworker, &jobs[i]) != 0) {
+            /* the workers already started write into result: join them before
+             * the caller may reuse it */
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);
+            return -1;
+        }
     }
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     return 0;

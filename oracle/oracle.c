@@ -911,7 +911,10 @@ double orc_bench_records(const orc_transform *t, int dir, uint8_t *arena,
         jobs[i] = (bench_job) { t, dir, arena, stride, data_len,
                                 n * (uint64_t) i / (uint64_t) threads,
                                 n * (uint64_t) (i + 1) / (uint64_t) threads, seq0, status };
-        if (pthread_create(&tid[i], NULL, bench_worker, &jobs[i]) != 0) return -1.0;
+        if (pthread_create(&tid[i], NULL, bench_worker, &jobs[i]) != 0) {
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);   /* started workers use the caller's buffers */
+            return -1.0;
+        }
     }
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &b);
@@ -966,7 +969,10 @@ double orc_bench_records_multi(const orc_transform *const *ts, uint32_t nconn, i
     clock_gettime(CLOCK_MONOTONIC, &a);
     for (int i = 0; i < threads; i++) {
         jobs[i] = (bench_mjob) { ts, nconn, dir, i, threads, arena, stride, data_len, n, status };
-        if (pthread_create(&tid[i], NULL, bench_mworker, &jobs[i]) != 0) return -1.0;
+        if (pthread_create(&tid[i], NULL, bench_mworker, &jobs[i]) != 0) {
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);   /* started workers use the caller's buffers */
+            return -1.0;
+        }
     }
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     clock_gettime(CLOCK_MONOTONIC, &b);

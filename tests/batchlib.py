@@ -80,9 +80,10 @@ class Batch:
         km = np.concatenate([M.key_material(c, v, k, iv, g) for (c, v, k, iv, g) in self.slots])
         return km
 
-    def run_gpu(self, decrypt: bool, lanes=0, inplace=True, kt=None, mean_bytes=0):
+    def run_gpu(self, decrypt: bool, lanes=0, inplace=True, kt=None, mean_bytes=0, stream=None):
         """kt: an already loaded key table (e.g. filled by keytab_derive);
-        mean_bytes: the record-size hint of tlsrec_batch_*_sized."""
+        mean_bytes: the record-size hint of tlsrec_batch_*_sized; stream: a
+        HIP stream handle other than torch's (e.g. 2 = hipStreamPerThread)."""
         import torch
         dev = torch.device("cuda")
         own = kt is None
@@ -96,7 +97,9 @@ class Batch:
         recs = torch.from_numpy(self.desc.view(np.uint8).copy()).to(dev)
         res = torch.zeros(len(self.recs) * 16, dtype=torch.uint8, device=dev)
         fn = M.batch_decrypt if decrypt else M.batch_encrypt
-        fn(kt, recs, res, len(self.recs), arena, out, lanes=lanes, mean_bytes=mean_bytes)
+        if stream is not None:
+            torch.cuda.synchronize()      # torch's fills above ran on its own stream
+        fn(kt, recs, res, len(self.recs), arena, out, lanes=lanes, mean_bytes=mean_bytes, stream=stream)
         torch.cuda.synchronize()
         out_np = out.cpu().numpy()
         res_np = res.cpu().numpy().view(M.BATCH_RES)

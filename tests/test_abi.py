@@ -32,6 +32,26 @@ def test_library_loads_and_exports_every_symbol():
         assert n in _abi.SIGNATURES, f"python binding lacks {n}"
 
 
+def _exports(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+
+def test_test_hooks_only_in_the_test_build():
+    """The release library carries no test hook (the reference compiles its
+    own only under MBEDTLS_TEST_HOOKS, library/ssl_misc.h:2685); the
+    test-hooks build exports them and every entry point of the ABI."""
+    rel = _exports(_abi.LIB_PATH)
+    tst = _exports(_abi.TEST_LIB_PATH)
+    assert not [s for s in rel if s.startswith("tlsrec__test_")], sorted(s for s in rel if "test" in s)
+    for s in ("tlsrec__test_skip_record", "tlsrec__test_fail_staging", "tlsrec__test_server_shadow",
+              "tlsrec__test_lane_ops", "tlsrec__test_scan"):
+        assert s in tst, s
+    for n in _declared():
+        assert n in tst, n
+
+
 def test_struct_layouts():
     assert ctypes.sizeof(_abi.CRecord) == 88       # + cid_len, cid[32]
     assert ctypes.sizeof(_abi.CTransform) == 232   # + in/out_cid_len, in/out_cid[32]

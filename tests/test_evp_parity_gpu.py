@@ -41,10 +41,11 @@ def _threads():
     return bench.host_cores()[0]
 
 
-def _layout(n, head, rng, span=None):
+def _layout(n, head, rng, span=None, misalign=False):
     """lengths (25 % edge values, 75 % uniform 0..2048, every edge value at
     least 100 times; or uniform in span), 128-B aligned record buffers with
-    tag / padding room"""
+    tag / padding room (misalign: each buffer starts 0..127 bytes into its
+    128-B slot)"""
     if span:
         lens = rng.integers(span[0], span[1] + 1, n).astype(np.uint32)
     else:
@@ -53,9 +54,11 @@ def _layout(n, head, rng, span=None):
         lens[pick] = EDGE[rng.integers(0, len(EDGE), int(pick.sum()))]
         lens[:len(EDGE) * 100] = np.tile(EDGE, 100)
     size = head + lens.astype(np.uint64) + 48
-    al = (size + 127) // 128 * 128
+    al = (size + 127) // 128 * 128 + (128 if misalign else 0)
     off = np.zeros(n, dtype=np.uint64)
     off[1:] = np.cumsum(al)[:-1]
+    if misalign:
+        off += rng.integers(0, 128, n).astype(np.uint64)
     return lens, size, off, int(off[-1] + al[-1])
 
 
@@ -90,12 +93,12 @@ def test_paired_wave_passes_vs_openssl_evp(cipher, ver, nkeys, rpk, span, mean):
     _evp_case(cipher, ver, nkeys, nkeys * rpk, lens=span, mean_bytes=mean)
 
 
-def _evp_case(cipher, ver, nkeys, n, lens=None, mean_bytes=0):
+def _evp_case(cipher, ver, nkeys, n, lens=None, mean_bytes=0, misalign=False):
     torch = _torch()
     dev = torch.device("cuda")
     rng = np.random.default_rng(cipher * 100 + ver + nkeys + n)
     head = 8 if ver == M.VERSION_TLS1_2 and cipher != M.CIPHER_CHACHA20_POLY1305 else 0
-    lens_, size, off, total = _layout(n, head, rng, lens)
+    lens_, size, off, total = _layout(n, head, rng, lens, misalign)
     lens = lens_
     keys, ivs = _keys(cipher, nkeys, rng)
     kl = M.KEYLEN[cipher]
@@ -236,3 +239,120 @@ def test_paired_wave_passes_tree_modes_vs_openssl_evp(monkeypatch, tm, nkeys, rp
     and all of them table-free by H as a value (TREEMUL=7)"""
     monkeypatch.setenv("TLSREC_GCM_TREEMUL", tm)
     _evp_case(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, nkeys, nkeys * rpk, lens=span, mean_bytes=mean)
+
+
+def _evp_sample(torch, dev, A, B, stride, sample, km_keys, km_ivs, slots, cipher, ver, content, threads):
+    """EVP check of the sampled records' ciphertexts (B) sealed from A, with a
+    compact key table holding only the sample's keys"""
+    uk, kidx = np.unique(slots[sample], return_inverse=True)
+    n = len(sample)
+    rows_a = A.view(-1, stride)[torch.from_numpy(sample).to(dev)].cpu().numpy()
+    rows_b = B.view(-1, stride)[torch.from_numpy(sample).to(dev)].cpu().numpy()
+    off = np.arange(n, dtype=np.uint64) * stride
+    return O.evp_check_records(1, cipher, ver, km_keys[uk], km_ivs[uk], kidx.astype(np.uint32),
+                               sample.astype(np.uint64) // len(km_keys), off, np.full(n, content, np.uint32),
+                               rows_a.reshape(-1).copy(), rows_b.reshape(-1).copy(), threads)
+
+
+def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
+    """SURVEY 8(d)-4's 1400-B variant at its stated size, as bench.py times it:
+    65 536 keys x 64 records x 1 400 B TLS 1.3, AES-256-GCM (even keys) and
+    ChaCha20-Poly1305 (odd keys), record i under key i % 65 536 with sequence
+    number i // 65 536, the record-size hint (the line-grouped paired 2-lane
+    GCM passes, 2-lane ChaCha20-Poly1305).  Encrypt: every status and length,
+    a >= 4096-record EVP sample over both ciphers and the first and last keys.
+    Decrypt: 1 record in 1024 bit-flipped, INVALID_MAC at exactly those
+    indices, every other plaintext checked on the device, the failed ones wiped
+    (ssl_msg.c:1412-1424)."""
+    torch = _torch()
+    dev = torch.device("cuda")
+    nkeys, rpk, content = 1 << 16, 64, 1400
+    n = nkeys * rpk
+    inner, wire, stride = 1408, 1424, 1536
+    rng = np.random.default_rng(0xC45)
+    keys = rng.integers(0, 256, (nkeys, 32), dtype=np.uint8)
+    ivs = rng.integers(0, 256, (nkeys, 12), dtype=np.uint8)
+    cip = np.where(np.arange(nkeys) % 2 == 0, M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305)
+    km = np.zeros(nkeys, dtype=M.KEY_MATERIAL)
+    km["cipher"] = cip
+    km["tls_minor"] = 4
+    km["fixed_ivlen"] = 12
+    km["taglen"] = 16
+    km["key"] = keys
+    km["iv"][:, :12] = ivs
+    kt = M.KeyTable(nkeys)
+    kt.load(km)
+    slots = (np.arange(n) % nkeys).astype(np.uint32)
+    try:
+        d = M.records(n)
+        d["buf_off"] = np.arange(n, dtype=np.uint64) * stride
+        d["buf_len"] = stride
+        d["data_len"] = content
+        d["slot"] = slots
+        d["ctr"] = M.seq_bytes(np.arange(n, dtype=np.uint64) // nkeys)
+        d["type"] = 23
+        d["ver"] = (3, 3)
+        g = torch.Generator(device=dev)
+        g.manual_seed(4545)
+        A = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
+        B = torch.empty_like(A)
+        res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        M.batch_encrypt(kt, torch.from_numpy(d.view(np.uint8).copy()).to(dev), res, n, A, B, mean_bytes=wire)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(M.BATCH_RES)
+        assert (r["status"] == 0).all(), np.unique(r["status"], return_counts=True)
+        assert (r["data_offset"] == 0).all() and (r["data_len"] == wire).all()
+
+        # EVP: >= 4096 records over both ciphers, with every record of the
+        # first and of the last key
+        sample = np.unique(np.concatenate([np.arange(0, n, 1021, dtype=np.int64)[:4100],
+                                           np.arange(0, n, nkeys, dtype=np.int64),
+                                           np.arange(nkeys - 1, n, nkeys, dtype=np.int64)]))
+        assert len(sample) >= 4096
+        for c in (M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305):
+            s = sample[cip[slots[sample]] == c]
+            assert len(s) >= 1024
+            bad = _evp_sample(torch, dev, A, B, stride, s, keys, ivs, slots, c, M.VERSION_TLS1_3, content, _threads())
+            assert int((bad != 0).sum()) == 0, f"cipher {c}: {int((bad != 0).sum())} of {len(s)} differ from OpenSSL"
+
+        # decrypt with 1 record in 1024 bit-flipped (odd: tag, even: ciphertext)
+        tam = np.arange(29, n, 1024, dtype=np.int64)
+        pos = np.where(np.arange(len(tam)) % 2 == 1, inner + (tam % 16), (tam * 37) % inner)
+        flat = torch.from_numpy(tam * stride + pos).to(dev)
+        bit = torch.from_numpy((1 << (tam % 8)).astype(np.uint8)).to(dev)
+        B[flat] = B[flat] ^ bit
+        dd = d.copy()
+        dd["data_len"] = wire
+        C = torch.empty_like(A)
+        res.zero_()
+        M.batch_decrypt(kt, torch.from_numpy(dd.view(np.uint8).copy()).to(dev), res, n, B, C, mean_bytes=wire)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(M.BATCH_RES)
+        want = np.zeros(n, dtype=np.int32)
+        want[tam] = M.ERR_SSL_INVALID_MAC
+        assert np.array_equal(r["status"], want), np.flatnonzero(r["status"] != want)[:10]
+        ok = np.ones(n, bool)
+        ok[tam] = False
+        assert (r["data_len"][ok] == content).all() and (r["type"][ok] == 23).all()
+        assert (r["data_offset"][ok] == 0).all()
+        Av, Cv = A.view(n, stride), C.view(n, stride)
+        okd = torch.from_numpy(ok).to(dev)
+        for lo in range(0, n, 1 << 18):
+            hi = lo + (1 << 18)
+            same = (Av[lo:hi, :content] == Cv[lo:hi, :content]).all(dim=1)
+            assert bool((same | ~okd[lo:hi]).all()), f"plaintext mismatch in rows {lo}..{hi}"
+        wiped = Cv[torch.from_numpy(tam).to(dev), :inner]
+        assert int(wiped.count_nonzero()) == 0, "a record that failed its tag kept output bytes"
+        del A, B, C
+    finally:
+        kt.close()
+
+
+@pytest.mark.parametrize("nkeys,rpk", [(2048, 64), (4096, 32), (4096, 16)], ids=["L2", "L4", "L8"])
+@pytest.mark.parametrize("cipher,ver", [(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3), (M.CIPHER_AES_128_GCM, M.VERSION_TLS1_2),
+                                        (M.CIPHER_CHACHA20_POLY1305, M.VERSION_TLS1_3)], ids=lambda x: str(x))
+def test_line_groups_unaligned_records_vs_openssl_evp(cipher, ver, nkeys, rpk):
+    """the line-grouped body of the small-record passes with record buffers at
+    arbitrary byte offsets (not 128-B lines) and ragged lengths, so group
+    boundaries fall anywhere in a record (the stream / DTLS layers' case)"""
+    _evp_case(cipher, ver, nkeys, nkeys * rpk, lens=(900, 1500), mean_bytes=1300, misalign=True)

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_lane_ops_match_their_lane_maps():
-    lib = _abi.load()
+    lib = _abi.test_library()     # self-test entry points: the test-hooks build
     out = np.zeros(17 * 64, dtype=np.uint32)
     f = lib.tlsrec__test_lane_ops
     f.argtypes = [ctypes.c_void_p]
