@@ -12,7 +12,7 @@ from ._abi import (CIPHER_AES_128_GCM, CIPHER_AES_256_GCM, CIPHER_CHACHA20_POLY1
                    CIPHER_ARIA_128_CCM, CIPHER_ARIA_192_CCM, CIPHER_ARIA_256_CCM,
                    CIPHER_CAMELLIA_128_GCM, CIPHER_CAMELLIA_192_GCM, CIPHER_CAMELLIA_256_GCM,
                    CIPHER_CAMELLIA_128_CCM, CIPHER_CAMELLIA_192_CCM, CIPHER_CAMELLIA_256_CCM,
-                   ERR_SSL_BAD_INPUT_DATA, ERR_SSL_BUFFER_TOO_SMALL, ERR_SSL_FEATURE_UNAVAILABLE,
+                   ERR_SSL_BAD_INPUT_DATA, ERR_SSL_BUFFER_TOO_SMALL, ERR_SSL_FEATURE_UNAVAILABLE, ERR_SSL_ALLOC_FAILED,
                    ERR_SSL_HW_ACCEL_FAILED, ERR_SSL_INTERNAL_ERROR, ERR_SSL_INVALID_MAC,
                    ERR_SSL_INVALID_RECORD, ERR_SSL_UNEXPECTED_CID, MSG_APPLICATION_DATA, MSG_CID,
                    CID_LEN_MAX, VERSION_TLS1_2, VERSION_TLS1_3, ERR_SSL_COUNTER_WRAPPING,

@@ -301,41 +301,47 @@ struct ScratchEntry {
 static pthread_mutex_t g_scratch_mu = PTHREAD_MUTEX_INITIALIZER;
 static ScratchEntry *g_scratch = nullptr;
 
-/* hipStreamPerThread entries belong to their thread: freed when it exits, so
- * a server whose connections come and go on short-lived threads does not
- * accumulate device memory */
+/* hipStreamPerThread entries belong to their thread: when it exits they are
+ * marked orphaned, and the next acquire frees them, so a server whose
+ * connections come and go on short-lived threads does not accumulate device
+ * memory.  The exit hook itself makes no HIP call: it runs after
+ * the HIP runtime's own thread-local state is gone.  hipFree waits for the
+ * device, so work the dead thread left on its stream has finished by then. */
+static const uintptr_t SCRATCH_ORPHAN = 1;     /* never a pthread_t of a live thread */
 static pthread_key_t g_scratch_key;
 static pthread_once_t g_scratch_once = PTHREAD_ONCE_INIT;
+static volatile int g_scratch_orphans = 0;
 
 static void scratch_thread_exit(void *)
 {
     const uintptr_t me = (uintptr_t) pthread_self();
-    ScratchEntry *mine = nullptr;
     pthread_mutex_lock(&g_scratch_mu);
+    for (ScratchEntry *e = g_scratch; e; e = e->next)
+        if (e->thread == me) {
+            e->thread = SCRATCH_ORPHAN;
+            g_scratch_orphans++;
+        }
+    pthread_mutex_unlock(&g_scratch_mu);
+}
+
+static void scratch_key_init(void) { pthread_key_create(&g_scratch_key, scratch_thread_exit); }
+
+/* with g_scratch_mu held */
+static void scratch_reclaim_locked(void)
+{
     for (ScratchEntry **pp = &g_scratch; *pp;) {
         ScratchEntry *e = *pp;
-        if (e->thread == me) {
+        if (e->thread == SCRATCH_ORPHAN) {
             *pp = e->next;
-            e->next = mine;
-            mine = e;
+            if (e->mem) hipFree(e->mem);
+            pthread_mutex_destroy(&e->mu);
+            free(e);
+            g_scratch_orphans--;
         } else {
             pp = &e->next;
         }
     }
-    pthread_mutex_unlock(&g_scratch_mu);
-    while (mine) {
-        ScratchEntry *nx = mine->next;
-        if (mine->mem) {
-            hipStreamSynchronize(hipStreamPerThread);    /* this thread's own stream */
-            hipFree(mine->mem);
-        }
-        pthread_mutex_destroy(&mine->mu);
-        free(mine);
-        mine = nx;
-    }
 }
-
-static void scratch_key_init(void) { pthread_key_create(&g_scratch_key, scratch_thread_exit); }
 
 extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, tlsrec_scratch_lease *lease)
 {
@@ -347,6 +353,7 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
      * stream is one queue for every thread and needs nothing) */
     const uintptr_t thr = st == hipStreamPerThread ? (uintptr_t) pthread_self() : 0;
     pthread_mutex_lock(&g_scratch_mu);
+    if (g_scratch_orphans) scratch_reclaim_locked();
     ScratchEntry *e = g_scratch;
     while (e && !(e->device == dev && e->stream == st && e->thread == thr && e->kind == kind)) e = e->next;
     if (!e) {
@@ -494,6 +501,9 @@ extern "C" void tlsrec__test_server_shadow(void *dev, size_t bytes)
 static constexpr uint32_t g_test_skip = 0xffffffffu;
 #endif
 
+extern "C" void tlsrec__server_yield(void);
+extern "C" void tlsrec__server_note_batch(hipStream_t stream);
+
 /* Launch options of one batch:
  *   only_mask  launch only these ciphers' kernels (1 << TLSREC_CIPHER_*; the
  *              single-record engine knows its records' ciphers), 0 = every
@@ -532,6 +542,8 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
      * before the AEAD kernels run (the guard kernel, or the bucket count
      * kernel), so a record that no kernel reaches fails closed -- the
      * reference's auth_done check, ssl_msg.c:1260 / :1804. */
+    /* batch work takes the CUs the record server holds (server.hip) */
+    if (!opt.coalesced) tlsrec__server_yield();
     BucketScratch bs;
     const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced;
     if (identity) {
@@ -731,6 +743,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     tlsrec__scratch_release(&bs.lease);
+    if (!opt.coalesced) tlsrec__server_note_batch(st);
     return rc;
 }
 

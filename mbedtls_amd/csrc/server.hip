@@ -39,10 +39,23 @@
  *
  * Termination: a server grid lives `life` ticks of the device wall clock
  * (TLSREC_SERVER_MS, default 20 ms) and at most `max_iter` polls, and leaves
- * early on the set's stop word (process exit).  The host submits to a grid
- * only inside its window minus a margin and launches the next grid on the
- * other slot set when the window closes; a request the grid did not take
- * (its kernel has ended) is withdrawn and runs on the launch path.
+ * early on the set's stop word (process exit, or batch work arriving: below)
+ * or when no request of the set was served for `idle` ticks
+ * (TLSREC_SERVER_IDLE_MS, default 1 ms), so a hipDeviceSynchronize after the
+ * last single-record call waits about that long, not a whole window.  The
+ * host submits to a grid only inside its window minus a margin and launches
+ * the next grid on the other slot set when the window closes; a request the
+ * grid did not take (its kernel has ended) is withdrawn and runs on the
+ * launch path.
+ *
+ * Yielding to batch work (r04): the grid holds 64 CUs (89 KiB of LDS each,
+ * so no 128 KiB batch workgroup fits beside it).  Every batch launch outside
+ * the single-record engine (tlsrec_batch_*, the stream / DTLS layers, the
+ * host pipeline) calls tlsrec__server_yield before its kernels -- the live
+ * grids get their stop word -- and tlsrec__server_note_batch after them,
+ * which records an event on the batch's stream.  No grid is launched while
+ * that event is pending; single-record calls meanwhile take the coalescing
+ * launch path, whose kernels queue with the batch like any other work.
  */
 #include <hip/hip_runtime.h>
 #include <atomic>
@@ -732,7 +745,8 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
  * per CU): the compiler is told to schedule for one wave per EU -- all
  * lookups of an AES round in flight together. */
 __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tlsrec_server_kernel(
-    SrvReq *reqs, const uint32_t *stop, uint64_t life_ticks, uint32_t max_iter, uint32_t flags)
+    SrvReq *reqs, const uint32_t *stop, uint64_t life_ticks, uint32_t max_iter, uint32_t flags, uint64_t *last_active,
+    uint64_t idle_ticks)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SRV_LDS];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -764,7 +778,17 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
                                                  stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0) {
                     v = 2;
                 } else {
-                    v = (uint64_t) (wall_clock64() - t0) > life_ticks ? 2u : 0u;
+                    const uint64_t now = wall_clock64();
+                    v = (uint64_t) (now - t0) > life_ticks ? 2u : 0u;
+                    if ((it & 15) == 8) {
+                        /* the set's last served request, any workgroup: all
+                         * of the grid leaves together once it is idle_ticks old */
+                        uint64_t la = __hip_atomic_load(last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        la = (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) la) |
+                             (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (la >> 32)) << 32;
+                        const uint64_t since = la > t0 ? la : t0;
+                        if (now - since > idle_ticks) v = 2u;
+                    }
                 }
             }
             if (lane == 0) {
@@ -798,6 +822,7 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                 }
                 __hip_atomic_store(&rq->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(last_active, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             served = seq;
             idle = 0;
@@ -835,6 +860,8 @@ namespace {
 struct SrvSet {
     SrvReq *h = nullptr, *d = nullptr;
     uint32_t *stop_h = nullptr, *stop_d = nullptr;
+    uint64_t *last_active = nullptr;  /* device: wall clock of the set's last served request */
+    uint64_t t_last = 0;              /* host: time of the last submit to this grid */
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
     bool launched = false;
@@ -854,7 +881,12 @@ int g_trace = 0;                  /* TLSREC_SERVER_TRACE=1: device phase times, 
 uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr_gcm = 0, g_tr_cyc = 0, g_tr_a1 = 0,
          g_tr_b1 = 0;
 double g_tick_ns = 10.0;
-uint64_t g_submit_ns = 0, g_life_ticks = 0;
+uint64_t g_submit_ns = 0, g_life_ticks = 0, g_idle_ticks = 0, g_idle_ns = 0;
+/* batch work (tlsrec__server_yield / _note_batch): no grid while it is pending */
+int g_yield = 1;                  /* TLSREC_SERVER_YIELD=0: the server ignores batch work */
+hipEvent_t g_batch_ev = nullptr;
+bool g_batch_pending = false;
+std::atomic<uint64_t> g_yields{0};
 uint32_t g_max_iter = 0;
 std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
 
@@ -906,6 +938,13 @@ int srv_setup_locked()
         hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
         return g_state;
     g_life_ticks = (uint64_t) (ms * khz);
+    double idle_ms = 1.0;
+    if (const char *m = getenv("TLSREC_SERVER_IDLE_MS")) idle_ms = atof(m);
+    if (!(idle_ms >= 0.05)) idle_ms = 0.05;
+    if (idle_ms > ms) idle_ms = ms;
+    g_idle_ticks = (uint64_t) (idle_ms * khz);
+    g_idle_ns = (uint64_t) (idle_ms * 1e6);
+    if (const char *y = getenv("TLSREC_SERVER_YIELD")) g_yield = strcmp(y, "0") != 0;
     g_tick_ns = 1e6 / khz;
     g_max_iter = (uint32_t) (ms * 10000.0);          /* backstop: a poll (a PCIe read + s_sleep) is > 0.1 us */
     const double margin = ms * 0.1 > 1.0 ? ms * 0.1 : 1.0;
@@ -918,13 +957,15 @@ int srv_setup_locked()
             hipHostMalloc((void **) &S.stop_h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer(&sd, S.stop_h, 0) != hipSuccess ||
             hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc((void **) &S.last_active, 64) != hipSuccess)
             return g_state;
         memset(S.h, 0, sizeof(SrvReq) * SRV_SLOTS);
         memset(S.stop_h, 0, 64);
         S.d = (SrvReq *) hd;
         S.stop_d = (uint32_t *) sd;
     }
+    if (hipEventCreateWithFlags(&g_batch_ev, hipEventDisableTiming) != hipSuccess) return g_state;
     atexit(srv_shutdown);
     g_state = 1;
     return g_state;
@@ -937,14 +978,29 @@ bool kernel_done(SrvSet &S) { return !S.launched || hipEventQuery(S.ev) != hipEr
 SrvSet *srv_current_locked(uint64_t now)
 {
     SrvSet *S = &g_set[g_cur];
-    if (S->launched && now - S->t_launch < g_submit_ns) return S;
+    if (S->launched && now - S->t_launch < g_submit_ns) {
+        /* a grid idle for half its idle limit may have left: ask its event */
+        if (now - S->t_last < g_idle_ns / 2 || !kernel_done(*S)) return S;
+        S->t_launch = 0;              /* ended early: never submit to it again */
+    }
+    /* batch work pending on the device: the launch path, no grid beside it */
+    if (g_batch_pending) {
+        const hipError_t q = hipEventQuery(g_batch_ev);
+        if (q == hipErrorNotReady) return nullptr;
+        g_batch_pending = false;
+    }
     SrvSet *N = &g_set[g_cur ^ 1];
     /* the other set must be drained: its grid ended, no host thread in it */
     if (N->nbusy != 0 || !kernel_done(*N)) return nullptr;
     __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
     (void) hipGetLastError();         /* an earlier call's status (hipEventQuery's NotReady) is not the launch's */
+    if (hipMemsetAsync(N->last_active, 0, 8, N->st) != hipSuccess) {
+        g_state = -1;
+        return nullptr;
+    }
     hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d,
-                       (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter, (uint32_t) g_trace);
+                       (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter, (uint32_t) g_trace, N->last_active,
+                       g_idle_ticks);
     const hipError_t le = hipGetLastError();
     if (le != hipSuccess || hipEventRecord(N->ev, N->st) != hipSuccess) {
         if (g_debug) fprintf(stderr, "tlsrec server: launch failed: %s\n", hipGetErrorString(le));
@@ -953,6 +1009,7 @@ SrvSet *srv_current_locked(uint64_t now)
     }
     N->launched = true;
     N->t_launch = now;
+    N->t_last = now;
     g_cur ^= 1;
     g_launches++;
     return N;
@@ -996,6 +1053,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     }
     S->busy[i] = 1;
     S->nbusy++;
+    S->t_last = now_ns();
     const uint32_t seq = ++S->seq[i];
     pthread_mutex_unlock(&g_mu);
 
@@ -1063,6 +1121,39 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     pthread_mutex_unlock(&g_mu);
     return rc;
 }
+
+/* Batch work is about to be launched (engine.hip batch(), outside the
+ * single-record engine): the live grids leave (stop word) and none is
+ * submitted to again.  Cheap when no server was ever set up. */
+extern "C" void tlsrec__server_yield(void)
+{
+    if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return;
+    pthread_mutex_lock(&g_mu);
+    for (auto &S : g_set)
+        if (S.launched && S.t_launch != 0) {
+            __atomic_store_n(S.stop_h, 1u, __ATOMIC_RELEASE);
+            S.t_launch = 0;
+            g_yields++;
+        }
+    pthread_mutex_unlock(&g_mu);
+}
+
+/* ... and has been launched on `stream`: no grid until it has finished */
+extern "C" void tlsrec__server_note_batch(hipStream_t stream)
+{
+    if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void) hipGetLastError();
+        return;                       /* a graph being captured: nothing runs yet */
+    }
+    pthread_mutex_lock(&g_mu);
+    if (hipEventRecord(g_batch_ev, stream) == hipSuccess) g_batch_pending = true;
+    else (void) hipGetLastError();
+    pthread_mutex_unlock(&g_mu);
+}
+
+extern "C" uint64_t tlsrec__server_yields(void) { return g_yields.load(); }
 
 /* tests: route single-record calls through the server (1) or never (0) */
 extern "C" void tlsrec__server_enable(int on) { g_enabled.store(on ? 1 : 0); }
