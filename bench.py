@@ -95,6 +95,9 @@ def parse():
                     help="use the process group even at WORLD_SIZE=1 (rehearses the RCCL path on one GPU)")
     ap.add_argument("--e2e-records", type=int, default=0, help="records of the end-to-end leg (0 = ~2 GiB worth)")
     ap.add_argument("--verify", type=int, default=64, help="records spot-checked against the oracle")
+    ap.add_argument("--key-order", choices=["round-robin", "contiguous"], default="round-robin",
+                    help="record i under key i %% keys (default, SURVEY 8(d)-4) or i // (records / keys) "
+                         "(diagnostic: a key's descriptors adjacent in memory)")
     return ap.parse_args()
 
 
@@ -245,7 +248,10 @@ def main():
     recs["data_len"] = content
     # records round-robin over keys: neighbours never share a
     # key; the engine's bucket pass groups them by key on the device
-    recs["slot"] = (np.arange(n, dtype=np.uint64) % nkeys).astype(np.uint32)
+    if args.key_order == "contiguous":
+        recs["slot"] = (np.arange(n, dtype=np.uint64) * nkeys // n).astype(np.uint32)
+    else:
+        recs["slot"] = (np.arange(n, dtype=np.uint64) % nkeys).astype(np.uint32)
     seq = np.arange(shard0, shard0 + n, dtype=np.uint64)
     recs["ctr"] = M.seq_bytes(seq)
     recs["type"] = 23

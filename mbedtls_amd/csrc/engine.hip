@@ -258,9 +258,12 @@ static uint32_t gcm_tm(bool pair)
      * in the 8-wave passes); bit 2: the AAD fold and the two final multiplies
      * by H as a value too (default on for the paired passes, same-box: c4s
      * 720 -> 742, k4 549 -> 558, 64 K keys x 16 x 1.4 KiB 362 -> 377 GiB/s:
-     * the key's 8 KiB H^1 table in global memory cost 32 lines per multiply) */
+     * the key's 8 KiB H^1 table in global memory cost 32 lines per multiply);
+     * bit 3 (r04, default on for every wave pass): lane powers -- AAD and the
+     * length block in the lane layout, one multiply by H^(L-q) per lane and a
+     * lane XOR replace the fold, the tree and the final multiplies */
     const char *e = getenv("TLSREC_GCM_TREEMUL");
-    return e ? (uint32_t) atoi(e) & 7u : (pair ? 7u : 1u);
+    return e ? (uint32_t) atoi(e) & 15u : (pair ? 15u : 9u);
 }
 
 /* paired wave passes (16 waves, two per key table) for small records of many
@@ -1057,7 +1060,6 @@ static int engine_queue(uint32_t cipher, int dec)
 
 struct EnginePage {
     tlsrec_keytab *kt;
-    uint4 *d_hpw;                        /* H^1 .. H^64 per GCM slot (the record server's closing powers) */
     uint8_t used[ENGINE_PAGE_SLOTS];
     uint8_t cid[ENGINE_PAGE_SLOTS];      /* the slot has a DTLS connection ID (the record server takes none) */
     uint32_t nused;
@@ -1134,10 +1136,6 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
             } else {
                 EnginePage &N = g_pages[pg];
                 r = tlsrec_keytab_create(&N.kt, ENGINE_PAGE_SLOTS);
-                if (r == 0 && hipMalloc((void **) &N.d_hpw, sizeof(uint4) * 64 * ENGINE_PAGE_SLOTS) != hipSuccess) {
-                    N.d_hpw = NULL;
-                    r = TLSREC_ERR_SSL_ALLOC_FAILED;
-                }
                 for (int q = 0; r == 0 && q < ENGINE_QUEUES; q++)
                     if (!(N.co[q] = combiner_new())) r = TLSREC_ERR_SSL_ALLOC_FAILED;
                 if (r != 0) {
@@ -1146,8 +1144,6 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
                         combiner_free(N.co[q]);
                         N.co[q] = NULL;
                     }
-                    if (N.d_hpw) hipFree(N.d_hpw);
-                    N.d_hpw = NULL;
                     if (N.kt) tlsrec_keytab_free(N.kt);
                     N.kt = NULL;
                 }
@@ -1160,10 +1156,6 @@ extern "C" int tlsrec__engine_slot_alloc(const tlsrec_key_material *km)
         for (int i = 0; i < ENGINE_PAGE_SLOTS; i++)
             if (!P.used[i]) { slot = i; break; }
         r = tlsrec_keytab_load(P.kt, (uint32_t) slot, 1, km, 0, g_load);
-        if (r == 0 && tlsrec_cipher_is_gcm(km->cipher) &&
-            tlsrec__launch_srv_hpow(P.kt->d_ghtab + (size_t) slot * KEY_TABLE_WORDS, P.d_hpw + (size_t) slot * 64,
-                                    g_load) != hipSuccess)
-            r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0 && hipStreamSynchronize(g_load) != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) {
             P.used[slot] = 1;
@@ -1188,8 +1180,7 @@ extern "C" void tlsrec__engine_slot_free(int slot)
         hipMemsetAsync(kt->d_slots + i, 0, sizeof(SlotState), g_load);
         hipMemsetAsync(kt->d_cipher + i, 0, 1, g_load);
         hipMemsetAsync(kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS, 0, sizeof(uint4) * KEY_TABLE_WORDS, g_load);
-        /* the record server's H^1..H^64 of the slot (key-derived, like H) */
-        hipMemsetAsync(P->d_hpw + (size_t) i * 64, 0, sizeof(uint4) * 64, g_load);
+        /* (the GHASH tables end with H^1..H^64, the record server's closing powers) */
         hipStreamSynchronize(g_load);
         kt->h_cipher[i] = 0;
         kt->nloaded--;
@@ -1211,7 +1202,7 @@ extern "C" int tlsrec__test_engine_slot_dump(int slot, void *state, void *ghtab,
     int r = kt ? 0 : TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (!r && (hipMemcpy(state, kt->d_slots + i, sizeof(SlotState), hipMemcpyDeviceToHost) != hipSuccess ||
                hipMemcpy(ghtab, kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS, 1024, hipMemcpyDeviceToHost) != hipSuccess ||
-               hipMemcpy(hpw, g_pages[slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) i * 64, 1024,
+               hipMemcpy(hpw, kt->d_ghtab + (size_t) i * KEY_TABLE_WORDS + KEY_HPOW_OFF, 1024,
                          hipMemcpyDeviceToHost) != hipSuccess))
         r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     pthread_mutex_unlock(&g_mu);
@@ -1374,12 +1365,12 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
         d.slot = idx;
         const void *p_state = kt->d_slots + idx;
         const void *p_ghtab = kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS;
-        const void *p_hpw = g_pages[rec->slot / ENGINE_PAGE_SLOTS].d_hpw + (size_t) idx * 64;
+        const void *p_hpw = kt->d_ghtab + (size_t) idx * KEY_TABLE_WORDS + KEY_HPOW_OFF;
 #ifdef TLSREC_TEST_HOOKS
         if (g_test_shadow) {
             /* copies at the first address of the test's buffer whose low word
              * has bit 31 set, all three inside that half of the 4 GiB window */
-            const size_t sz[3] = { sizeof(SlotState), sizeof(uint4) * KEY_TABLE_WORDS, sizeof(uint4) * 64 };
+            const size_t sz[3] = { sizeof(SlotState), sizeof(uint4) * KEY_TABLE_WORDS, 0 };
             const size_t tot = sz[0] + sz[1] + sz[2];
             const uintptr_t b0 = (uintptr_t) g_test_shadow, end = b0 + g_test_shadow_bytes;
             uintptr_t at = (b0 + 255) & ~(uintptr_t) 255;
@@ -1399,7 +1390,7 @@ extern "C" int tlsrec__engine_run(int dec, const tlsrec_batch_rec *rec, unsigned
             if (hipStreamSynchronize(g_load) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
             p_state = dsts[0];
             p_ghtab = dsts[1];
-            p_hpw = dsts[2];
+            p_hpw = (const uint4 *) dsts[1] + KEY_HPOW_OFF;    /* the powers inside the copied tables */
         }
 #endif
         const int r = tlsrec__server_run(dec, cipher, tlsrec_cipher_nr((int) cipher), &d, p_state, p_ghtab, p_hpw,

@@ -336,6 +336,16 @@ __global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, 
     }
     __syncthreads();
     uint4 *out = ghtab + (size_t) slot * KEY_TABLE_WORDS;
+    /* H^1 .. H^64 as values: lane t multiplies the powers H^(2^b) of the set
+     * bits b of t + 1 (the exponent is public, the products masked) */
+    if (tid < KEY_HPOW_N) {
+        const uint32_t e = (uint32_t) tid + 1;
+        const int b0 = __builtin_ctz(e);
+        G128 x = pw[b0];
+        for (int b = b0 + 1; b < KEY_TABLES; b++)
+            if ((e >> b) & 1) x = g_mul_base(base[b], x);
+        out[KEY_HPOW_OFF + tid] = g_to_words(x);
+    }
     for (int e = tid; e < KEY_TABLES * 32 * 16; e += 256) {
         const int p = e >> 9, k = (e >> 4) & 31, nib = e & 15;
         uint4 acc = make_uint4(0, 0, 0, 0);

@@ -31,7 +31,7 @@
  *        C_m, LEN (j = 0 the AAD, whose counter block J0 gives E_K(J0)), each
  *        C block's keystream from the T-tables, a Horner chain per lane with
  *        H^64 (the key's 4-bit table staged to LDS), then Y_q * H^(n - j_last)
- *        (H^1 .. H^64 precomputed per key slot: tlsrec_srv_hpow_kernel) and an
+ *        (H^1 .. H^64 precomputed per key slot by the key setup, KEY_HPOW_OFF) and an
  *        XOR over the 64 lanes by DPP / permlane.
  *   ChaCha20-Poly1305: lane q makes ChaCha20 block q (+ 64 k), block 0 being
  *        the one-time Poly1305 key; Poly1305 runs the same lane-Horner form
@@ -835,23 +835,6 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
-/* H^1 .. H^64 of one GCM key slot, from its 4-bit tables H^(2^b): lane q
- * multiplies the identity by H^(2^b) for the set bits b of q + 1. */
-__global__ __launch_bounds__(64) void tlsrec_srv_hpow_kernel(const uint4 *ghtab, uint4 *out)
-{
-    const uint8_t *g = reinterpret_cast<const uint8_t *>(ghtab);
-    const uint32_t e = threadIdx.x + 1;
-    uint4 x = make_uint4(0x80u, 0, 0, 0);                /* 1: the GCM string 80 00 .. 00 */
-    if (e & 1) x = gmul<0>(g, x);
-    if (e & 2) x = gmul<1>(g, x);
-    if (e & 4) x = gmul<2>(g, x);
-    if (e & 8) x = gmul<3>(g, x);
-    if (e & 16) x = gmul<4>(g, x);
-    if (e & 32) x = gmul<5>(g, x);
-    if (e & 64) x = gmul<6>(g, x);
-    out[threadIdx.x] = x;
-}
-
 /* ======================================================================
  * Host side
  * ==================================================================== */
@@ -887,6 +870,9 @@ int g_yield = 1;                  /* TLSREC_SERVER_YIELD=0: the server ignores b
 hipEvent_t g_batch_ev = nullptr;
 bool g_batch_pending = false;
 std::atomic<uint64_t> g_yields{0};
+/* why a call took the launch path: batch work pending, the other set not
+ * drained, the grid gone before it took the request (tlsrec__server_why) */
+uint64_t g_why_batch = 0, g_why_drain = 0, g_why_withdrawn = 0, g_why_noslot = 0;
 uint32_t g_max_iter = 0;
 std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
 
@@ -986,18 +972,22 @@ SrvSet *srv_current_locked(uint64_t now)
     /* batch work pending on the device: the launch path, no grid beside it */
     if (g_batch_pending) {
         const hipError_t q = hipEventQuery(g_batch_ev);
-        if (q == hipErrorNotReady) return nullptr;
+        if (q == hipErrorNotReady) {
+            g_why_batch++;
+            return nullptr;
+        }
         g_batch_pending = false;
     }
     SrvSet *N = &g_set[g_cur ^ 1];
     /* the other set must be drained: its grid ended, no host thread in it */
-    if (N->nbusy != 0 || !kernel_done(*N)) return nullptr;
-    __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
-    (void) hipGetLastError();         /* an earlier call's status (hipEventQuery's NotReady) is not the launch's */
-    if (hipMemsetAsync(N->last_active, 0, 8, N->st) != hipSuccess) {
-        g_state = -1;
+    if (N->nbusy != 0 || !kernel_done(*N)) {
+        g_why_drain++;
         return nullptr;
     }
+    __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
+    (void) hipGetLastError();         /* an earlier call's status (hipEventQuery's NotReady) is not the launch's */
+    /* (last_active keeps the previous grid's last serve: older than the new
+     * grid's start, which the idle check takes instead) */
     hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d,
                        (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter, (uint32_t) g_trace, N->last_active,
                        g_idle_ticks);
@@ -1016,12 +1006,6 @@ SrvSet *srv_current_locked(uint64_t now)
 }
 
 } /* namespace */
-
-extern "C" hipError_t tlsrec__launch_srv_hpow(const uint4 *ghtab_slot, uint4 *out, hipStream_t st)
-{
-    hipLaunchKernelGGL(tlsrec_srv_hpow_kernel, dim3(1), dim3(64), 0, st, ghtab_slot, out);
-    return hipGetLastError();
-}
 
 /* Serve one record.  `plan` is the record's framing plan (tlsrec_frame.h, as
  * tlsrec_encrypt_buf / _decrypt_buf computed it; status 0).  Returns 0 with
@@ -1047,6 +1031,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
         for (int k = 0; k < SRV_SLOTS; k++)
             if (!S->busy[k]) { i = k; break; }
     if (i < 0) {
+        if (S) g_why_noslot++;
         pthread_mutex_unlock(&g_mu);
         g_fallback++;
         return 1;
@@ -1089,6 +1074,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
             if (g_debug) fprintf(stderr, "tlsrec server: grid ended (%s) before seq %u\n", hipGetErrorString(eq), seq);
             if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
             __atomic_store_n(&rq->done, seq, __ATOMIC_RELEASE);   /* withdraw: no later grid serves it */
+            __atomic_fetch_add(&g_why_withdrawn, 1, __ATOMIC_RELAXED);
             rc = 1;
             break;
         }
@@ -1154,6 +1140,18 @@ extern "C" void tlsrec__server_note_batch(hipStream_t stream)
 }
 
 extern "C" uint64_t tlsrec__server_yields(void) { return g_yields.load(); }
+
+/* diagnostics: launch-path fallbacks by reason -- batch work pending, the
+ * other slot set not drained, withdrawn (the grid ended first), no free slot */
+extern "C" void tlsrec__server_why(uint64_t out[4])
+{
+    pthread_mutex_lock(&g_mu);
+    out[0] = g_why_batch;
+    out[1] = g_why_drain;
+    out[2] = __atomic_load_n(&g_why_withdrawn, __ATOMIC_RELAXED);
+    out[3] = g_why_noslot;
+    pthread_mutex_unlock(&g_mu);
+}
 
 /* tests: route single-record calls through the server (1) or never (0) */
 extern "C" void tlsrec__server_enable(int on) { g_enabled.store(on ? 1 : 0); }

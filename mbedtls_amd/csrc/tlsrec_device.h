@@ -795,6 +795,10 @@ __device__ inline G128 g_mul(G128 x, G128 y)
     return z;
 }
 
+/* x * P with base[j] = P * x^j (words, tlsrec_keysetup_kernel's LDS
+ * base): the XOR of the base entries of x's set bits, masked, not branched */
+__device__ inline G128 g_mul_base(const uint4 *base, G128 x);
+
 __device__ __forceinline__ uint4 g_to_words(G128 v)
 {
     return make_uint4(bswap32((uint32_t) (v.hi >> 32)), bswap32((uint32_t) v.hi),
@@ -807,6 +811,18 @@ __device__ __forceinline__ G128 g_from_words(uint4 w)
     v.hi = ((uint64_t) bswap32(w.x) << 32) | bswap32(w.y);
     v.lo = ((uint64_t) bswap32(w.z) << 32) | bswap32(w.w);
     return v;
+}
+
+__device__ inline G128 g_mul_base(const uint4 *base, G128 x)
+{
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < 128; j++) {
+        const uint64_t bit = (j < 64) ? (x.hi >> (63 - j)) & 1 : (x.lo >> (127 - j)) & 1;
+        const uint32_t m = 0u - (uint32_t) bit;
+        const uint4 b = base[j];
+        acc.x ^= b.x & m; acc.y ^= b.y & m; acc.z ^= b.z & m; acc.w ^= b.w & m;
+    }
+    return g_from_words(acc);
 }
 
 /* ---------------- ChaCha20 (RFC 8439 2.3) ------------------------------ */

@@ -342,15 +342,26 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
             const uint32_t mm = m ? m : 1;
             constexpr uint32_t BL = (uint32_t) (B * L);
-            const uint32_t z = (BL - mm % BL) % BL;                    /* front padding */
-            const uint32_t J = jb.run ? (mm + z) / BL : 0;
+            /* Lane powers (wave passes, tm bit 3): the whole GHASH input A, C_1 ..
+             * C_m, LEN in the lane layout -- C_1 at position 0 (line-aligned, no
+             * front padding), LEN at position m, and A at position -1, i.e. the
+             * block lane L-1's chain holds before its first one (its Xp starts
+             * as A: no step, no multiply).  A lane's chain stops at the record's
+             * end, so lane q's Horner sum needs one multiply, by H^(d+1) with d
+             * = (m - q) mod L its last block's distance to LEN (the key's powers
+             * as values, KEY_HPOW_OFF), and an XOR over the record's lanes gives
+             * GHASH: no AAD fold, no lane tree, no final multiplies (8 sequential
+             * multiplies per record at L = 32 before, 4 at L = 2). */
+            const bool lp = WP && !CID && (a.tm & 8u);
+            const uint32_t z = lp ? 0u : (BL - mm % BL) % BL;           /* front padding: position of C_1 */
+            const uint32_t J = jb.run ? (lp ? (m + BL) / BL : (mm + z) / BL) : 0;
             const uint32_t Jmax = wave_max(J);
             /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
              * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
              * only the step with cc == 0 reads it. */
             uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + (PAIR ? wave * LY::FOLDN + g : wave * 64 + lane);
             /* the lane that holds block 0 (cc == 0) */
-            if (jb.run && (uint32_t) q == z % L) {
+            if (!lp && jb.run && (uint32_t) q == z % L) {
                 uint4 f = jb.aadw;
                 if (m) {
                     if constexpr (WP)   /* tm bit 2: by H as a value -- the key's H^1 table is 8 KiB of
@@ -365,6 +376,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * does not depend on step j's keystream, so its table reads share
              * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
             uint4 Z = make_uint4(0, 0, 0, 0), Xp = make_uint4(0, 0, 0, 0);
+            if (lp && jb.run && q == L - 1) Xp = jb.aadw;              /* A: position -1, lane L-1's chain */
             /* TLS 1.3 inner type: position + 1 of the last non-zero output block */
             uint32_t nzpos = 0;
             /* a readable 16-byte address for lanes with nothing to load */
@@ -425,8 +437,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                             X = DEC ? blk : o;
                             if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                         }
-                        if (live && cc == 0) X = xor4(X, *fold);
-                        if (live) { Z = Zn; Xp = X; }
+                        if (lp) {
+                            if (cc == (int32_t) m)
+                                X = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
+                            if (live && cc <= (int32_t) m) { Z = Zn; Xp = X; }    /* the chain ends at LEN */
+                        } else {
+                            if (live && cc == 0) X = xor4(X, *fold);
+                            if (live) { Z = Zn; Xp = X; }
+                        }
                     }
                 };
                 uint32_t j = 0;
@@ -509,6 +527,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                     steps(std::integral_constant<bool, false>());
             }
             uint4 Y = xor4(Z, Xp);
+            /* lane powers: this lane's H^(L - q), read while the tail runs */
+            uint4 hq = make_uint4(0, 0, 0, 0);
+            if (lp) hq = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (m + (uint32_t) (L - q)) % L];
             uint32_t nzkey = 0;
             if (DEC && jb.inner && nzpos) {
                 /* the lane's last non-zero plaintext block, as written above */
@@ -519,7 +540,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             /* L = 8 and 32 (the paired passes of DTLS / stream records, 16 per
              * key, and of k4) too: their tree read the key's H^1 .. H^16 tables
              * from HBM, 8 KiB each, for a handful of records per key */
-            if constexpr (WP && L >= 2 && L <= 32) {
+            if (lp) {
+                Y = group_xor4<L>(gf_mul_v(Y, hq));                  /* GHASH, in every lane of the record */
+            } else if constexpr (WP && L >= 2 && L <= 32) {
                 if (a.tm & (L == 16 ? 1u : 2u)) {
                     const SlotState &ss = a.slots[s];
                     uint4 h1;
@@ -536,7 +559,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             } else {
                 Y = gtree<L / 2>(gp, Y, lane, q);
             }
-            if (q == 0) {                                            /* the group leader's sum */
+            if (!lp && q == 0) {                                     /* the group leader's sum */
                 uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
                 if (WP && (a.tm & 4u)) {
                     Y = gf_mul_v(Y, h1v);                            /* T */

@@ -27,7 +27,12 @@ constexpr int KEY_TABLES = 7;                      /* H^1, H^2, ..., H^64 (4-bit
 constexpr int KEY_G5_POWER = 3;                     /* H^(2^3) */
 constexpr int KEY_G5_WORDS = 26 * 32;               /* uint4 entries (13 KiB) */
 constexpr int KEY_G5_OFF = KEY_TABLES * 512;        /* uint4 offset of the G5 table in a slot */
-constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512 + KEY_G5_WORDS;   /* uint4 entries per slot (69 KiB) */
+/* then H^1 .. H^64 as values (GCM-string words, 1 KiB): lane q of an L-lane
+ * record multiplies its Horner sum by H^(L-q) once (the GCM kernel's lane
+ * powers, GcmArgs::tm bit 3), and the record server's closing powers */
+constexpr int KEY_HPOW_OFF = KEY_G5_OFF + KEY_G5_WORDS;
+constexpr int KEY_HPOW_N = 64;
+constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512 + KEY_G5_WORDS + KEY_HPOW_N;   /* uint4 entries per slot (70 KiB) */
 
 constexpr int GCM_WAVES = 16;                       /* default waves per workgroup (one WG per CU) */
 /* The bucket pass counts ChaCha20-Poly1305 records (one class for every key:
@@ -79,7 +84,9 @@ struct GcmArgs {
     uint32_t cipher;          /* TLSREC_CIPHER_AES_128_GCM / _256_GCM / _192_GCM */
     uint32_t g5;              /* host-side launch choice: 5-bit GHASH Horner table (8-lane, 16-wave kernel) */
     uint32_t tm;              /* wave passes, table-free multiplies (tlsrec_clmul.h): bit 0 the 16-lane tree,
-                                 bit 1 the 2- / 4- / 8- / 32-lane tree, bit 2 the AAD fold and final multiplies */
+                                 bit 1 the 2- / 4- / 8- / 32-lane tree, bit 2 the AAD fold and final multiplies,
+                                 bit 3 lane powers: AAD and length block in the lane layout, one multiply by
+                                 H^(L-q) per lane and an XOR over the record's lanes instead of all of these */
     uint32_t skip;            /* test hook (tlsrec__test_skip_record): this record index is never reached */
 };
 
@@ -170,7 +177,6 @@ hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_
 size_t tlsrec__scan_scratch_bytes(uint32_t n);
 hipError_t tlsrec__exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *scratch, hipStream_t st);
 /* server.hip: H^1 .. H^64 of one GCM key slot (64 uint4), from its GHASH tables */
-hipError_t tlsrec__launch_srv_hpow(const uint4 *ghtab_slot, uint4 *out, hipStream_t st);
 /* every result of a batch to INTERNAL_ERROR before its AEAD kernels (fail closed, kernels.hip) */
 hipError_t tlsrec__launch_res_guard(tlsrec_batch_res *res, uint32_t n, hipStream_t st);
 }

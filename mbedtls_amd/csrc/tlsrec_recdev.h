@@ -212,6 +212,19 @@ __device__ __forceinline__ uint32_t group_or(uint32_t v)
     return group_reduce<L>(v, [](uint32_t a, uint32_t b) { return a | b; });
 }
 
+template <int L>
+__device__ __forceinline__ uint32_t group_xor(uint32_t v)
+{
+    return group_reduce<L>(v, [](uint32_t a, uint32_t b) { return a ^ b; });
+}
+
+/* every lane of an aligned group of L lanes gets the XOR of the group's values */
+template <int L>
+__device__ __forceinline__ uint4 group_xor4(uint4 v)
+{
+    return make_uint4(group_xor<L>(v.x), group_xor<L>(v.y), group_xor<L>(v.z), group_xor<L>(v.w));
+}
+
 __device__ __forceinline__ void zero_range(uint8_t *dst, uint32_t from, uint32_t to, int q, int L)
 {
     for (uint32_t i = from + (uint32_t) q; i < to; i += (uint32_t) L) dst[i] = 0;

@@ -38,7 +38,7 @@ if "--ceiling" in args:
     del args[k:k + 2]
 root, kern, records = args[0], args[1], int(args[2])
 out = {}
-for p in ("pmc_sq1", "pmc_sq2", "pmc_sq3", "pmc_fetch", "pmc_write"):
+for p in ("pmc_sq1", "pmc_sq2", "pmc_sq3", "pmc_fetch", "pmc_write", "pmc_rdreq"):
     if os.path.isdir(os.path.join(root, p)):
         out[p] = summarize(os.path.join(root, p), kern)
 sq1, sq2 = out["pmc_sq1"], out["pmc_sq2"]
@@ -61,6 +61,14 @@ if "pmc_sq3" in out:
 if "pmc_fetch" in out and "pmc_write" in out:
     d["hbm_bytes_per_record"] = (out["pmc_fetch"]["hbm_read_bytes_corrected"] +
                                  out["pmc_write"]["hbm_write_bytes"]) / records
+    d["hbm_read_bytes_per_record_fetch_x2"] = out["pmc_fetch"]["hbm_read_bytes_corrected"] / records
+    d["hbm_write_bytes_per_record"] = out["pmc_write"]["hbm_write_bytes"] / records
+if "pmc_rdreq" in out and "hbm_read_bytes_sized" in out["pmc_rdreq"] and "pmc_write" in out:
+    # L2->fabric reads by request size (32/64/128 B): the byte count that
+    # tools/probes/fetch_calib pins for every access shape (profiles/r04a)
+    d["hbm_read_bytes_per_record_sized"] = out["pmc_rdreq"]["hbm_read_bytes_sized"] / records
+    d["hbm_bytes_per_record_sized"] = (out["pmc_rdreq"]["hbm_read_bytes_sized"] +
+                                       out["pmc_write"]["hbm_write_bytes"]) / records
 out["derived"] = d
 print(json.dumps(out, indent=1))
 if ceil_path:

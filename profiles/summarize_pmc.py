@@ -30,6 +30,11 @@ def summarize(root, pattern):
         out["hbm_read_bytes_corrected"] = out["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in out:
         out["hbm_write_bytes"] = out["WRITE_SIZE"] * 1024
+    # L2 -> fabric reads by request size (tools/probes/fetch_calib: the sized
+    # sum is the calibrated byte count for every access shape of the kernels)
+    sized = [out.get(f"TCC_EA0_RDREQ_{s}_sum") for s in ("32B", "64B", "128B")]
+    if None not in sized:
+        out["hbm_read_bytes_sized"] = 32 * sized[0] + 64 * sized[1] + 128 * sized[2]
     return out
 
 

@@ -230,13 +230,15 @@ def test_c2_full_size_tamper_1_in_1024_and_evp_sample():
         kt.close()
 
 
-@pytest.mark.parametrize("tm", ["7", "0"])
+@pytest.mark.parametrize("tm", ["15", "7", "0"])
 @pytest.mark.parametrize("nkeys,rpk,span,mean", [(2048, 64, (1000, 1500), 1300), (4096, 16, (1000, 1500), 1300),
                                                   (8192, 4, (12000, 16383), 14000)], ids=["L2", "L8", "L32"])
 def test_paired_wave_passes_tree_modes_vs_openssl_evp(monkeypatch, tm, nkeys, rpk, span, mean):
     """the wave passes' once-per-record multiplies (AAD fold, lane tree, the
-    two final multiplies) from the key's tables in global memory (TREEMUL=0)
-    and all of them table-free by H as a value (TREEMUL=7)"""
+    two final multiplies) from the key's tables in global memory (TREEMUL=0),
+    all of them table-free by H as a value (TREEMUL=7), and the r04 default,
+    lane powers (TREEMUL=15: AAD and length block in the lane layout, one
+    multiply by H^(L-q) per lane)"""
     monkeypatch.setenv("TLSREC_GCM_TREEMUL", tm)
     _evp_case(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, nkeys, nkeys * rpk, lens=span, mean_bytes=mean)
 

@@ -94,7 +94,10 @@ def test_served_records_match_oracle(cipher, ver):
     assert not errs, errs[:4]
     s1, f1, _ = _stats()
     calls = 2 * len(LENGTHS) * 3
-    assert f1 - f0 <= 2, "calls went back to the launch path"
+    why = (ctypes.c_uint64 * 4)()
+    _abi.load().tlsrec__server_why(why)
+    assert f1 - f0 <= 2, ("calls went back to the launch path (batch pending, set not drained, withdrawn, "
+                          f"no slot so far: {list(why)})")
     assert s1 - s0 >= calls // 2, "the record server did not serve these calls"
 
 

@@ -51,6 +51,12 @@ def main():
         for name, v in c.items():
             if name.startswith("TCC_"):
                 row[name] = v
+        n32, n64, n128 = (c.get(f"TCC_EA0_RDREQ_{s}_sum") for s in ("32B", "64B", "128B"))
+        if None not in (n32, n64, n128):
+            sized = 32 * n32 + 64 * n64 + 128 * n128
+            row["rdreq_sized_bytes"] = sized
+            if not k.startswith("calib_w_") and sized:
+                row["rdreq_sized_factor"] = round(e["line_bytes"] / sized, 4)
         out[k] = row
     print(json.dumps(out, indent=1))
 
