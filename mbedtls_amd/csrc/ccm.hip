@@ -104,7 +104,7 @@ __global__ __launch_bounds__(CCM_THREADS) void tlsrec_ccm_kernel(CcmArgs a)
         }
         const uint32_t taglen = km.taglen;
         uint32_t nw[3];
-        nonce_words<DEC>(p, d, a.in, nw);
+        nonce_words<DEC>(p, d, km, a.in, nw);
         const uint32_t n0 = nw[0], n1 = nw[1], n2 = nw[2];
         const uint8_t *src = a.in + d.buf_off + p.aead_pos;
         uint8_t *dst = a.out + d.buf_off + p.aead_pos;

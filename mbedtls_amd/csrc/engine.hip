@@ -251,7 +251,7 @@ static uint32_t gcm_g5(void)
  * instead of the key's H^8 / H^4 / H^2 / H^1 tables from HBM (24 KiB more per
  * key pass).  Same-box: k4 455 -> 461 GiB/s, stream 4 x 16 KiB per key
  * receive 424/429 -> 432/432.  TLSREC_GCM_TREEMUL=0 selects the tables. */
-static uint32_t gcm_tm(bool pair)
+static uint32_t gcm_tm(bool pair, bool wp)
 {
     /* bit 0: 16-lane wave passes (default on); bit 1: 2- and 4-lane ones
      * (default on for the paired passes: c4s 740 -> 750 GiB/s same-box; ±1 %
@@ -259,11 +259,16 @@ static uint32_t gcm_tm(bool pair)
      * by H as a value too (default on for the paired passes, same-box: c4s
      * 720 -> 742, k4 549 -> 558, 64 K keys x 16 x 1.4 KiB 362 -> 377 GiB/s:
      * the key's 8 KiB H^1 table in global memory cost 32 lines per multiply);
-     * bit 3 (r04, default on for every wave pass): lane powers -- AAD and the
-     * length block in the lane layout, one multiply by H^(L-q) per lane and a
-     * lane XOR replace the fold, the tree and the final multiplies */
+     * bit 3 (r04): lane powers -- AAD and the length block in the lane
+     * layout, one multiply by H^(d+1) per lane and a lane XOR replace the
+     * fold, the tree and the final multiplies (the key-pass kernels then
+     * stage only the Horner table).  Default on for the wave passes, whose
+     * tails were table-free multiplies (same box: k4 582 -> 636 GiB/s, DTLS
+     * 16 x 1.4 KiB +17 %); off for the 16-wave key passes, whose LDS-table
+     * tree is cheaper than a VALU multiply on an LDS-bound kernel (c2 712 vs
+     * 712-720, c2s 577 vs 545, c4 1034 vs 1032; profiles/r04h). */
     const char *e = getenv("TLSREC_GCM_TREEMUL");
-    return e ? (uint32_t) atoi(e) & 15u : (pair ? 15u : 9u);
+    return e ? (uint32_t) atoi(e) & 15u : (pair ? 15u : (wp ? 9u : 1u));
 }
 
 /* paired wave passes (16 waves, two per key table) for small records of many
@@ -272,6 +277,16 @@ static int gcm_pair_env(void)
 {
     const char *e = getenv("TLSREC_GCM_PAIR");
     return e ? atoi(e) : 1;
+}
+
+/* key-ordered descriptor copy for the GCM kernels (bucket scatter):
+ * TLSREC_GCM_SRECS=1.  Off by default: same box, k4 665 vs 665-666, c4s 836
+ * vs 840-843, c4 1032 vs 1035 GiB/s (profiles/r04h) -- the scattered 40-byte
+ * writes cost what the contiguous reads save. */
+static bool srecs_env(void)
+{
+    const char *e = getenv("TLSREC_GCM_SRECS");
+    return e && atoi(e) == 1;
 }
 
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */
@@ -429,6 +444,8 @@ struct BucketScratch {
     tlsrec_scratch_lease lease = { nullptr, nullptr };
     uint32_t *counts, *offs, *perm;
     uint2 *keyrank;
+    bool want_srecs = false;  /* GCM kernels will run: keep the descriptors in perm order too */
+    tlsrec_batch_rec *srecs = nullptr;
     void *scan_tmp;           /* tlsrec__exclusive_scan's block sums */
     size_t scan_bytes;
 };
@@ -443,7 +460,9 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     const size_t al = 256;
     const size_t szk = (nk * 4 + al - 1) / al * al, szp = ((size_t) n * 4 + al - 1) / al * al;
     const size_t szr = ((size_t) n * 8 + al - 1) / al * al;
-    const size_t total = 2 * szk + szp + szr + b.scan_bytes + al;
+    /* the descriptors in perm order for the GCM kernels (GcmArgs::srecs) */
+    const size_t szs = b.want_srecs ? ((size_t) n * sizeof(tlsrec_batch_rec) + al - 1) / al * al : 0;
+    const size_t total = 2 * szk + szp + szr + szs + b.scan_bytes + al;
     const int lr = tlsrec__scratch_acquire(st, 0, total, &b.lease);
     if (lr) return lr;
     uint8_t *m = (uint8_t *) b.lease.mem;
@@ -451,7 +470,8 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     b.offs = (uint32_t *) (m + szk);
     b.perm = (uint32_t *) (m + 2 * szk);
     b.keyrank = (uint2 *) (m + 2 * szk + szp);
-    b.scan_tmp = m + 2 * szk + szp + szr;
+    b.srecs = szs ? (tlsrec_batch_rec *) (m + 2 * szk + szp + szr) : nullptr;
+    b.scan_tmp = m + 2 * szk + szp + szr + szs;
     BucketArgs a;
     a.slots = kt->d_slots;
     a.cipher_of = kt->d_cipher;
@@ -464,6 +484,7 @@ static int bucket(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_
     a.keyrank = b.keyrank;
     a.nk = (uint32_t) nk;
     a.perm = b.perm;
+    a.srecs = b.srecs;
     if (tlsrec__launch_bucket_zero(&a, st) != hipSuccess ||
         tlsrec__launch_bucket_count(&a, st) != hipSuccess ||
         tlsrec__exclusive_scan(b.counts, b.offs, (uint32_t) nk, (uint32_t *) b.scan_tmp, st) != hipSuccess ||
@@ -552,6 +573,12 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     if (identity) {
         if (!prefilled && tlsrec__launch_res_guard(res, n, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else {
+        const uint32_t gcm_mask = (1u << TLSREC_CIPHER_AES_128_GCM) | (1u << TLSREC_CIPHER_AES_256_GCM) |
+                                  (1u << TLSREC_CIPHER_AES_192_GCM) | (1u << TLSREC_CIPHER_ARIA_128_GCM) |
+                                  (1u << TLSREC_CIPHER_ARIA_192_GCM) | (1u << TLSREC_CIPHER_ARIA_256_GCM) |
+                                  (1u << TLSREC_CIPHER_CAMELLIA_128_GCM) | (1u << TLSREC_CIPHER_CAMELLIA_192_GCM) |
+                                  (1u << TLSREC_CIPHER_CAMELLIA_256_GCM);
+        bs.want_srecs = (cmask & gcm_mask) != 0 && srecs_env();
         int r = bucket(kt, recs, res, n, st, bs);
         if (r) {
             tlsrec__scratch_release(&bs.lease);
@@ -592,6 +619,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.res = res;
         a.n = n;
         a.perm = identity ? nullptr : bs.perm;
+        a.srecs = identity ? nullptr : bs.srecs;
         a.lo = identity ? nullptr : bs.offs + (size_t) ci * cap;
         a.hi = identity ? nullptr : bs.offs + (size_t) (ci + 1) * cap;
         a.in = in;
@@ -659,7 +687,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         /* coalesced calls wait on the lane tree: from the key's tables (one
          * L2 round trip per level) rather than table-free (~1 700 dependent
          * VALU ticks per level) */
-        a.tm = opt.coalesced ? 0u : gcm_tm(pair);
+        a.tm = opt.coalesced ? 0u : gcm_tm(pair, wp);
         a.skip = skip;
         uint64_t per_wg = (uint64_t) waves * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
@@ -683,6 +711,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.res = res;
         a.n = n;
         a.perm = identity ? nullptr : bs.perm;
+        a.srecs = identity ? nullptr : bs.srecs;
         a.lo = identity ? nullptr : bs.offs + base;
         a.hi = identity ? nullptr : bs.offs + base + cap;
         a.in = in;

@@ -497,7 +497,13 @@ __global__ __launch_bounds__(256) void tlsrec_bucket_scatter_kernel(BucketArgs a
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     const uint2 kr = a.keyrank[i];
-    if (kr.x != 0xffffffffu) a.perm[a.offs[kr.x] + kr.y] = i;
+    if (kr.x != 0xffffffffu) {
+        const uint32_t p = a.offs[kr.x] + kr.y;
+        a.perm[p] = i;
+        /* the GCM classes' descriptors in perm order (not CCM, 3 cap.., or
+         * ChaCha, 4 cap..4 cap + CP_SPREAD: their kernels read recs[]) */
+        if (a.srecs && (kr.x < 3 * a.capacity || kr.x >= 4 * a.capacity + CP_SPREAD)) a.srecs[p] = a.recs[i];
+    }
 }
 
 /* ======================================================================
@@ -682,7 +688,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
                 __builtin_memcpy(kmm, &km, sizeof(kmm));    /* all but the key: the plan's inputs */
                 tlsrec_plan p;
                 make_plan<DEC, CID>(p, d, km, &a.slots[d.slot], a.in);
-                nonce_words<DEC>(p, d, a.in, nw);
+                nonce_words<DEC>(p, d, km, a.in, nw);
                 for (int i = 0; i < 8; i++) key[i] = ld_u32le(km.key + 4 * i);
             }
         }

@@ -1104,6 +1104,10 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     pthread_mutex_lock(&g_mu);
     S->busy[i] = 0;
     S->nbusy--;
+    /* the grid is gone: no later call may submit to it (each submit refreshes
+     * t_last, so without this the next calls would see a "recent" grid and
+     * skip the event query -- a streak of withdrawals) */
+    if (rc == 1) S->t_launch = 0;
     pthread_mutex_unlock(&g_mu);
     return rc;
 }

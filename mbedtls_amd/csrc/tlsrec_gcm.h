@@ -89,11 +89,11 @@ struct GcmJob {
     uint8_t *dst;
 
     template <bool DEC>
-    __device__ __forceinline__ void setup(const tlsrec_plan &p, const tlsrec_batch_rec &d, const uint8_t *in,
-                                          uint8_t *out)
+    __device__ __forceinline__ void setup(const tlsrec_plan &p, const tlsrec_batch_rec &d,
+                                          const tlsrec_key_material &km, const uint8_t *in, uint8_t *out)
     {
         uint32_t nw[3];
-        nonce_words<DEC>(p, d, in, nw);
+        nonce_words<DEC>(p, d, km, in, nw);
         nw0 = nw[0]; nw1 = nw[1]; nw2 = nw[2];
         aadw = aad_words(p);
         aad_len = p.aad_len;
@@ -203,15 +203,19 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
      * positions and its halves take them alternately, so both see the same
      * key runs */
     const int pr = wave & (W / 2 - 1), ph = wave / (W / 2);
-    /* pass membership: lane l tracks the record at chunk position k = l */
-    uint32_t my_slot = 0xffffffffu, my_rec = 0;
+    /* pass membership: lane l tracks the record at chunk position k = l;
+     * its descriptor is dsrc[my_d] -- the key-ordered copy the bucket pass
+     * wrote (a.srecs, contiguous per key), or recs[] itself */
+    const tlsrec_batch_rec *const dsrc = (a.perm && a.srecs) ? a.srecs + lo : a.recs;
+    uint32_t my_slot = 0xffffffffu, my_rec = 0, my_d = 0;
     {
         /* WP: a wave's positions are contiguous (its key runs stay together) */
         const uint64_t pos = PAIR ? wg_base + (uint64_t) pr * 2 * a.rpw + 2 * (uint64_t) lane + (uint64_t) ph
                              : WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
         if (lane < (int) a.rpw && pos < count) {
             my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
-            const uint32_t s = a.recs[my_rec].slot;
+            my_d = (a.perm && a.srecs) ? (uint32_t) pos : my_rec;
+            const uint32_t s = dsrc[my_d].slot;
             if (TLSREC_HOOK_SKIP(my_rec, a.skip)) {
                 /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
             } else if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
@@ -265,11 +269,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             s = __builtin_amdgcn_readfirstlane(*cur);
             if (s == 0xffffffffu) break;
             if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
-            /* stage the slot's GHASH tables and round keys */
+            /* stage the slot's GHASH tables and round keys -- with lane powers
+             * (tm bit 3) only the Horner multiplier's: the tree tables H^1 ..
+             * H^(L/2) are not read (G5: its 13 KiB table alone; 4-bit: H^L) */
             {
                 const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
                 uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
-                for (int i = tid; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
+                const int t0 = (!CID && (a.tm & 8u)) ? (G5 ? LY::NT : LY::NT - 1) : 0;
+                for (int i = tid + t0 * 512; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
                 if constexpr (G5) {
                     uint4 *d5 = reinterpret_cast<uint4 *>(lds + LY::HG5);
                     for (int i = tid; i < KEY_G5_WORDS; i += NTHR) d5[i] = src[KEY_G5_OFF + i];
@@ -294,10 +301,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             bool mine = my_slot == s;
             uint32_t nw[3] = { 0, 0, 0 };
             if (mine) {
-                const tlsrec_batch_rec d = a.recs[my_rec];
+                const tlsrec_batch_rec d = dsrc[my_d];
                 tlsrec_plan p;
                 make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
-                nonce_words<DEC>(p, d, a.in, nw);
+                nonce_words<DEC>(p, d, km, a.in, nw);
                 /* only this pass's records: with many keys of few records
                  * each, most of a wave's 64 positions belong to other passes
                  * (masked lanes issue no table reads) */
@@ -322,18 +329,19 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * each, the pass would otherwise walk all rpw positions */
             if (__ballot(active) == 0) continue;
             const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
+            const uint64_t didx = (uint32_t) __shfl((int) my_d, (int) slot_in_chunk & 63);
             /* Only what the AEAD loop needs stays live across it; the plan is
              * re-derived from the (cached) descriptor afterwards. */
             GcmJob jb;
             jb.run = false;
             if (active) {
-                const tlsrec_batch_rec d = a.recs[ridx];
+                const tlsrec_batch_rec d = dsrc[didx];
                 tlsrec_plan p;
                 make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
                 if (p.status != 0) {
                     if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
                 } else {
-                    jb.setup<DEC>(p, d, a.in, a.out);
+                    jb.setup<DEC>(p, d, km, a.in, a.out);
                     /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
                      * into the block the AAD fold multiplies by H below */
                     if (CID && p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
@@ -342,7 +350,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
             const uint32_t mm = m ? m : 1;
             constexpr uint32_t BL = (uint32_t) (B * L);
-            /* Lane powers (wave passes, tm bit 3): the whole GHASH input A, C_1 ..
+            /* Lane powers (tm bit 3; not with CIDs): the whole GHASH input A, C_1 ..
              * C_m, LEN in the lane layout -- C_1 at position 0 (line-aligned, no
              * front padding), LEN at position m, and A at position -1, i.e. the
              * block lane L-1's chain holds before its first one (its Xp starts
@@ -352,9 +360,12 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * as values, KEY_HPOW_OFF), and an XOR over the record's lanes gives
              * GHASH: no AAD fold, no lane tree, no final multiplies (8 sequential
              * multiplies per record at L = 32 before, 4 at L = 2). */
-            const bool lp = WP && !CID && (a.tm & 8u);
+            /* (m a multiple of BL: LEN would open a step of its own; lane 0
+             * takes it at the tail instead, Y_0 = Y_0 H^L + LEN, one multiply) */
+            const bool lp = !CID && (a.tm & 8u);
+            const bool lenx = lp && m % BL == 0;
             const uint32_t z = lp ? 0u : (BL - mm % BL) % BL;           /* front padding: position of C_1 */
-            const uint32_t J = jb.run ? (lp ? (m + BL) / BL : (mm + z) / BL) : 0;
+            const uint32_t J = jb.run ? (lp ? (lenx ? m / BL : (m + BL) / BL) : (mm + z) / BL) : 0;
             const uint32_t Jmax = wave_max(J);
             /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
              * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
@@ -528,8 +539,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             }
             uint4 Y = xor4(Z, Xp);
             /* lane powers: this lane's H^(L - q), read while the tail runs */
-            uint4 hq = make_uint4(0, 0, 0, 0);
+            uint4 hq = make_uint4(0, 0, 0, 0), hl = make_uint4(0, 0, 0, 0);
             if (lp) hq = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (m + (uint32_t) (L - q)) % L];
+            if (lenx && q == 0) hl = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1)];
             uint32_t nzkey = 0;
             if (DEC && jb.inner && nzpos) {
                 /* the lane's last non-zero plaintext block, as written above */
@@ -541,6 +553,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * key, and of k4) too: their tree read the key's H^1 .. H^16 tables
              * from HBM, 8 KiB each, for a handful of records per key */
             if (lp) {
+                if (__ballot(lenx && q == 0))                        /* LEN after a whole last step */
+                    if (lenx && q == 0)
+                        Y = xor4(gf_mul_v(Y, hl), make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8)));
                 Y = group_xor4<L>(gf_mul_v(Y, hq));                  /* GHASH, in every lane of the record */
             } else if constexpr (WP && L >= 2 && L <= 32) {
                 if (a.tm & (L == 16 ? 1u : 2u)) {
@@ -572,7 +587,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             if (!jb.run) continue;
             const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
             const uint4 tag = xor4(Y, ej0);
-            const tlsrec_batch_rec d = a.recs[ridx];
+            const tlsrec_batch_rec d = dsrc[didx];
             tlsrec_plan p;
             make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
             if (!DEC) {

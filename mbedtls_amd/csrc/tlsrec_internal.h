@@ -88,6 +88,9 @@ struct GcmArgs {
                                  bit 3 lane powers: AAD and length block in the lane layout, one multiply by
                                  H^(L-q) per lane and an XOR over the record's lanes instead of all of these */
     uint32_t skip;            /* test hook (tlsrec__test_skip_record): this record index is never reached */
+    const tlsrec_batch_rec *srecs;   /* with perm: the descriptors in perm order (srecs[p] = recs[perm[p]],
+                                        written by the bucket scatter), so a key pass reads its records'
+                                        descriptors from one contiguous run instead of a line per record */
 };
 
 struct CpArgs {
@@ -120,6 +123,7 @@ struct BucketArgs {
     uint2 *keyrank;           /* [n] each record's (key, rank within its key) from the count pass */
     uint32_t nk;
     uint32_t *perm;           /* [n] */
+    tlsrec_batch_rec *srecs;  /* [n] descriptors in perm order (GcmArgs::srecs), or NULL */
 };
 
 /* AES-CCM records (ccm.hip): one lane per record, key passes per wave. */

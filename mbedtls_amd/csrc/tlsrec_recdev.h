@@ -327,19 +327,30 @@ __device__ inline void finish_early(const tlsrec_plan &p, const tlsrec_batch_rec
     *res = r;
 }
 
+/* The record nonce as three little-endian words, ssl_build_record_nonce
+ * (ssl_msg.c:768-781): the fixed IV (12 bytes, or 4 for the TLS 1.2 GCM /
+ * CCM suites) XOR the sequence number in bytes 4..11 -- or, decrypting a
+ * record with an explicit nonce, the record's 8 bytes at data_offset
+ * (ssl_msg.c:1352-1365).  Built from the key material's words: the plan's
+ * byte form (tlsrec_frame.h tlsrec__nonce, through a pointer into km) kept
+ * the key material and the nonce bytes in scratch memory, 13 byte stores per
+ * call in the GCM kernels. */
 template <bool DEC>
-__device__ __forceinline__ void nonce_words(const tlsrec_plan &p, const tlsrec_batch_rec &d, const uint8_t *in,
-                                            uint32_t nw[3])
+__device__ __forceinline__ void nonce_words(const tlsrec_plan &p, const tlsrec_batch_rec &d,
+                                            const tlsrec_key_material &km, const uint8_t *in, uint32_t nw[3])
 {
-    uint8_t nonce[12];
-    for (int i = 0; i < 12; i++) nonce[i] = p.nonce[i];
+    uint32_t iv[3], ctr[2];
+    __builtin_memcpy(iv, km.iv, 12);
+    __builtin_memcpy(ctr, d.ctr, 8);
+    const bool full = km.fixed_ivlen == 12;
+    nw[0] = iv[0];
+    nw[1] = (full ? iv[1] : 0u) ^ ctr[0];
+    nw[2] = (full ? iv[2] : 0u) ^ ctr[1];
     if (DEC && p.explicit_iv) {   /* encrypt uses rec->ctr (ssl_msg.c:1012-1019) */
         const uint8_t *e = in + d.buf_off + d.data_offset;   /* ssl_msg.c:1360 dynamic_iv = data */
-        for (int i = 0; i < 8; i++) nonce[4 + i] = e[i];
+        nw[1] = ld_u32le(e);
+        nw[2] = ld_u32le(e + 4);
     }
-    nw[0] = ld_u32le(nonce);
-    nw[1] = ld_u32le(nonce + 4);
-    nw[2] = ld_u32le(nonce + 8);
 }
 
 __device__ __forceinline__ uint4 aad_words(const tlsrec_plan &p)

@@ -358,3 +358,23 @@ def test_line_groups_unaligned_records_vs_openssl_evp(cipher, ver, nkeys, rpk):
     arbitrary byte offsets (not 128-B lines) and ragged lengths, so group
     boundaries fall anywhere in a record (the stream / DTLS layers' case)"""
     _evp_case(cipher, ver, nkeys, nkeys * rpk, lens=(900, 1500), mean_bytes=1300, misalign=True)
+
+
+@pytest.mark.parametrize("nkeys,rpk,span,mean", [(2048, 64, (1000, 1500), 1300), (8192, 4, (12000, 16383), 14000),
+                                                  (64, 1024, (0, 4000), 0)], ids=["pairL2", "pairL32", "keypassL8"])
+def test_key_ordered_descriptors_vs_openssl_evp(monkeypatch, nkeys, rpk, span, mean):
+    """TLSREC_GCM_SRECS=1: the bucket pass also writes the GCM records'
+    descriptors in key order and the GCM kernels read them there (paired
+    passes and the 16-wave key passes)"""
+    monkeypatch.setenv("TLSREC_GCM_SRECS", "1")
+    _evp_case(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, nkeys, nkeys * rpk, lens=span, mean_bytes=mean)
+    _evp_case(M.CIPHER_AES_128_GCM, M.VERSION_TLS1_2, nkeys, nkeys * rpk, lens=span, mean_bytes=mean)
+
+
+@pytest.mark.parametrize("nkeys,n", [(1, 30_000), (64, 65_536)], ids=["1key_G5", "64keys_keypass"])
+@pytest.mark.parametrize("cipher,ver", CASES[:4], ids=lambda x: str(x))
+def test_key_pass_lane_powers_vs_openssl_evp(monkeypatch, cipher, ver, nkeys, n):
+    """TLSREC_GCM_TREEMUL=9: lane powers in the 16-wave key-pass kernels too
+    (off by default there), single key (the G5 kernel) and many keys"""
+    monkeypatch.setenv("TLSREC_GCM_TREEMUL", "9")
+    _evp_case(cipher, ver, nkeys, n)
