@@ -399,6 +399,10 @@ def main():
         e2e = end_to_end(M, kt, recs, arena, out_arena, n, stride, lead, head, content, wire, inner, direction,
                          args.e2e_records)
 
+    if world > 1 and args.config == "c2":
+        # BASELINE configs[4] (c5): the c2 shard on every rank, keys broadcast over RCCL
+        workload = (f"AES-256-GCM decrypt, {n * world} x 16 KiB TLS 1.3 records sharded across {world} MI355X "
+                    f"({n} per GPU), key broadcast over RCCL/xGMI (BASELINE c5: 8M records at N = 8)")
     out = {
         "metric": METRIC,
         "value": round(value, 3),

@@ -289,6 +289,15 @@ static bool srecs_env(void)
     return e && atoi(e) == 1;
 }
 
+/* lanes per record of the paired passes over small records (2, 4 or 8):
+ * measurement override of the records-per-key rule */
+static int gcm_pair_l_env(void)
+{
+    const char *e = getenv("TLSREC_GCM_PAIR_L");
+    const int v = e ? atoi(e) : 0;
+    return (v == 2 || v == 4 || v == 8) ? v : 0;
+}
+
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */
 static uint32_t gcm_lanes_env(void)
 {
@@ -672,6 +681,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0) {
             int Lp = 0;
             if (small) Lp = rpk >= 48 ? 2 : (rpk >= 24 ? 4 : 8);
+            if (small && gcm_pair_l_env()) Lp = gcm_pair_l_env();     /* measurement override */
             else if (avg_bytes > 4096 && rpk >= 4 && rpk < 12) Lp = rpk >= 8 ? 16 : 32;
             if (Lp && (uint64_t) n >= (uint64_t) cu * 16 * (uint64_t) (64 / Lp)) {
                 L = Lp;
