@@ -600,16 +600,6 @@ __device__ __forceinline__ P5 p_reduce(D5 d)
     return o;
 }
 
-__device__ __forceinline__ void chacha_block_kn(const uint32_t *kn, uint32_t counter, uint32_t out[16])
-{
-    uint32_t key[8], nw[3];
-#pragma unroll
-    for (int i = 0; i < 8; i++) key[i] = kn[i];
-#pragma unroll
-    for (int i = 0; i < 3; i++) nw[i] = kn[8 + i];
-    chacha_block(key, counter, nw, out);
-}
-
 /* Keystream exchange slot of (chunk lane c, 16-B group g) in a wave's 4 KiB
  * LDS row: the group rotates with c >> 1 so that the eight lanes of a
  * ds_write_b128 lane group hit 32 distinct banks. */
@@ -645,8 +635,13 @@ __device__ __forceinline__ uint32_t ks_half(uint32_t c, uint32_t g)
  * blocks before the end, and the record's sum is  sum_q acc_q r^(d_q)  (a
  * shuffle-add over the L lanes), then the length block and s.
  */
+/* 3 waves per SIMD (the L = 2 kernels; L >= 4 and CID are held to 2 by their
+ * LDS): the per-record first-column-round words take the VGPRs to 172-176,
+ * and at 2 waves the c3 shape lost what the 3 saved quarter rounds gain;
+ * capped at 168 the compiler spills 6-12 registers outside the step loop
+ * (same box: c3 1 224 -> 1 220, c3d 1 195 -> 1 204, 16 KiB 1 637 -> 1 677 GiB/s) */
 template <int L, bool DEC, bool CID = false>
-__global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
+__global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(3))) void tlsrec_chachapoly_kernel(CpArgs a)
 {
     constexpr int R = 64 / L;
     constexpr int LOGL = Log2<L>::v;
@@ -760,6 +755,16 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
                 }
             }
         }
+        /* the record's key stream: first column round, once per record (chacha_cc_make) */
+        uint32_t kcc[CHACHA_CC_WORDS];
+        {
+            uint32_t key[8], nw[3];
+#pragma unroll
+            for (int i = 0; i < 8; i++) key[i] = cr.key[i];
+#pragma unroll
+            for (int i = 0; i < 3; i++) nw[i] = cr.nonce[i];
+            chacha_cc_make(key, nw, kcc);
+        }
         const uint32_t aead_len = run ? p.aead_len : 0;
         const uint32_t B = (aead_len + 63) >> 6;              /* ChaCha20 blocks (64 B) */
         const uint32_t M = (aead_len + 15) >> 4;              /* Poly1305 C blocks (16 B) */
@@ -805,7 +810,7 @@ __global__ __launch_bounds__(CP_THREADS) void tlsrec_chachapoly_kernel(CpArgs a)
          * keystream of slot L*t + q */
         auto keystream = [&](uint32_t j, uint4 (&K)[4]) {
             uint32_t ks[16];
-            chacha_block_kn(cr.key, L * j - z + (uint32_t) q + 1u, ks);
+            chacha_block_cc<const uint32_t *>(cr.key, cr.nonce, kcc, L * j - z + (uint32_t) q + 1u, ks);
             asm volatile("" ::: "memory");   /* after the previous step's reads */
             if constexpr (SPLIT) {
 #pragma unroll
