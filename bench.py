@@ -364,9 +364,15 @@ def main():
         with open(tpath) as f:
             tj = json.load(f)
         if tj.get("direction") == direction and tj.get("record_inner_bytes") == inner:
-            traffic = round(tj["hbm_bytes_per_record"] * n)
-            traffic_src = (f"profiles/traffic_{args.config}.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                           f"run {tj.get('source', '?')}, {tj['hbm_bytes_per_record']:.0f} B/record x {n} records)")
+            # reads from the request-size-resolved L2->fabric counters when the
+            # profile has them (calibrated), else FETCH_SIZE x 2
+            per_rec = tj.get("hbm_bytes_per_record_sized", tj["hbm_bytes_per_record"])
+            reads = tj.get("read_counters", "FETCH_SIZE x 2")
+            if "hbm_bytes_per_record_sized" in tj:
+                reads = "TCC_EA0_RDREQ_{32B,64B,128B}_sum x size"
+            traffic = round(per_rec * n)
+            traffic_src = (f"profiles/traffic_{args.config}.json (rocprofv3 --pmc, reads {reads}, writes WRITE_SIZE; "
+                           f"run {tj.get('source', '?')}, {per_rec:.0f} B/record x {n} records)")
     # The unit that actually bounds the kernel (LDS for the table ciphers):
     # its busy fraction from the committed PMC run (profiles/ceiling_<config>.json)
     # and the rate this kernel would reach with that unit 100 % busy.
