@@ -68,6 +68,8 @@ CONFIGS = {
                    "ChaCha20-Poly1305 encrypt, 1M x 16 KiB TLS 1.3 records, single key (chacha16k sent)"),
     "c2s": ("AES-256-GCM", "TLS1.3", "decrypt", 1400, 1 << 20, 1,
             "AES-256-GCM decrypt, 1M x 1.4 KiB TLS 1.3 records, single key (the GCM half of c4s without the key passes)"),
+    "c2se": ("AES-256-GCM", "TLS1.3", "encrypt", 1400, 1 << 20, 1,
+             "AES-256-GCM encrypt, 1M x 1.4 KiB TLS 1.3 records, single key (c2s sent)"),
     "c4s": ("MIX", "TLS1.3", "decrypt", 1400, 1 << 22, 1 << 16,
             "64K keys x 64 records, AES-256-GCM (even keys) + ChaCha20-Poly1305 (odd keys), records round-robin over keys, 1.4 KiB TLS 1.3 decrypt"),
 }
