@@ -572,13 +572,14 @@ def cpu_baseline(cname, ver, content, inner, wire, stride, km, target_s, directi
     reference's default x86 path (AES-NI on by default, ChangeLog:1021-1024);
     'port' -- this repository's C restatement (oracle/, table AES + 4-bit
     Shoup GHASH, the Mbed TLS builtin design).  Multi-connection configs (c4,
-    c4s) run both legs with one key context per connection, record i under
-    connection i % keys (ssl_misc.h:1073-1120: one transform per connection).
+    c4s, k4: any config with more than one key) run both legs with one key
+    context per connection, record i under connection i % keys
+    (ssl_misc.h:1073-1120: one transform per connection).
     The headline value is the faster leg (the stronger CPU baseline); both are
     listed, with the EVP leg's per-call time split."""
     import oracle as O
     from tests.prng import prng_array
-    mix = cname == "MIX"
+    mix = len(km) > 1      # one transform per connection (c4, c4s, k4)
     cipher = {"CHACHA20-POLY1305": O.CHACHA20_POLY1305, "AES-128-GCM": O.AES_128_GCM, "AES-128-CCM": O.AES_128_CCM,
               "AES-128-CCM-8": O.AES_128_CCM_8, "AES-192-GCM": O.AES_192_GCM,
               "ARIA-256-GCM": O.ARIA_256_GCM, "CAMELLIA-128-GCM": O.CAMELLIA_128_GCM}.get(cname, O.AES_256_GCM)
