@@ -264,9 +264,9 @@ static uint32_t gcm_tm(bool pair, bool wp)
      * fold, the tree and the final multiplies (the key-pass kernels then
      * stage only the Horner table).  Default on for the wave passes, whose
      * tails were table-free multiplies (same box: k4 582 -> 636 GiB/s, DTLS
-     * 16 x 1.4 KiB +17 %); off for the 16-wave key passes, whose LDS-table
-     * tree is cheaper than a VALU multiply on an LDS-bound kernel (c2 712 vs
-     * 712-720, c2s 577 vs 545, c4 1034 vs 1032; profiles/r04h). */
+     * 16 x 1.4 KiB +17 %); compiled into the wave-pass kernels only (the
+     * 16-wave key passes' LDS-table tree is cheaper than a VALU multiply on an
+     * LDS-bound kernel, and the run-time flag alone cost c2 5 %, tlsrec_gcm.h). */
     const char *e = getenv("TLSREC_GCM_TREEMUL");
     return e ? (uint32_t) atoi(e) & 15u : (pair ? 15u : (wp ? 9u : 1u));
 }
@@ -620,6 +620,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         int L = (lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) ? (int) lanes
                 : (nl <= 1 || rpk >= 128) ? 8 : (rpk >= 48 ? 16 : 64);
         if (!(lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) && Lfill > L) L = Lfill;
+        /* one key, small records (<= 4 KiB, size hint): 4 lanes per record
+         * (16 records per wave round) once the batch fills the chip at that --
+         * half the lane tree and twice the records in flight per wave.  Same
+         * box (r04r): c2s 592/582 -> 652/661, c2se 610/604 -> 682/681 GiB/s;
+         * 16 KiB records keep 8 (c2 750/742 at 8, 732/737 at 4). */
+        if (!(lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 64) && nl <= 1 && L == 8 &&
+            rpwave >= 16 && avg_bytes != 0 && avg_bytes <= 4096)
+            L = 4;
         if (kt->has_cid) L = 8;     /* the CID variant: one configuration */
         GcmArgs a;
         a.slots = kt->d_slots;

@@ -275,7 +275,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             {
                 const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
                 uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
-                const int t0 = (!CID && (a.tm & 8u)) ? (G5 ? LY::NT : LY::NT - 1) : 0;
+                const int t0 = (WP && !CID && (a.tm & 8u)) ? (G5 ? LY::NT : LY::NT - 1) : 0;
                 for (int i = tid + t0 * 512; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
                 if constexpr (G5) {
                     uint4 *d5 = reinterpret_cast<uint4 *>(lds + LY::HG5);
@@ -362,7 +362,11 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
              * multiplies per record at L = 32 before, 4 at L = 2). */
             /* (m a multiple of BL: LEN would open a step of its own; lane 0
              * takes it at the tail instead, Y_0 = Y_0 H^L + LEN, one multiply) */
-            const bool lp = !CID && (a.tm & 8u);
+            /* wave passes only: as a run-time flag in the 16-wave key-pass
+             * kernels it cost c2 5 % with the flag off (the hot loop carries
+             * the LEN position test and its registers; same box, r04p/q:
+             * 737 -> 700 GiB/s), and on it was no faster (r04e) */
+            const bool lp = WP && !CID && (a.tm & 8u);
             const bool lenx = lp && m % BL == 0;
             const uint32_t z = lp ? 0u : (BL - mm % BL) % BL;           /* front padding: position of C_1 */
             const uint32_t J = jb.run ? (lp ? (lenx ? m / BL : (m + BL) / BL) : (mm + z) / BL) : 0;

@@ -373,8 +373,10 @@ def test_key_ordered_descriptors_vs_openssl_evp(monkeypatch, nkeys, rpk, span, m
 
 @pytest.mark.parametrize("nkeys,n", [(1, 30_000), (64, 65_536)], ids=["1key_G5", "64keys_keypass"])
 @pytest.mark.parametrize("cipher,ver", CASES[:4], ids=lambda x: str(x))
-def test_key_pass_lane_powers_vs_openssl_evp(monkeypatch, cipher, ver, nkeys, n):
-    """TLSREC_GCM_TREEMUL=9: lane powers in the 16-wave key-pass kernels too
-    (off by default there), single key (the G5 kernel) and many keys"""
+def test_key_pass_tree_modes_vs_openssl_evp(monkeypatch, cipher, ver, nkeys, n):
+    """TLSREC_GCM_TREEMUL=9 on the 16-wave key-pass kernels, single key (the G5
+    kernel, 4 lanes per record) and many keys: lane powers are compiled into
+    the wave-pass kernels only, so the key passes must ignore bit 3 and still
+    match OpenSSL byte for byte"""
     monkeypatch.setenv("TLSREC_GCM_TREEMUL", "9")
     _evp_case(cipher, ver, nkeys, n)
