@@ -795,10 +795,6 @@ __device__ inline G128 g_mul(G128 x, G128 y)
     return z;
 }
 
-/* x * P with base[j] = P * x^j (words, tlsrec_keysetup_kernel's LDS
- * base): the XOR of the base entries of x's set bits, masked, not branched */
-__device__ inline G128 g_mul_base(const uint4 *base, G128 x);
-
 __device__ __forceinline__ uint4 g_to_words(G128 v)
 {
     return make_uint4(bswap32((uint32_t) (v.hi >> 32)), bswap32((uint32_t) v.hi),
@@ -813,17 +809,32 @@ __device__ __forceinline__ G128 g_from_words(uint4 w)
     return v;
 }
 
-__device__ inline G128 g_mul_base(const uint4 *base, G128 x)
+/* x * P with base[j] = P * x^j (words, tlsrec_keysetup_kernel's LDS base):
+ * the XOR of the base entries of x's set bits, masked, not branched -- over
+ * four lanes: lane r (= lane & 3) sums terms 32 r .. 32 r + 31, the XOR over
+ * the four lanes gives the product in each of them (the four lanes of a
+ * group must be active together) */
+__device__ inline G128 g_mul_base_q(const uint4 *base, G128 x, int r)
 {
+    const uint64_t half = r < 2 ? x.hi : x.lo;
+    const int top = (r & 1) ? 31 : 63;
     uint4 acc = make_uint4(0, 0, 0, 0);
-    for (int j = 0; j < 128; j++) {
-        const uint64_t bit = (j < 64) ? (x.hi >> (63 - j)) & 1 : (x.lo >> (127 - j)) & 1;
-        const uint32_t m = 0u - (uint32_t) bit;
-        const uint4 b = base[j];
+#pragma unroll 8
+    for (int i = 0; i < 32; i++) {
+        const uint32_t m = 0u - (uint32_t) ((half >> (top - i)) & 1);
+        const uint4 b = base[32 * r + i];
         acc.x ^= b.x & m; acc.y ^= b.y & m; acc.z ^= b.z & m; acc.w ^= b.w & m;
+    }
+#pragma unroll
+    for (int d = 1; d < 4; d <<= 1) {
+        acc.x ^= (uint32_t) __shfl_xor((int) acc.x, d);
+        acc.y ^= (uint32_t) __shfl_xor((int) acc.y, d);
+        acc.z ^= (uint32_t) __shfl_xor((int) acc.z, d);
+        acc.w ^= (uint32_t) __shfl_xor((int) acc.w, d);
     }
     return g_from_words(acc);
 }
+
 
 /* ---------------- ChaCha20 (RFC 8439 2.3) ------------------------------ */
 #define TLSREC_QR(a, b, c, d)                                  \
