@@ -236,7 +236,12 @@ __device__ inline void cam_encrypt_u64(const uint8_t *sb, const uint64_t sk[34],
 }
 
 /* One 256-thread workgroup per slot. */
-__global__ __launch_bounds__(256) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab, uint8_t *cipher_of,
+/* 8 waves per SIMD (64 VGPRs, 24 spilled): one workgroup per slot runs long
+ * dependent chains (key expansion, the squarings of H, the power ladder), so
+ * resident workgroups are the throughput.  The H^1..H^64 values of r04 had
+ * taken it to 102 VGPRs and 4 waves (keysched 14.3 -> 11.5 M connections/s);
+ * same box, profiles/r04w: 4 waves 11.6 M, 6 waves 14.4 M, 8 waves 16.0 M. */
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void tlsrec_keysetup_kernel(SlotState *slots, uint4 *ghtab, uint8_t *cipher_of,
                                                              const tlsrec_key_material *keys,
                                                              uint32_t first, uint32_t count)
 {

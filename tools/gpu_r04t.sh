@@ -17,3 +17,13 @@ for v in lad; do
   (cd /tmp && TLSREC_LIBRARY=$R/ablib/libtlsrec_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$v -o run --output-format csv -- python3 $R/tools/bench_keysched.py > $R/$O/prof_$v.json 2> $R/$O/prof_$v.err) || { echo "prof $v failed"; exit 1; }
   cut -d, -f1-4 $O/prof_$v/run_kernel_stats.csv | head -6
 done
+# c4's GCM half: lanes per record 16 (auto, 64 records per key) vs 8
+b() {  # name, env, args
+  local name=$1 envs=$2; shift 2
+  env $envs timeout -k 10 300 python3 bench.py --no-cpu --no-e2e --verify 16 "$@" > $O/$name.json 2> $O/$name.err || { echo "FAIL $name"; tail -3 $O/$name.err; return 1; }
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['kernel_ms_avg'], d['check']['bad_records'])" $O/$name.json $name
+}
+for rep in 1 2; do
+  b c4_auto_$rep X=1 --config c4 || exit 1
+  b c4_L8_$rep TLSREC_GCM_LANES=8 --config c4 || exit 1
+done
