@@ -50,6 +50,8 @@ CONFIGS = {
             "AES-128-CCM decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
     "ccm8": ("AES-128-CCM-8", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
              "AES-128-CCM_8 decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
+    "ccme": ("AES-128-CCM", "TLS1.3", "encrypt", 16383, 1 << 20, 1,
+             "AES-128-CCM encrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2, ccm sent)"),
     "gcm192": ("AES-192-GCM", "TLS1.3", "decrypt", 16383, 1 << 20, 1,
                "AES-192-GCM decrypt, 1M x 16 KiB TLS 1.3 records, single key (8(f)-2)"),
     "aria256": ("ARIA-256-GCM", "TLS1.2", "decrypt", 16384, 1 << 20, 1,
