@@ -80,6 +80,15 @@ def test_bulk_records_vs_openssl_evp(cipher, ver, nkeys, n):
     _evp_case(cipher, ver, nkeys, n)
 
 
+@pytest.mark.parametrize("cipher,ver", CASES[:4], ids=lambda x: str(x))
+def test_single_key_small_records_four_lanes_vs_openssl_evp(cipher, ver):
+    """One key, 70 000 records of 0..2 048 B (every edge length) with a size
+    hint under 4 KiB: the single-key key pass at 4 lanes per record (engine.hip,
+    r04; it needs >= 16 records per wave of a full grid), both directions
+    against OpenSSL EVP"""
+    _evp_case(cipher, ver, 1, 70_000, mean_bytes=1100)
+
+
 @pytest.mark.parametrize("nkeys,rpk,span,mean", [(2048, 64, (1000, 1500), 1300), (2048, 32, (1000, 1500), 1300),
                                                   (4096, 16, (1000, 1500), 1300), (4096, 8, (12000, 16383), 14000),
                                                   (8192, 4, (12000, 16383), 14000)],

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+O=gpurun_out/${TAG:-r04t4}
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider tests/test_evp_parity_gpu.py -k four_lanes > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
