@@ -268,7 +268,13 @@ static uint32_t gcm_tm(bool pair, bool wp)
      * 16-wave key passes' LDS-table tree is cheaper than a VALU multiply on an
      * LDS-bound kernel, and the run-time flag alone cost c2 5 %, tlsrec_gcm.h). */
     const char *e = getenv("TLSREC_GCM_TREEMUL");
-    return e ? (uint32_t) atoi(e) & 15u : (pair ? 15u : (wp ? 9u : 1u));
+    uint32_t tm = e ? (uint32_t) atoi(e) & 15u : (pair ? 15u : (wp ? 9u : 1u));
+    /* bit 4 (r05): the paired passes build the key's Horner table in LDS
+     * from H^L (tlsrec_clmul.h tlsrec_gtab4_window) instead of staging its
+     * 8 KiB from HBM per key pass; TLSREC_GCM_HBUILD=0 stages it */
+    const char *hb = getenv("TLSREC_GCM_HBUILD");
+    if (pair && !(hb && atoi(hb) == 0)) tm |= 16u;
+    return tm;
 }
 
 /* paired wave passes (16 waves, two per key table) for small records of many
@@ -354,19 +360,35 @@ static void scratch_thread_exit(void *)
 static void scratch_key_init(void) { pthread_key_create(&g_scratch_key, scratch_thread_exit); }
 
 /* with g_scratch_mu held */
-static void scratch_reclaim_locked(void)
+/* Under g_scratch_mu: unlink the orphaned entries (their threads exited) and
+ * return them as a list; scratch_free_list frees them after the lock is
+ * dropped -- hipFree waits for the device (a record-server grid, other
+ * streams' kernels), and no other launcher should queue behind that. */
+static ScratchEntry *scratch_reclaim_locked(void)
 {
+    ScratchEntry *dead = nullptr;
     for (ScratchEntry **pp = &g_scratch; *pp;) {
         ScratchEntry *e = *pp;
         if (e->thread == SCRATCH_ORPHAN) {
             *pp = e->next;
-            if (e->mem) hipFree(e->mem);
-            pthread_mutex_destroy(&e->mu);
-            free(e);
+            e->next = dead;
+            dead = e;
             g_scratch_orphans--;
         } else {
             pp = &e->next;
         }
+    }
+    return dead;
+}
+
+static void scratch_free_list(ScratchEntry *e)
+{
+    while (e) {
+        ScratchEntry *next = e->next;
+        if (e->mem) (void) hipFree(e->mem);
+        pthread_mutex_destroy(&e->mu);
+        free(e);
+        e = next;
     }
 }
 
@@ -380,13 +402,14 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
      * stream is one queue for every thread and needs nothing) */
     const uintptr_t thr = st == hipStreamPerThread ? (uintptr_t) pthread_self() : 0;
     pthread_mutex_lock(&g_scratch_mu);
-    if (g_scratch_orphans) scratch_reclaim_locked();
+    ScratchEntry *dead = g_scratch_orphans ? scratch_reclaim_locked() : nullptr;
     ScratchEntry *e = g_scratch;
     while (e && !(e->device == dev && e->stream == st && e->thread == thr && e->kind == kind)) e = e->next;
     if (!e) {
         e = (ScratchEntry *) calloc(1, sizeof(*e));
         if (!e) {
             pthread_mutex_unlock(&g_scratch_mu);
+            scratch_free_list(dead);
             return TLSREC_ERR_SSL_ALLOC_FAILED;
         }
         e->device = dev;
@@ -402,6 +425,7 @@ extern "C" int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, t
         }
     }
     pthread_mutex_unlock(&g_scratch_mu);
+    scratch_free_list(dead);
     pthread_mutex_lock(&e->mu);
     if (e->bytes < bytes) {
         /* grow: the stream's earlier work may still read the old buffer */
@@ -575,8 +599,15 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
      * before the AEAD kernels run (the guard kernel, or the bucket count
      * kernel), so a record that no kernel reaches fails closed -- the
      * reference's auth_done check, ssl_msg.c:1260 / :1804. */
-    /* batch work takes the CUs the record server holds (server.hip) */
-    if (!opt.coalesced) tlsrec__server_yield();
+    /* batch work takes the CUs the record server holds (server.hip): yield
+     * now, note the batch's stream on every way out (the server launches no
+     * grid between the two) */
+    struct YieldGuard {
+        hipStream_t st;
+        bool on;
+        ~YieldGuard() { if (on) tlsrec__server_note_batch(st); }
+    } yg{ st, !opt.coalesced };
+    if (yg.on) tlsrec__server_yield();
     BucketScratch bs;
     const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced;
     if (identity) {
@@ -793,7 +824,6 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     tlsrec__scratch_release(&bs.lease);
-    if (!opt.coalesced) tlsrec__server_note_batch(st);
     return rc;
 }
 

@@ -40,13 +40,25 @@
  * Termination: a server grid lives `life` ticks of the device wall clock
  * (TLSREC_SERVER_MS, default 20 ms) and at most `max_iter` polls, and leaves
  * early on the set's stop word (process exit, or batch work arriving: below)
- * or when no request of the set was served for `idle` ticks
+ * or when no request of the set was claimed for `idle` ticks
  * (TLSREC_SERVER_IDLE_MS, default 1 ms), so a hipDeviceSynchronize after the
  * last single-record call waits about that long, not a whole window.  The
  * host submits to a grid only inside its window minus a margin and launches
- * the next grid on the other slot set when the window closes; a request the
- * grid did not take (its kernel has ended) is withdrawn and runs on the
- * launch path.
+ * the next grid on the other slot set when the window closes.
+ *
+ * The idle exit is ordered against host submits (r05): before it posts a
+ * request the host bumps the set's `activity` word and then reads `closing`
+ * (both in host-mapped memory, a full fence between); the idle exit is
+ * workgroup 0's alone: it writes `closing` = 1, fences, and re-reads
+ * `activity` -- unchanged, it commits (the device-memory `quit` word, which the
+ * other workgroups poll); changed, it clears `closing` and stays.  Whichever
+ * of the two stores comes first, one side sees the other's (Dekker): a host
+ * that read `closing` = 0 has a grid that will not leave before the request's
+ * workgroup has polled it, and a host that read 1 does not post at all and
+ * launches the next grid on the other set.  `closing` stays 1 after a commit,
+ * so a grid that left while no call came is found the same way.  A request a
+ * grid never took (its kernel ended: a stop word racing a post) is withdrawn
+ * and runs on the launch path.
  *
  * Yielding to batch work (r04): the grid holds 64 CUs (89 KiB of LDS each,
  * so no 128 KiB batch workgroup fits beside it).  Every batch launch outside
@@ -128,6 +140,19 @@ struct SrvReq {
 static_assert(offsetof(SrvReq, done) == 64 && offsetof(SrvReq, desc) == 128 && offsetof(SrvReq, res) == 272 &&
                   offsetof(SrvReq, buf) == 384 && sizeof(SrvReq) % 64 == 0,
               "SrvReq layout");
+
+/* A set's control words in pinned host memory mapped into the device, one
+ * cache line each (the idle-exit handshake above). */
+struct SrvCtl {
+    uint32_t stop;            /* host: leave now (process exit, batch work) */
+    uint8_t pad0[60];
+    uint32_t activity;        /* host: bumped before every post to this grid */
+    uint8_t pad1[60];
+    uint32_t closing;         /* workgroup 0: deciding to leave idle (1), or left */
+    uint8_t pad2[60];
+};
+static_assert(offsetof(SrvCtl, activity) == 64 && offsetof(SrvCtl, closing) == 128 && sizeof(SrvCtl) == 192,
+              "SrvCtl layout");
 
 /* ---------------- LDS record access (16-byte aligned AEAD region) -------- */
 __device__ __forceinline__ uint4 lds16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
@@ -609,6 +634,11 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p)
+{
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
 __device__ __forceinline__ uint32_t comp(uint4 v, int i)
 {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
@@ -745,7 +775,7 @@ __device__ __forceinline__ void srv_serve(SrvReq *rq, uint64_t w0, const SlotSta
  * per CU): the compiler is told to schedule for one wave per EU -- all
  * lookups of an AES round in flight together. */
 __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void tlsrec_server_kernel(
-    SrvReq *reqs, const uint32_t *stop, uint64_t life_ticks, uint32_t max_iter, uint32_t flags, uint64_t *last_active,
+    SrvReq *reqs, SrvCtl *sc, uint64_t life_ticks, uint32_t max_iter, uint32_t flags, uint32_t *quit,
     uint64_t idle_ticks)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[SRV_LDS];
@@ -758,6 +788,9 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
     uint32_t served = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&rq->done, __ATOMIC_RELAXED,
                                                                        __HIP_MEMORY_SCOPE_SYSTEM));
     uint32_t idle = 0;
+    /* workgroup 0's idle clock: the activity word as last seen, and when it changed */
+    uint32_t a_seen = blockIdx.x == 0 ? ld_sys32(&sc->activity) : 0u;
+    uint64_t t_seen = t0;
     for (uint32_t it = 0;; it++) {
         uint32_t *c = ctl + (it & 1) * 10;
         if (wave == 0) {
@@ -774,20 +807,37 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
                     const uint64_t tagw = (uint64_t) (seq & 0xffffu) << 48;
                     v = (((h1 ^ tagw) | (h2 ^ tagw) | (h3 ^ tagw)) >> 48) ? 3u : 1u;   /* half-posted: again */
                     v = __builtin_amdgcn_readfirstlane(v);
-                } else if ((it & 15) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                                 stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0) {
+                } else if ((it & 15) == 0 &&
+                           (ld_sys32(&sc->stop) != 0 ||
+                            __builtin_amdgcn_readfirstlane(
+                                __hip_atomic_load(quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)) {
                     v = 2;
                 } else {
                     const uint64_t now = wall_clock64();
                     v = (uint64_t) (now - t0) > life_ticks ? 2u : 0u;
-                    if ((it & 15) == 8) {
-                        /* the set's last served request, any workgroup: all
-                         * of the grid leaves together once it is idle_ticks old */
-                        uint64_t la = __hip_atomic_load(last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        la = (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) la) |
-                             (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (la >> 32)) << 32;
-                        const uint64_t since = la > t0 ? la : t0;
-                        if (now - since > idle_ticks) v = 2u;
+                    if (blockIdx.x == 0 && (it & 15) == 8 && v == 0) {
+                        /* the idle exit (workgroup 0 for the grid): no claim
+                         * seen for idle_ticks -> closing = 1, fence, re-read */
+                        const uint32_t a = ld_sys32(&sc->activity);
+                        if (a != a_seen) {
+                            a_seen = a;
+                            t_seen = now;
+                        } else if (now - t_seen > idle_ticks) {
+                            __hip_atomic_store(&sc->closing, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                            const uint32_t a2 = __builtin_amdgcn_readfirstlane(
+                                __hip_atomic_load(&sc->activity, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM));
+                            if (a2 == a_seen) {
+                                /* committed: the other workgroups leave at their next stop check */
+                                __hip_atomic_store(quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                v = 2u;
+                            } else {
+                                /* a claim landed: stay (the host that made it read closing = 0) */
+                                __hip_atomic_store(&sc->closing, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+                                a_seen = a2;
+                                t_seen = now;
+                            }
+                        }
                     }
                 }
             }
@@ -822,7 +872,6 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                 }
                 __hip_atomic_store(&rq->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(last_active, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             served = seq;
             idle = 0;
@@ -842,9 +891,9 @@ namespace {
 
 struct SrvSet {
     SrvReq *h = nullptr, *d = nullptr;
-    uint32_t *stop_h = nullptr, *stop_d = nullptr;
-    uint64_t *last_active = nullptr;  /* device: wall clock of the set's last served request */
-    uint64_t t_last = 0;              /* host: time of the last submit to this grid */
+    SrvCtl *ctl_h = nullptr, *ctl_d = nullptr;
+    uint32_t *quit = nullptr;         /* device: workgroup 0 committed to the idle exit */
+    uint32_t activity = 0;            /* host copy of ctl_h->activity */
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
     bool launched = false;
@@ -864,15 +913,22 @@ int g_trace = 0;                  /* TLSREC_SERVER_TRACE=1: device phase times, 
 uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr_gcm = 0, g_tr_cyc = 0, g_tr_a1 = 0,
          g_tr_b1 = 0;
 double g_tick_ns = 10.0;
-uint64_t g_submit_ns = 0, g_life_ticks = 0, g_idle_ticks = 0, g_idle_ns = 0;
-/* batch work (tlsrec__server_yield / _note_batch): no grid while it is pending */
+uint64_t g_submit_ns = 0, g_life_ticks = 0, g_idle_ticks = 0;
+/* batch work (tlsrec__server_yield / _note_batch): no grid while any is
+ * queued or pending.  Batches may run on several streams at once: each
+ * records its own event in a small ring, and the batches between their yield
+ * and their note (kernels still being queued) are counted. */
 int g_yield = 1;                  /* TLSREC_SERVER_YIELD=0: the server ignores batch work */
-hipEvent_t g_batch_ev = nullptr;
-bool g_batch_pending = false;
+constexpr int BATCH_EVS = 16;
+hipEvent_t g_batch_ev[BATCH_EVS] = {};
+uint32_t g_batch_pending = 0;     /* bit k: event k recorded, not yet seen complete */
+uint32_t g_batch_next = 0;
+uint32_t g_batch_queueing = 0;    /* batches between tlsrec__server_yield and _note_batch */
 std::atomic<uint64_t> g_yields{0};
 /* why a call took the launch path: batch work pending, the other set not
- * drained, the grid gone before it took the request (tlsrec__server_why) */
-uint64_t g_why_batch = 0, g_why_drain = 0, g_why_withdrawn = 0, g_why_noslot = 0;
+ * drained, the grid gone before it took the request (tlsrec__server_why);
+ * claims that found a grid closing (and moved to the other set) */
+uint64_t g_why_batch = 0, g_why_drain = 0, g_why_withdrawn = 0, g_why_noslot = 0, g_closing = 0;
 uint32_t g_max_iter = 0;
 std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
 
@@ -886,13 +942,23 @@ uint64_t now_ns()
 void srv_shutdown()
 {
     pthread_mutex_lock(&g_mu);
-    for (auto &S : g_set)
+    for (auto &S : g_set) {
         if (S.launched) {
-            __atomic_store_n(S.stop_h, 1u, __ATOMIC_RELEASE);
+            __atomic_store_n(&S.ctl_h->stop, 1u, __ATOMIC_RELEASE);
             const hipError_t e = hipEventSynchronize(S.ev);
             if (g_debug) fprintf(stderr, "tlsrec server: shutdown, grid drained: %s\n", hipGetErrorString(e));
             S.launched = false;
         }
+        if (S.quit) (void) hipFree(S.quit);
+        S.quit = nullptr;
+    }
+    for (auto &e : g_batch_ev)
+        if (e) {
+            (void) hipEventSynchronize(e);
+            (void) hipEventDestroy(e);
+            e = nullptr;
+        }
+    g_state = -1;
     if (g_trace && g_tr_n)
         fprintf(stderr, "{\"server_trace\": {\"requests\": %llu, \"load_us\": %.2f, \"aead_us\": %.2f, "
                         "\"writeback_us\": %.2f}}\n",
@@ -929,7 +995,6 @@ int srv_setup_locked()
     if (!(idle_ms >= 0.05)) idle_ms = 0.05;
     if (idle_ms > ms) idle_ms = ms;
     g_idle_ticks = (uint64_t) (idle_ms * khz);
-    g_idle_ns = (uint64_t) (idle_ms * 1e6);
     if (const char *y = getenv("TLSREC_SERVER_YIELD")) g_yield = strcmp(y, "0") != 0;
     g_tick_ns = 1e6 / khz;
     g_max_iter = (uint32_t) (ms * 10000.0);          /* backstop: a poll (a PCIe read + s_sleep) is > 0.1 us */
@@ -940,18 +1005,19 @@ int srv_setup_locked()
         if (hipHostMalloc((void **) &S.h, sizeof(SrvReq) * SRV_SLOTS, hipHostMallocMapped | hipHostMallocCoherent) !=
                 hipSuccess ||
             hipHostGetDevicePointer(&hd, S.h, 0) != hipSuccess ||
-            hipHostMalloc((void **) &S.stop_h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(&sd, S.stop_h, 0) != hipSuccess ||
+            hipHostMalloc((void **) &S.ctl_h, sizeof(SrvCtl), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(&sd, S.ctl_h, 0) != hipSuccess ||
             hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess ||
-            hipMalloc((void **) &S.last_active, 64) != hipSuccess)
+            hipMalloc((void **) &S.quit, 64) != hipSuccess || hipMemset(S.quit, 0, 64) != hipSuccess)
             return g_state;
         memset(S.h, 0, sizeof(SrvReq) * SRV_SLOTS);
-        memset(S.stop_h, 0, 64);
+        memset(S.ctl_h, 0, sizeof(SrvCtl));
         S.d = (SrvReq *) hd;
-        S.stop_d = (uint32_t *) sd;
+        S.ctl_d = (SrvCtl *) sd;
     }
-    if (hipEventCreateWithFlags(&g_batch_ev, hipEventDisableTiming) != hipSuccess) return g_state;
+    for (auto &e : g_batch_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return g_state;
     atexit(srv_shutdown);
     g_state = 1;
     return g_state;
@@ -964,19 +1030,20 @@ bool kernel_done(SrvSet &S) { return !S.launched || hipEventQuery(S.ev) != hipEr
 SrvSet *srv_current_locked(uint64_t now)
 {
     SrvSet *S = &g_set[g_cur];
-    if (S->launched && now - S->t_launch < g_submit_ns) {
-        /* a grid idle for half its idle limit may have left: ask its event */
-        if (now - S->t_last < g_idle_ns / 2 || !kernel_done(*S)) return S;
-        S->t_launch = 0;              /* ended early: never submit to it again */
+    /* inside its window (an idle exit is found by the caller's claim) */
+    if (S->launched && S->t_launch != 0 && now - S->t_launch < g_submit_ns) return S;
+    /* batch work queued or pending on the device: the launch path, no grid beside it */
+    if (g_batch_queueing) {
+        g_why_batch++;
+        return nullptr;
     }
-    /* batch work pending on the device: the launch path, no grid beside it */
-    if (g_batch_pending) {
-        const hipError_t q = hipEventQuery(g_batch_ev);
-        if (q == hipErrorNotReady) {
+    for (uint32_t m = g_batch_pending; m; m &= m - 1) {
+        const int k = __builtin_ctz(m);
+        if (hipEventQuery(g_batch_ev[k]) == hipErrorNotReady) {
             g_why_batch++;
             return nullptr;
         }
-        g_batch_pending = false;
+        g_batch_pending &= ~(1u << k);
     }
     SrvSet *N = &g_set[g_cur ^ 1];
     /* the other set must be drained: its grid ended, no host thread in it */
@@ -984,14 +1051,16 @@ SrvSet *srv_current_locked(uint64_t now)
         g_why_drain++;
         return nullptr;
     }
-    __atomic_store_n(N->stop_h, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&N->ctl_h->stop, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&N->ctl_h->closing, 0u, __ATOMIC_SEQ_CST);
     (void) hipGetLastError();         /* an earlier call's status (hipEventQuery's NotReady) is not the launch's */
-    /* (last_active keeps the previous grid's last serve: older than the new
-     * grid's start, which the idle check takes instead) */
-    hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d,
-                       (const uint32_t *) N->stop_d, g_life_ticks, g_max_iter, (uint32_t) g_trace, N->last_active,
-                       g_idle_ticks);
-    const hipError_t le = hipGetLastError();
+    /* quit = 0 in stream order ahead of the grid (the previous grid may have set it) */
+    hipError_t le = hipMemsetAsync(N->quit, 0, sizeof(uint32_t), N->st);
+    if (le == hipSuccess) {
+        hipLaunchKernelGGL(tlsrec_server_kernel, dim3(SRV_GROUPS), dim3(SRV_WAVES * 64), 0, N->st, N->d, N->ctl_d,
+                           g_life_ticks, g_max_iter, (uint32_t) g_trace, N->quit, g_idle_ticks);
+        le = hipGetLastError();
+    }
     if (le != hipSuccess || hipEventRecord(N->ev, N->st) != hipSuccess) {
         if (g_debug) fprintf(stderr, "tlsrec server: launch failed: %s\n", hipGetErrorString(le));
         g_state = -1;
@@ -999,7 +1068,6 @@ SrvSet *srv_current_locked(uint64_t now)
     }
     N->launched = true;
     N->t_launch = now;
-    N->t_last = now;
     g_cur ^= 1;
     g_launches++;
     return N;
@@ -1025,20 +1093,37 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
         pthread_mutex_unlock(&g_mu);
         return 1;
     }
-    SrvSet *S = srv_current_locked(now_ns());
+    SrvSet *S = nullptr;
     int i = -1;
-    if (S)
+    /* at most two sets: a claim that finds the current grid closing moves to
+     * the other set (launching its grid) */
+    for (int attempt = 0; attempt < 2 && i < 0; attempt++) {
+        S = srv_current_locked(now_ns());
+        if (!S) break;
         for (int k = 0; k < SRV_SLOTS; k++)
             if (!S->busy[k]) { i = k; break; }
+        if (i < 0) {
+            g_why_noslot++;
+            break;
+        }
+        /* the claim: activity, full fence, closing (workgroup 0 does the
+         * mirror image before it leaves idle) */
+        __atomic_store_n(&S->ctl_h->activity, ++S->activity, __ATOMIC_SEQ_CST);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        if (__atomic_load_n(&S->ctl_h->closing, __ATOMIC_SEQ_CST) != 0) {
+            S->t_launch = 0;          /* leaving or left: never submit to it again */
+            g_closing++;
+            i = -1;
+            S = nullptr;
+        }
+    }
     if (i < 0) {
-        if (S) g_why_noslot++;
         pthread_mutex_unlock(&g_mu);
         g_fallback++;
         return 1;
     }
     S->busy[i] = 1;
     S->nbusy++;
-    S->t_last = now_ns();
     const uint32_t seq = ++S->seq[i];
     pthread_mutex_unlock(&g_mu);
 
@@ -1104,9 +1189,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     pthread_mutex_lock(&g_mu);
     S->busy[i] = 0;
     S->nbusy--;
-    /* the grid is gone: no later call may submit to it (each submit refreshes
-     * t_last, so without this the next calls would see a "recent" grid and
-     * skip the event query -- a streak of withdrawals) */
+    /* the grid is gone: no later call may submit to it */
     if (rc == 1) S->t_launch = 0;
     pthread_mutex_unlock(&g_mu);
     return rc;
@@ -1119,9 +1202,10 @@ extern "C" void tlsrec__server_yield(void)
 {
     if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return;
     pthread_mutex_lock(&g_mu);
+    g_batch_queueing++;               /* no grid until this batch's note (below) */
     for (auto &S : g_set)
         if (S.launched && S.t_launch != 0) {
-            __atomic_store_n(S.stop_h, 1u, __ATOMIC_RELEASE);
+            __atomic_store_n(&S.ctl_h->stop, 1u, __ATOMIC_RELEASE);
             S.t_launch = 0;
             g_yields++;
         }
@@ -1133,13 +1217,24 @@ extern "C" void tlsrec__server_note_batch(hipStream_t stream)
 {
     if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-        (void) hipGetLastError();
-        return;                       /* a graph being captured: nothing runs yet */
-    }
+    const bool capturing = hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    if (capturing) (void) hipGetLastError();
     pthread_mutex_lock(&g_mu);
-    if (hipEventRecord(g_batch_ev, stream) == hipSuccess) g_batch_pending = true;
-    else (void) hipGetLastError();
+    if (g_batch_queueing) g_batch_queueing--;
+    if (!capturing) {                 /* (a graph being captured: nothing runs yet) */
+        /* a free ring entry, else the oldest (recording over a pending event
+         * moves it later, which keeps the rule "no grid while batch work is
+         * pending" -- it only waits longer) */
+        int k = -1;
+        for (int j = 0; j < BATCH_EVS; j++) {
+            const int c = (int) ((g_batch_next + (uint32_t) j) % BATCH_EVS);
+            if (!(g_batch_pending & (1u << c))) { k = c; break; }
+        }
+        if (k < 0) k = (int) (g_batch_next % BATCH_EVS);
+        g_batch_next = (uint32_t) k + 1;
+        if (hipEventRecord(g_batch_ev[k], stream) == hipSuccess) g_batch_pending |= 1u << k;
+        else (void) hipGetLastError();
+    }
     pthread_mutex_unlock(&g_mu);
 }
 
@@ -1155,6 +1250,15 @@ extern "C" void tlsrec__server_why(uint64_t out[4])
     out[2] = __atomic_load_n(&g_why_withdrawn, __ATOMIC_RELAXED);
     out[3] = g_why_noslot;
     pthread_mutex_unlock(&g_mu);
+}
+
+/* diagnostics: claims that found their grid closing (idle exit) and moved on */
+extern "C" uint64_t tlsrec__server_closing(void)
+{
+    pthread_mutex_lock(&g_mu);
+    const uint64_t c = g_closing;
+    pthread_mutex_unlock(&g_mu);
+    return c;
 }
 
 /* tests: route single-record calls through the server (1) or never (0) */

@@ -95,4 +95,70 @@ TLSREC_CLMUL_FN void tlsrec_gf128_mul(const uint32_t x[4], const uint32_t y[4], 
     for (int i = 0; i < 4; i++) out[i] = tlsrec_brev8x4(r[i]);
 }
 
+/* x * X^s for 0 <= s <= 63 (X the field's generator): with the GCM string
+ * as a 128-bit big-endian number V (X^0 the most significant bit), V >> s,
+ * and the s bits that fall off (X^128 .. X^(127+s)) folded back with
+ * X^128 = X^7 + X^2 + X + 1 -- their product by that stays below X^(s+7) <=
+ * X^70, so one fold is enough.  hi / lo are V's two 64-bit halves. */
+TLSREC_CLMUL_FN void tlsrec_gf128_shr(uint64_t *hi, uint64_t *lo, uint32_t s)
+{
+    const uint64_t h = *hi, l = *lo;
+    const uint64_t d = s ? l << (64 - s) : 0;              /* the dropped bits, at the top of a word */
+    uint64_t rl = s ? (l >> s) | (h << (64 - s)) : l;
+    uint64_t rh = h >> s;
+    rh ^= d ^ (d >> 1) ^ (d >> 2) ^ (d >> 7);
+    rl ^= (d << 63) ^ (d << 62) ^ (d << 57);
+    *hi = rh;
+    *lo = rl;
+}
+
+TLSREC_CLMUL_FN uint32_t tlsrec_bswap32(uint32_t v)
+{
+    return (v >> 24) | ((v >> 8) & 0xff00u) | ((v << 8) & 0xff0000u) | (v << 24);
+}
+
+/* The 4-bit position table of P (the layout of the key-setup kernel and of
+ * tlsrec_device.h gmul): window k, entry n = sum over the set bits 3-i of n
+ * of P * X^(4k+i), i.e. B_k * poly_n with B_k = P * X^(4k) and poly_n the
+ * degree-3 polynomial of n's bits.  The paired GCM passes build a key's
+ * Horner table in LDS this way from P = H^L alone instead of reading its
+ * 8 KiB from HBM: a lane starts at B_k = P * X^(4k) (two shifts), makes its
+ * entry n, and steps to window k + 4 by X^16. */
+TLSREC_CLMUL_FN void tlsrec_gtab4_entry(uint64_t bh, uint64_t bl, uint32_t n, uint64_t *rh, uint64_t *rl)
+{
+    uint64_t ah = 0, al = 0;
+    for (int i = 0; i < 4; i++) {
+        const uint64_t m = 0 - (uint64_t) ((n >> (3 - i)) & 1u);   /* masks: P is secret */
+        ah ^= bh & m;
+        al ^= bl & m;
+        tlsrec_gf128_shr(&bh, &bl, 1);
+    }
+    *rh = ah;
+    *rl = al;
+}
+
+/* words (the kernels' uint4 layout) <-> the 128-bit big-endian halves */
+TLSREC_CLMUL_FN void tlsrec_g_from_words(const uint32_t w[4], uint64_t *hi, uint64_t *lo)
+{
+    *hi = (uint64_t) tlsrec_bswap32(w[0]) << 32 | tlsrec_bswap32(w[1]);
+    *lo = (uint64_t) tlsrec_bswap32(w[2]) << 32 | tlsrec_bswap32(w[3]);
+}
+
+TLSREC_CLMUL_FN void tlsrec_g_to_words(uint64_t hi, uint64_t lo, uint32_t w[4])
+{
+    w[0] = tlsrec_bswap32((uint32_t) (hi >> 32));
+    w[1] = tlsrec_bswap32((uint32_t) hi);
+    w[2] = tlsrec_bswap32((uint32_t) (lo >> 32));
+    w[3] = tlsrec_bswap32((uint32_t) lo);
+}
+
+/* B_k = P * X^(4k), 0 <= k < 32 */
+TLSREC_CLMUL_FN void tlsrec_gtab4_base(const uint32_t p[4], uint32_t k, uint64_t *bh, uint64_t *bl)
+{
+    tlsrec_g_from_words(p, bh, bl);
+    const uint32_t sh = 4 * k, s1 = sh > 63 ? 63 : sh;
+    tlsrec_gf128_shr(bh, bl, s1);
+    tlsrec_gf128_shr(bh, bl, sh - s1);
+}
+
 #endif /* TLSREC_CLMUL_H */

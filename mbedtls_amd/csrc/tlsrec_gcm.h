@@ -77,6 +77,30 @@ __device__ __forceinline__ void pair_sync(uint32_t *cnt, uint32_t &phase, int la
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+/* Half ph of the pair builds windows 16 ph .. 16 ph + 15 of the 4-bit
+ * position table of P (tlsrec_clmul.h tlsrec_gtab4_*) at tab: lane (k0, n)
+ * makes entry n of windows k0, k0 + 4, k0 + 8, k0 + 12.  Out of line: the
+ * record kernel's registers are full, and inlined the build moved its spills
+ * into the per-record code. */
+__device__ __noinline__ void gtab4_build_half(uint8_t *tab, const uint4 *pp, int lane, int ph)
+{
+    const uint4 pv = *pp;
+    const uint32_t pw[4] = { pv.x, pv.y, pv.z, pv.w };
+    const uint32_t n = (uint32_t) lane & 15u, k0 = 16u * (uint32_t) ph + ((uint32_t) lane >> 4);
+    uint64_t bh, bl;
+    tlsrec_gtab4_base(pw, k0, &bh, &bl);
+    uint4 *dst = reinterpret_cast<uint4 *>(tab + k0 * 256 + n * 16);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        uint64_t eh, el;
+        uint32_t w[4];
+        tlsrec_gtab4_entry(bh, bl, n, &eh, &el);
+        tlsrec_g_to_words(eh, el, w);
+        dst[t * 64] = make_uint4(w[0], w[1], w[2], w[3]);    /* window k0 + 4 t */
+        if (t < 3) tlsrec_gf128_shr(&bh, &bl, 16);
+    }
+}
+
 /* Per-record state that the AEAD loop reads (kept small: it lives in
  * VGPRs across the loop). */
 struct GcmJob {
@@ -248,9 +272,16 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             pair_sync(pcnt, phase, lane);
             s = __builtin_amdgcn_readfirstlane(min(pmin[0], pmin[1]));
             if (s == 0xffffffffu) break;
-            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
-            uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
-            for (int i = lane + ph * 256; i < (ph + 1) * 256; i += 64) dst[i] = src[i];
+            if (a.tm & 16u) {
+                /* built from H^L itself (tm bit 4, r05): one 16-byte read of
+                 * the key's powers instead of 8 KiB of table per key pass */
+                gtab4_build_half(const_cast<uint8_t *>(hor), a.ghtab + (size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1),
+                                 lane, ph);
+            } else {
+                const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
+                uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
+                for (int i = lane + ph * 256; i < (ph + 1) * 256; i += 64) dst[i] = src[i];
+            }
             pair_sync(pcnt, phase, lane);
         } else if constexpr (WP) {
             /* wave pass: the wave's smallest pending slot; stage its H^L table

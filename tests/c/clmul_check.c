@@ -14,3 +14,25 @@ void clmul_check_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16])
     tlsrec_gf128_mul(a, b, r);
     memcpy(out, r, 16);
 }
+
+/* the 4-bit position table of p (32 windows x 16 entries x 16 B) as the
+ * paired GCM passes build it: lane (window k0 < 4, entry n) starts at
+ * B_k0 and steps by X^16 to windows k0 + 4, k0 + 8, ... */
+void clmul_check_gtab4(const uint8_t p[16], uint8_t out[8192])
+{
+    uint32_t a[4];
+    memcpy(a, p, 16);
+    for (uint32_t k0 = 0; k0 < 4; k0++)
+        for (uint32_t n = 0; n < 16; n++) {
+            uint64_t bh, bl;
+            tlsrec_gtab4_base(a, k0, &bh, &bl);
+            for (uint32_t k = k0; k < 32; k += 4) {
+                uint64_t eh, el;
+                uint32_t w[4];
+                tlsrec_gtab4_entry(bh, bl, n, &eh, &el);
+                tlsrec_g_to_words(eh, el, w);
+                memcpy(out + k * 256 + n * 16, w, 16);
+                tlsrec_gf128_shr(&bh, &bl, 16);
+            }
+        }
+}

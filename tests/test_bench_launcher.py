@@ -78,3 +78,62 @@ def test_bench_rank_checks_world_against_gpus():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"],
                        capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 2 and "WORLD_SIZE 2 but --gpus 4" in p.stderr, p.stderr[-2000:]
+
+
+def _fake_topology(tmp_path, gpus_minors, cpu_nodes=1, open_minors=None):
+    nodes = tmp_path / "nodes"
+    dri = tmp_path / "dri"
+    nodes.mkdir()
+    dri.mkdir()
+    k = 0
+    for _ in range(cpu_nodes):
+        (nodes / str(k)).mkdir()
+        (nodes / str(k) / "properties").write_text("cpu_cores_count 64\nsimd_count 0\ndrm_render_minor 0\n")
+        k += 1
+    for m in gpus_minors:
+        (nodes / str(k)).mkdir()
+        (nodes / str(k) / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\ngfx_target_version 90500\n"
+                                                   f"drm_render_minor {m}\n")
+        k += 1
+    for m in (gpus_minors if open_minors is None else open_minors):
+        (dri / f"renderD{m}").write_text("")
+    return str(nodes), str(dri)
+
+
+def test_count_gpus_from_sysfs(tmp_path):
+    """the launcher's device count: GPU topology nodes whose render node is
+    there to open (a container sees the host's 8 nodes, 2 render nodes), the
+    *_VISIBLE_DEVICES caps, and 0 without a KFD tree"""
+    nodes, dri = _fake_topology(tmp_path, [128, 136, 144, 152, 160, 168, 176, 184], open_minors=[136, 160])
+    assert bench.count_gpus(nodes, dri, env={}) == 2
+    assert bench.count_gpus(nodes, dri, env={"HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert bench.count_gpus(nodes, dri, env={"ROCR_VISIBLE_DEVICES": "0,1,2"}) == 2
+    assert bench.count_gpus(nodes, dri, env={"CUDA_VISIBLE_DEVICES": ""}) == 0
+    assert bench.count_gpus(str(tmp_path / "absent"), dri, env={}) == 0
+
+
+def test_launcher_parent_makes_no_gpu_call(tmp_path):
+    """bench.py --gpus N as its own launcher: counting devices and deciding
+    (here: refusing, with no devices) never imports torch or loads the HIP
+    runtime in the parent -- checked from inside the process at exit"""
+    probe = tmp_path / "probe.py"
+    probe.write_text(
+        "import atexit, sys, runpy\n"
+        "def _report():\n"
+        "    maps = open('/proc/self/maps').read()\n"
+        "    print('PARENT', 'torch' in sys.modules, 'libamdhip64' in maps, 'libtlsrec' in maps, file=sys.stderr)\n"
+        "atexit.register(_report)\n"
+        f"sys.argv = [{os.path.join(ROOT, 'bench.py')!r}, '--gpus', '2', '--steps', '1']\n"
+        f"runpy.run_path({os.path.join(ROOT, 'bench.py')!r}, run_name='__main__')\n")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, str(probe)], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "PARENT False False False" in p.stderr, p.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_count_gpus_matches_hip():
+    """on a GPU box the sysfs count agrees with the HIP runtime's"""
+    import torch
+    assert bench.count_gpus() == torch.cuda.device_count() >= 1

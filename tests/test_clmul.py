@@ -46,3 +46,27 @@ def test_clmul_identity_and_commutes(libs):
         x, y = prng_bytes(9600 + i, 16), prng_bytes(9700 + i, 16)
         assert _mul(c, "clmul_check_mul", x, one) == x
         assert _mul(c, "clmul_check_mul", x, y) == _mul(c, "clmul_check_mul", y, x)
+
+
+def _xpow_string(bits):
+    """the GCM string of sum X^j over j in bits (bit j = MSB-first bit j)"""
+    v = bytearray(16)
+    for j in bits:
+        v[j // 8] |= 0x80 >> (j % 8)
+    return bytes(v)
+
+
+def test_gtab4_table_vs_oracle(libs):
+    """the 4-bit position table built from P alone (tlsrec_gtab4_*, what the
+    paired GCM passes build in LDS from H^L): entry n of window k = P * sum of
+    X^(4k+i) over the set bits 3-i of n, against the oracle's multiply --
+    every window and entry, for H-like and edge values of P"""
+    c, o = libs
+    vals = [b"\x80" + bytes(15), bytes(15) + b"\x01", b"\xff" * 16] + [prng_bytes(9800 + i, 16) for i in range(12)]
+    out = ctypes.create_string_buffer(8192)
+    for p in vals:
+        c.clmul_check_gtab4(p, out)
+        for k in range(32):
+            for n in range(16):
+                want = _mul(o, "orc_gf128_mul", p, _xpow_string([4 * k + i for i in range(4) if (n >> (3 - i)) & 1]))
+                assert out.raw[k * 256 + 16 * n:k * 256 + 16 * n + 16] == want, (p.hex(), k, n)

@@ -265,25 +265,25 @@ def _evp_sample(torch, dev, A, B, stride, sample, km_keys, km_ivs, slots, cipher
                                rows_a.reshape(-1).copy(), rows_b.reshape(-1).copy(), threads)
 
 
-def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
-    """SURVEY 8(d)-4's 1400-B variant at its stated size, as bench.py times it:
-    65 536 keys x 64 records x 1 400 B TLS 1.3, AES-256-GCM (even keys) and
-    ChaCha20-Poly1305 (odd keys), record i under key i % 65 536 with sequence
-    number i // 65 536, the record-size hint (the line-grouped paired 2-lane
-    GCM passes, 2-lane ChaCha20-Poly1305).  Encrypt: every status and length,
-    a >= 4096-record EVP sample over both ciphers and the first and last keys.
-    Decrypt: 1 record in 1024 bit-flipped, INVALID_MAC at exactly those
-    indices, every other plaintext checked on the device, the failed ones wiped
-    (ssl_msg.c:1412-1424)."""
+def _full_size_row(nkeys, rpk, content, key_ciphers, seed, in_place=False):
+    """A BASELINE row at its stated size, as bench.py launches it: nkeys keys
+    (cipher of key k = key_ciphers[k % len]), nkeys x rpk TLS 1.3 records of
+    `content` bytes in 128-B slots, record i under key i % nkeys with sequence
+    number i // nkeys, the record-size hint (tlsrec_batch_*_sized).  Encrypt:
+    every status and length, a >= 4096-record EVP sample over every cipher
+    and the first and last keys.  Decrypt: 1 record in 1024 bit-flipped,
+    INVALID_MAC at exactly those indices, every other plaintext checked on the
+    device, the failed ones wiped (ssl_msg.c:1043, :1412-1424)."""
     torch = _torch()
     dev = torch.device("cuda")
-    nkeys, rpk, content = 1 << 16, 64, 1400
     n = nkeys * rpk
-    inner, wire, stride = 1408, 1424, 1536
-    rng = np.random.default_rng(0xC45)
+    inner = content + 1 + (16 - (content + 1) % 16) % 16
+    wire = inner + 16
+    stride = (wire + 127) // 128 * 128
+    rng = np.random.default_rng(seed)
     keys = rng.integers(0, 256, (nkeys, 32), dtype=np.uint8)
     ivs = rng.integers(0, 256, (nkeys, 12), dtype=np.uint8)
-    cip = np.where(np.arange(nkeys) % 2 == 0, M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305)
+    cip = np.array(key_ciphers, dtype=np.uint8)[np.arange(nkeys) % len(key_ciphers)]
     km = np.zeros(nkeys, dtype=M.KEY_MATERIAL)
     km["cipher"] = cip
     km["tls_minor"] = 4
@@ -304,7 +304,7 @@ def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
         d["type"] = 23
         d["ver"] = (3, 3)
         g = torch.Generator(device=dev)
-        g.manual_seed(4545)
+        g.manual_seed(seed)
         A = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
         B = torch.empty_like(A)
         res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
@@ -313,16 +313,17 @@ def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
         r = res.cpu().numpy().view(M.BATCH_RES)
         assert (r["status"] == 0).all(), np.unique(r["status"], return_counts=True)
         assert (r["data_offset"] == 0).all() and (r["data_len"] == wire).all()
+        assert (r["type"] == 23).all()
 
-        # EVP: >= 4096 records over both ciphers, with every record of the
+        # EVP: >= 4096 records over every cipher, with every record of the
         # first and of the last key
-        sample = np.unique(np.concatenate([np.arange(0, n, 1021, dtype=np.int64)[:4100],
-                                           np.arange(0, n, nkeys, dtype=np.int64),
-                                           np.arange(nkeys - 1, n, nkeys, dtype=np.int64)]))
+        sample = np.unique(np.concatenate([np.arange(0, n, max(1, n // 4100), dtype=np.int64)[:4100],
+                                           np.arange(0, n, nkeys, dtype=np.int64)[:4096],
+                                           np.arange(nkeys - 1, n, nkeys, dtype=np.int64)[:4096]]))
         assert len(sample) >= 4096
-        for c in (M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305):
+        for c in sorted(set(int(x) for x in key_ciphers)):
             s = sample[cip[slots[sample]] == c]
-            assert len(s) >= 1024
+            assert len(s) >= 4096 // len(set(key_ciphers)) - 8
             bad = _evp_sample(torch, dev, A, B, stride, s, keys, ivs, slots, c, M.VERSION_TLS1_3, content, _threads())
             assert int((bad != 0).sum()) == 0, f"cipher {c}: {int((bad != 0).sum())} of {len(s)} differ from OpenSSL"
 
@@ -334,7 +335,7 @@ def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
         B[flat] = B[flat] ^ bit
         dd = d.copy()
         dd["data_len"] = wire
-        C = torch.empty_like(A)
+        C = B if in_place else torch.empty_like(A)
         res.zero_()
         M.batch_decrypt(kt, torch.from_numpy(dd.view(np.uint8).copy()).to(dev), res, n, B, C, mean_bytes=wire)
         torch.cuda.synchronize()
@@ -348,8 +349,9 @@ def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
         assert (r["data_offset"][ok] == 0).all()
         Av, Cv = A.view(n, stride), C.view(n, stride)
         okd = torch.from_numpy(ok).to(dev)
-        for lo in range(0, n, 1 << 18):
-            hi = lo + (1 << 18)
+        step = max(1, (1 << 28) // stride)
+        for lo in range(0, n, step):
+            hi = lo + step
             same = (Av[lo:hi, :content] == Cv[lo:hi, :content]).all(dim=1)
             assert bool((same | ~okd[lo:hi]).all()), f"plaintext mismatch in rows {lo}..{hi}"
         wiped = Cv[torch.from_numpy(tam).to(dev), :inner]
@@ -357,6 +359,31 @@ def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
         del A, B, C
     finally:
         kt.close()
+        torch.cuda.empty_cache()
+
+
+def test_c4s_full_size_mixed_keys_tamper_and_evp_sample():
+    """SURVEY 8(d)-4's 1400-B variant at its stated size, as bench.py times it:
+    65 536 keys x 64 records x 1 400 B TLS 1.3, AES-256-GCM (even keys) and
+    ChaCha20-Poly1305 (odd keys), the line-grouped paired 2-lane GCM passes
+    and 2-lane ChaCha20-Poly1305."""
+    _full_size_row(1 << 16, 64, 1400, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305], 0xC45)
+
+
+def test_c3_c3d_full_size_tamper_and_evp_sample():
+    """BASELINE configs[2] (c3) at its stated size, as bench.py times it: one
+    key, 2^20 x 1 400 B TLS 1.3 ChaCha20-Poly1305, identity order, 2 lanes per
+    record (engine.hip: n / (cu x 8) >= 32).  Encrypt is c3, the tampered
+    decrypt of its output is c3d (the same launch)."""
+    _full_size_row(1, 1 << 20, 1400, [M.CIPHER_CHACHA20_POLY1305], 0xC3)
+
+
+def test_c4_full_size_mixed_keys_tamper_and_evp_sample():
+    """BASELINE configs[3] (c4) at its stated size, as bench.py times it:
+    65 536 keys x 64 records x 16 KiB TLS 1.3, AES-256-GCM (even keys) and
+    ChaCha20-Poly1305 (odd keys), the 16-lane GCM key passes and 2-lane
+    ChaCha20-Poly1305; decrypted in place (two 69 GB arenas)."""
+    _full_size_row(1 << 16, 64, 16383, [M.CIPHER_AES_256_GCM, M.CIPHER_CHACHA20_POLY1305], 0xC4, in_place=True)
 
 
 @pytest.mark.parametrize("nkeys,rpk", [(2048, 64), (4096, 32), (4096, 16)], ids=["L2", "L4", "L8"])

@@ -94,16 +94,44 @@ def test_served_records_match_oracle(cipher, ver):
     assert not errs, errs[:4]
     s1, f1, _ = _stats()
     calls = 2 * len(LENGTHS) * 3
+    why = _why()
+    # The grid's idle exit is ordered against submits (server.hip, the
+    # activity / closing handshake): a call never posts to a grid that is
+    # leaving, so nothing is withdrawn, and a call that finds the grid gone
+    # launches the next one instead of taking the launch path.
+    assert why[2] == 0, f"withdrawn requests: {why}"
+    assert f1 - f0 <= 2, ("calls went back to the launch path (batch pending, set not drained, "
+                          f"withdrawn, no slot so far: {why})")
+    assert s1 - s0 >= calls - 2, "the record server did not serve these calls"
+
+
+def _why():
     why = (ctypes.c_uint64 * 4)()
     _abi.load().tlsrec__server_why(why)
-    # A call can race the grid's idle exit (1 ms without requests, server.hip):
-    # the grid withdraws it and the call takes the launch path -- same bytes
-    # (test_server_and_launch_path_agree).  The host-side oracle work between
-    # calls sometimes exceeds the idle window, so a few such calls per 102 are
-    # expected; most must be served.
-    assert f1 - f0 <= calls // 10, ("calls went back to the launch path (batch pending, set not drained, "
-                                    f"withdrawn, no slot so far: {list(why)})")
-    assert s1 - s0 >= calls // 2, "the record server did not serve these calls"
+    return list(why)
+
+
+def test_idle_boundary_submits_are_never_withdrawn():
+    """Calls at the idle exit's boundary (TLSREC_SERVER_IDLE_MS = 0.05, gaps of
+    0..400 us between calls, 1 400-B and 16 KiB records) in a process of their
+    own (the idle limit is read once per process): every call is served by a
+    grid -- none withdrawn, none on the launch path -- the grids really leave
+    idle and are relaunched, and every record matches the oracle."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, TLSREC_SERVER_IDLE_MS="0.05")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-m", "tests._server_idle_child", "600"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["errors"] == [], r["errors"][:4]
+    assert r["why"][2] == 0, r
+    assert r["fallback"] <= 2, r
+    assert r["served"] >= r["calls"] - 2, r
+    assert r["launches"] >= 20, r      # the grids left idle and were relaunched many times
 
 
 @pytest.mark.parametrize("cipher", SERVED)
