@@ -304,6 +304,22 @@ static int gcm_pair_l_env(void)
     return (v == 2 || v == 4 || v == 8) ? v : 0;
 }
 
+/* Large records (> 4 KiB) take the paired passes below this many records per
+ * key (r05: 40; r04: 12).  With the rounds starting at each key's first
+ * position (tlsrec_gcm.h), 16 KiB records, 2^18 records (same box,
+ * profiles/r05/pair_big), 16-wave key passes -> paired 16 lanes:
+ *   records per key     16          23          32          47
+ *   GiB/s            637 -> 705  638 -> 667  667 -> 711  668 -> 654
+ * and the stream layer's 64 K connections x 16 x 16 KiB receive / send
+ * 602 -> 685 / 497 -> 542.  At 64 per key one key fills a key pass's 16
+ * waves exactly and the key passes stay (c4).  TLSREC_GCM_PAIR_BIG_MAX
+ * overrides. */
+static uint32_t gcm_pair_big_max(void)
+{
+    const char *e = getenv("TLSREC_GCM_PAIR_BIG_MAX");
+    return e ? (uint32_t) atoi(e) : 40u;
+}
+
 /* lanes per GCM record when the caller passes 0 (auto): measurement override */
 static uint32_t gcm_lanes_env(void)
 {
@@ -721,7 +737,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
             int Lp = 0;
             if (small) Lp = rpk >= 48 ? 2 : (rpk >= 24 ? 4 : 8);
             if (small && gcm_pair_l_env()) Lp = gcm_pair_l_env();     /* measurement override */
-            else if (avg_bytes > 4096 && rpk >= 4 && rpk < 12) Lp = rpk >= 8 ? 16 : 32;
+            else if (avg_bytes > 4096 && rpk >= 4 && rpk < gcm_pair_big_max()) Lp = rpk >= 8 ? 16 : 32;
             if (Lp && (uint64_t) n >= (uint64_t) cu * 16 * (uint64_t) (64 / Lp)) {
                 L = Lp;
                 wp = pair = true;

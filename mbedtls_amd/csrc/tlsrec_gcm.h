@@ -349,8 +349,16 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
         /* lanes of this wave read other lanes' E(J0): the wave's own LDS
          * writes complete before its later reads (in-order LDS queue). */
 
-        /* ---- record rounds: L lanes per record, R records per wave ---- */
-        for (uint32_t rr = 0; rr < a.rpw; rr += R) {
+        /* ---- record rounds: L lanes per record, R records per wave ----
+         * The pass's records hold a contiguous run [k0, k1] of this wave's
+         * chunk positions (positions are in key order); the rounds start at
+         * its first one (r05), so a key whose run does not begin on a multiple
+         * of R takes ceil(run / R) rounds instead of one more, half empty --
+         * with 16 KiB records, 23 per key: 3 rounds of 4 per half instead of 4 */
+        const uint64_t runm = __ballot(my_slot == s);
+        const uint32_t k0 = runm ? (uint32_t) __builtin_ctzll(runm) : 0u;
+        const uint32_t k1 = runm ? 64u - (uint32_t) __builtin_clzll(runm) : 0u;   /* one past the last */
+        for (uint32_t rr = k0; rr < k1; rr += R) {
             const uint32_t slot_in_chunk = rr + (uint32_t) g;
             const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
             const bool active = slot_in_chunk < a.rpw && owner_slot == s;

@@ -13,6 +13,7 @@ for row in "$@"; do
     dtls_small) cmd=(python3 tools/bench_dtls.py) ;;
     stream16s) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 16 --content 1400) ;;
     stream4) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 4) ;;
+    stream16) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 16) ;;
     *) cmd=(python3 bench.py --config $row --no-cpu --no-e2e --verify 16) ;;
   esac
   k=0
