@@ -8,6 +8,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <math.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -302,6 +303,54 @@ static int gcm_pair_l_env(void)
     const char *e = getenv("TLSREC_GCM_PAIR_L");
     const int v = e ? atoi(e) : 0;
     return (v == 2 || v == 4 || v == 8) ? v : 0;
+}
+
+/* Small records (<= 4 KiB) of many keys take the paired passes from 12 to
+ * this many records per key, the 16-wave key passes from there
+ * (TLSREC_GCM_PAIR_SMALL_MAX overrides; r04: 128). */
+static uint32_t gcm_pair_small_max(void)
+{
+    const char *e = getenv("TLSREC_GCM_PAIR_SMALL_MAX");
+    return e ? (uint32_t) atoi(e) : 256u;
+}
+
+/* ... and from this many (TLSREC_GCM_PAIR_SMALL_MIN overrides; r04: 12) */
+static uint32_t gcm_pair_small_min(void)
+{
+    const char *e = getenv("TLSREC_GCM_PAIR_SMALL_MIN");
+    return e ? (uint32_t) atoi(e) : 12u;
+}
+
+/* Lanes per record of the paired passes over small records, from the mean
+ * records per key (r05).  Each half of a pair takes about rpk / 2 of a key's
+ * records in rounds of R = 64 / L records, so a key pass fills
+ *     eff(L) = (rpk / 2) / (R * ceil(rpk / (2 R)))
+ * of its rounds; the L with the best eff(L) x base(L) wins, base = the
+ * full-round rates measured at 64 / 128 records per key (1 400-B AES-256-GCM,
+ * 2 : 4 : 8 lanes = 603 : 590 : 530 GiB/s).  The model against the same-box
+ * sweep (profiles/r05/small_rpk/), best measured lane count in brackets:
+ *   rpk      16  23  32  47  64  95  128  191
+ *   model     8   4   4   8   2   4    2    2
+ *   [best]    8   4   4   8   2   4    2    2
+ * r04's rule (2 from 48, 4 from 24, else 8) lost 14-29 % at 47 and 95 per
+ * key, and the 16-wave key passes it used from 128 per key 13-25 %. */
+extern "C" uint32_t tlsrec__gcm_pair_small_l(uint32_t rpk)
+{
+    static const uint32_t Ls[3] = { 2, 4, 8 };
+    static const double base[3] = { 1.0, 590.0 / 603.0, 530.0 / 603.0 };
+    double best = -1.0;
+    uint32_t bl = 8;
+    const double h = rpk / 2.0;
+    for (int i = 0; i < 3; i++) {
+        const double R = 64.0 / Ls[i];
+        const double rounds = ceil(h / R);
+        const double score = rounds > 0 ? base[i] * h / (R * rounds) : 0.0;
+        if (score > best + 1e-9) {
+            best = score;
+            bl = Ls[i];
+        }
+    }
+    return bl;
 }
 
 /* Large records (> 4 KiB) take the paired passes below this many records per
@@ -732,11 +781,14 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         /* Large records (known > 4 KiB) with 4..11 per key (k4, 16 KiB
          * streams): the same pairing at 16 or 32 lanes, 4 or 2 records of a key
          * per wave. */
+        /* (r05: small records up to 255 per key, L by the round-fill model of
+         * tlsrec__gcm_pair_small_l) */
         bool pair = false;
         if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0) {
             int Lp = 0;
-            if (small) Lp = rpk >= 48 ? 2 : (rpk >= 24 ? 4 : 8);
-            if (small && gcm_pair_l_env()) Lp = gcm_pair_l_env();     /* measurement override */
+            const bool small_pair = avg_bytes <= 4096 && rpk >= gcm_pair_small_min() && rpk < gcm_pair_small_max();
+            if (small_pair) Lp = (int) tlsrec__gcm_pair_small_l(rpk);
+            if (small_pair && gcm_pair_l_env()) Lp = gcm_pair_l_env();     /* measurement override */
             else if (avg_bytes > 4096 && rpk >= 4 && rpk < gcm_pair_big_max()) Lp = rpk >= 8 ? 16 : 32;
             if (Lp && (uint64_t) n >= (uint64_t) cu * 16 * (uint64_t) (64 / Lp)) {
                 L = Lp;

@@ -117,3 +117,18 @@ def test_no_gpu_means_loud_failure():
     assert r == M.ERR_SSL_HW_ACCEL_FAILED
     h = ctypes.c_void_p()
     assert L.tlsrec_keytab_create(ctypes.byref(h), 4) == M.ERR_SSL_HW_ACCEL_FAILED
+
+
+def test_pair_small_lane_model():
+    """the paired passes' lanes per record for small records (engine.hip
+    tlsrec__gcm_pair_small_l, a host function: no GPU needed) -- the round-fill
+    model picks the lane count that measured best at every records-per-key
+    point of the r05 sweep (profiles/r05/small_rpk/)"""
+    import ctypes
+    from mbedtls_amd import _abi
+    f = _abi.load().tlsrec__gcm_pair_small_l
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32]
+    best = {16: 8, 23: 4, 32: 4, 47: 8, 64: 2, 95: 4, 128: 2, 191: 2}
+    assert {r: f(r) for r in best} == best
+    assert all(f(r) in (2, 4, 8) for r in range(12, 256))
