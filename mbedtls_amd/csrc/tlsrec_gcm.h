@@ -227,459 +227,469 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
      * positions and its halves take them alternately, so both see the same
      * key runs */
     const int pr = wave & (W / 2 - 1), ph = wave / (W / 2);
-    /* pass membership: lane l tracks the record at chunk position k = l;
-     * its descriptor is dsrc[my_d] -- the key-ordered copy the bucket pass
-     * wrote (a.srecs, contiguous per key), or recs[] itself */
+    /* pass membership: lane l tracks the record at chunk position k = l
+     * (PAIR: of the pair's 2 rpw positions from cb); its descriptor is
+     * dsrc[my_d] -- the key-ordered copy the bucket pass wrote (a.srecs,
+     * contiguous per key), or recs[] itself.  (r05: membership and the key
+     * passes as two inlined lambdas; the G5 kernel then allocates with 20
+     * instead of 22 spilled VGPRs, 100 instead of 104 B of scratch) */
     const tlsrec_batch_rec *const dsrc = (a.perm && a.srecs) ? a.srecs + lo : a.recs;
-    uint32_t my_slot = 0xffffffffu, my_rec = 0, my_d = 0;
-    {
-        /* WP: a wave's positions are contiguous (its key runs stay together) */
-        const uint64_t pos = PAIR ? wg_base + (uint64_t) pr * 2 * a.rpw + 2 * (uint64_t) lane + (uint64_t) ph
-                             : WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
-        if (lane < (int) a.rpw && pos < count) {
-            my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
-            my_d = (a.perm && a.srecs) ? (uint32_t) pos : my_rec;
-            const uint32_t s = dsrc[my_d].slot;
-            if (TLSREC_HOOK_SKIP(my_rec, a.skip)) {
-                /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
-            } else if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
-                my_slot = s;
-            } else if (!a.perm && !(s < a.capacity && a.slots[s].km.cipher != 0)) {
-                /* identity order: this kernel is the only one that sees the record */
-                bad_slot_result(a.recs[my_rec], &a.res[my_rec]);
+    auto membership = [&](uint64_t cb, uint64_t pend, uint32_t &my_slot, uint32_t &my_rec,
+                          uint32_t &my_d) __attribute__((always_inline)) {
+        {
+            /* WP: a wave's positions are contiguous (its key runs stay together) */
+            const uint64_t pos = PAIR ? cb + 2 * (uint64_t) lane + (uint64_t) ph
+                                 : WP ? wg_base + (uint64_t) wave * a.rpw + lane : wg_base + (uint64_t) lane * W + wave;
+            if (lane < (int) a.rpw && pos < pend) {
+                my_rec = a.perm ? a.perm[lo + pos] : (uint32_t) pos;
+                my_d = (a.perm && a.srecs) ? (uint32_t) pos : my_rec;
+                const uint32_t s = dsrc[my_d].slot;
+                if (TLSREC_HOOK_SKIP(my_rec, a.skip)) {
+                    /* test hook: an unreached record keeps the guard's INTERNAL_ERROR */
+                } else if (s < a.capacity && a.slots[s].km.cipher == a.cipher) {
+                    my_slot = s;
+                } else if (!a.perm && !(s < a.capacity && a.slots[s].km.cipher != 0)) {
+                    /* identity order: this kernel is the only one that sees the record */
+                    bad_slot_result(a.recs[my_rec], &a.res[my_rec]);
+                }
             }
         }
-    }
-    if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
-    if (PAIR && tid >= 4 && tid < 32) ctl[tid] = 0;     /* pair minima [4, 20), barrier counters [20, 28) */
-    __syncthreads();
-
+    };
+    /* the key passes over the lanes' positions */
     /* Horner multiplier table H^L (hor) and the per-record tables H^1..H^(L/2) (gp) */
     constexpr int HPI = WP ? 0 : LOGL;                   /* H^L table index from hor */
     const uint8_t *hor = WP ? lds + LY::GH + (PAIR ? pr : wave) * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
     uint32_t phase = 0;                                  /* PAIR barrier count */
-    for (int iter = 0;; iter++) {
-        uint32_t s;
-        if constexpr (PAIR) {
-            /* the pair's smallest pending slot: both halves agree on it, stage
-             * half of its H^L table each, and meet before the table is used
-             * (the first barrier also tells the pair the previous table is no
-             * longer read) */
-            uint32_t *pmin = ctl + 4 + 2 * pr;
-            uint32_t *pcnt = ctl + 20 + pr;
-            const uint32_t m = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
-            if (lane == 0) pmin[ph] = m;
-            pair_sync(pcnt, phase, lane);
-            s = __builtin_amdgcn_readfirstlane(min(pmin[0], pmin[1]));
-            if (s == 0xffffffffu) break;
-            if (a.tm & 16u) {
-                /* built from H^L itself (tm bit 4, r05): one 16-byte read of
-                 * the key's powers instead of 8 KiB of table per key pass */
-                gtab4_build_half(const_cast<uint8_t *>(hor), a.ghtab + (size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1),
-                                 lane, ph);
-            } else {
+    auto passes = [&](uint32_t my_slot, uint32_t my_rec, uint32_t my_d) __attribute__((always_inline)) {
+        for (int iter = 0;; iter++) {
+            uint32_t s;
+            if constexpr (PAIR) {
+                /* the pair's smallest pending slot: both halves agree on it, stage
+                 * half of its H^L table each, and meet before the table is used
+                 * (the first barrier also tells the pair the previous table is no
+                 * longer read) */
+                uint32_t *pmin = ctl + 4 + 2 * pr;
+                uint32_t *pcnt = ctl + 20 + pr;
+                const uint32_t m = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
+                if (lane == 0) pmin[ph] = m;
+                pair_sync(pcnt, phase, lane);
+                s = __builtin_amdgcn_readfirstlane(min(pmin[0], pmin[1]));
+                if (s == 0xffffffffu) break;
+                if (a.tm & 16u) {
+                    /* built from H^L itself (tm bit 4, r05): one 16-byte read of
+                     * the key's powers instead of 8 KiB of table per key pass */
+                    gtab4_build_half(const_cast<uint8_t *>(hor), a.ghtab + (size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1),
+                                     lane, ph);
+                } else {
+                    const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
+                    uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
+                    for (int i = lane + ph * 256; i < (ph + 1) * 256; i += 64) dst[i] = src[i];
+                }
+                pair_sync(pcnt, phase, lane);
+            } else if constexpr (WP) {
+                /* wave pass: the wave's smallest pending slot; stage its H^L table
+                 * into the wave's LDS (in-order LDS queue: the wave's writes land
+                 * before its reads; the asm keeps the compiler from hoisting) */
+                s = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
+                if (s == 0xffffffffu) break;
                 const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
                 uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
-                for (int i = lane + ph * 256; i < (ph + 1) * 256; i += 64) dst[i] = src[i];
-            }
-            pair_sync(pcnt, phase, lane);
-        } else if constexpr (WP) {
-            /* wave pass: the wave's smallest pending slot; stage its H^L table
-             * into the wave's LDS (in-order LDS queue: the wave's writes land
-             * before its reads; the asm keeps the compiler from hoisting) */
-            s = __builtin_amdgcn_readfirstlane(wave_min(my_slot));
-            if (s == 0xffffffffu) break;
-            const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS + LOGL * 512;
-            uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(hor));
-            for (int i = lane; i < 512; i += 64) dst[i] = src[i];
-            asm volatile("" ::: "memory");
-        } else {
-            uint32_t *cur = &ctl[iter & 1];
-            if (my_slot != 0xffffffffu) atomicMin(cur, my_slot);
-            __syncthreads();
-            s = __builtin_amdgcn_readfirstlane(*cur);
-            if (s == 0xffffffffu) break;
-            if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
-            /* stage the slot's GHASH tables and round keys -- with lane powers
-             * (tm bit 3) only the Horner multiplier's: the tree tables H^1 ..
-             * H^(L/2) are not read (G5: its 13 KiB table alone; 4-bit: H^L) */
-            {
-                const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
-                uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
-                const int t0 = (WP && !CID && (a.tm & 8u)) ? (G5 ? LY::NT : LY::NT - 1) : 0;
-                for (int i = tid + t0 * 512; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
-                if constexpr (G5) {
-                    uint4 *d5 = reinterpret_cast<uint4 *>(lds + LY::HG5);
-                    for (int i = tid; i < KEY_G5_WORDS; i += NTHR) d5[i] = src[KEY_G5_OFF + i];
-                }
-            }
-            __syncthreads();
-        }
-        const uint8_t *gp = WP ? reinterpret_cast<const uint8_t *>(a.ghtab + (size_t) s * KEY_TABLE_WORDS) : lds + LY::GH;
-        /* H as a value (wave passes, tm bit 2): the AAD fold and the final multiplies */
-        uint4 h1v = make_uint4(0, 0, 0, 0);
-        if constexpr (WP)
-            if (a.tm & 4u) __builtin_memcpy(&h1v, a.slots[s].h, 16);
-        /* Round keys through the constant address space: scalar loads.  (Read
-         * through a.slots they compile to vector loads + vmcnt(0) waits in
-         * every round, since the kernel's own stores might alias the table.) */
-        const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) (ARIA ? a.slots[s].ark : a.slots[s].rkr);
-        const tlsrec_key_material km = a.slots[s].km;
-
-        /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
-        {
-            uint4 ej0 = make_uint4(0, 0, 0, 0);
-            bool mine = my_slot == s;
-            uint32_t nw[3] = { 0, 0, 0 };
-            if (mine) {
-                const tlsrec_batch_rec d = dsrc[my_d];
-                tlsrec_plan p;
-                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
-                nonce_words<DEC>(p, d, km, a.in, nw);
-                /* only this pass's records: with many keys of few records
-                 * each, most of a wave's 64 positions belong to other passes
-                 * (masked lanes issue no table reads) */
-                if constexpr (ARIA)
-                    ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
-                else
-                    ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
-            }
-            reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
-        }
-        /* lanes of this wave read other lanes' E(J0): the wave's own LDS
-         * writes complete before its later reads (in-order LDS queue). */
-
-        /* ---- record rounds: L lanes per record, R records per wave ----
-         * The pass's records hold a contiguous run [k0, k1] of this wave's
-         * chunk positions (positions are in key order); the rounds start at
-         * its first one (r05), so a key whose run does not begin on a multiple
-         * of R takes ceil(run / R) rounds instead of one more, half empty --
-         * with 16 KiB records, 23 per key: 3 rounds of 4 per half instead of 4 */
-        const uint64_t runm = __ballot(my_slot == s);
-        const uint32_t k0 = runm ? (uint32_t) __builtin_ctzll(runm) : 0u;
-        const uint32_t k1 = runm ? 64u - (uint32_t) __builtin_clzll(runm) : 0u;   /* one past the last */
-        for (uint32_t rr = k0; rr < k1; rr += R) {
-            const uint32_t slot_in_chunk = rr + (uint32_t) g;
-            const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
-            const bool active = slot_in_chunk < a.rpw && owner_slot == s;
-            /* a key's records sit in a contiguous run of each wave's chunk
-             * positions: rounds holding none of them are skipped (wave-uniform,
-             * no barrier inside the round) -- with many keys of few records
-             * each, the pass would otherwise walk all rpw positions */
-            if (__ballot(active) == 0) continue;
-            const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
-            const uint64_t didx = (uint32_t) __shfl((int) my_d, (int) slot_in_chunk & 63);
-            /* Only what the AEAD loop needs stays live across it; the plan is
-             * re-derived from the (cached) descriptor afterwards. */
-            GcmJob jb;
-            jb.run = false;
-            if (active) {
-                const tlsrec_batch_rec d = dsrc[didx];
-                tlsrec_plan p;
-                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
-                if (p.status != 0) {
-                    if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
-                } else {
-                    jb.setup<DEC>(p, d, km, a.in, a.out);
-                    /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
-                     * into the block the AAD fold multiplies by H below */
-                    if (CID && p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
-                }
-            }
-            const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
-            const uint32_t mm = m ? m : 1;
-            constexpr uint32_t BL = (uint32_t) (B * L);
-            /* Lane powers (tm bit 3; not with CIDs): the whole GHASH input A, C_1 ..
-             * C_m, LEN in the lane layout -- C_1 at position 0 (line-aligned, no
-             * front padding), LEN at position m, and A at position -1, i.e. the
-             * block lane L-1's chain holds before its first one (its Xp starts
-             * as A: no step, no multiply).  A lane's chain stops at the record's
-             * end, so lane q's Horner sum needs one multiply, by H^(d+1) with d
-             * = (m - q) mod L its last block's distance to LEN (the key's powers
-             * as values, KEY_HPOW_OFF), and an XOR over the record's lanes gives
-             * GHASH: no AAD fold, no lane tree, no final multiplies (8 sequential
-             * multiplies per record at L = 32 before, 4 at L = 2). */
-            /* (m a multiple of BL: LEN would open a step of its own; lane 0
-             * takes it at the tail instead, Y_0 = Y_0 H^L + LEN, one multiply) */
-            /* wave passes only: as a run-time flag in the 16-wave key-pass
-             * kernels it cost c2 5 % with the flag off (the hot loop carries
-             * the LEN position test and its registers; same box, r04p/q:
-             * 737 -> 700 GiB/s), and on it was no faster (r04e) */
-            const bool lp = WP && !CID && (a.tm & 8u);
-            const bool lenx = lp && m % BL == 0;
-            const uint32_t z = lp ? 0u : (BL - mm % BL) % BL;           /* front padding: position of C_1 */
-            const uint32_t J = jb.run ? (lp ? (lenx ? m / BL : (m + BL) / BL) : (mm + z) / BL) : 0;
-            const uint32_t Jmax = wave_max(J);
-            /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
-             * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
-             * only the step with cc == 0 reads it. */
-            uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + (PAIR ? wave * LY::FOLDN + g : wave * 64 + lane);
-            /* the lane that holds block 0 (cc == 0) */
-            if (!lp && jb.run && (uint32_t) q == z % L) {
-                uint4 f = jb.aadw;
-                if (m) {
-                    if constexpr (WP)   /* tm bit 2: by H as a value -- the key's H^1 table is 8 KiB of
-                                         * global memory, and a multiply touches 32 lines of it */
-                        f = (a.tm & 4u) ? gf_mul_v(f, h1v) : gmul<0>(gp, f);
-                    else
-                        f = gmul<0>(gp, f);
-                }
-                *fold = f;
-            }
-            /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
-             * does not depend on step j's keystream, so its table reads share
-             * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
-            uint4 Z = make_uint4(0, 0, 0, 0), Xp = make_uint4(0, 0, 0, 0);
-            if (lp && jb.run && q == L - 1) Xp = jb.aadw;              /* A: position -1, lane L-1's chain */
-            /* TLS 1.3 inner type: position + 1 of the last non-zero output block */
-            uint32_t nzpos = 0;
-            /* a readable 16-byte address for lanes with nothing to load */
-            const uint8_t *safe = jb.run ? jb.src : reinterpret_cast<const uint8_t *>(a.recs);
-            /* Body steps [1, jh): every lane of the wave holds a full, aligned
-             * block inside its record's content (wave-uniform bound), so they run
-             * without masks or branches.  Step 0 (AAD fold, front padding) and
-             * the tail (partial blocks, ragged lengths) take the general step. */
-            uint32_t jh = 0;
-            {
-                const uint32_t mfast = (jb.run && jb.aligned) ? jb.content_len / 16 : 0;
-                uint32_t h = jb.run ? (mfast + z) / BL : 0;
-                h = wave_min(h);
-                jh = h > 1 ? h : 0;
-            }
-            const uint32_t jl = jh ? 1u : Jmax;
-            auto steps = [&](auto cached) {
-                constexpr bool CACHED = decltype(cached)::value;
-                CtrCache ccache;
-                if constexpr (CACHED) ccache = ctr_cache<LY::AES>(lds, lanebase, rk, jb.nw0, jb.nw1, jb.nw2);
-                auto crypt = [&](int32_t cc, uint4 y, uint4 &ks, uint4 &Zn) {
-                    const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
-                    if constexpr (CACHED) {
-                        aes_ghash<NR, LY::AES, HPI, 2, 1, G5>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
-                    } else {
-                        if constexpr (ARIA)
-                            ks = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
-                        else
-                            ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
-                        if constexpr (G5)
-                            Zn = gmul5(hor, y);
-                        else
-                            Zn = gmul<HPI>(hor, y);
-                    }
-                };
-                auto general = [&](uint32_t j) {
-                    const bool live = jb.run && j < J;
-#pragma unroll
-                    for (int b = 0; b < B; b++) {
-                        const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
-                        const bool valid = live && cc >= 0 && (uint32_t) cc < m;
-                        const uint32_t pos = (uint32_t) cc * 16;
-                        /* full, aligned interior block: plain 16-byte load/store */
-                        const bool fast = valid && jb.aligned && pos + 16 <= jb.content_len;
-                        uint4 blk = gload16(fast ? jb.src + pos : safe);
-                        uint4 ks, Zn;
-                        crypt(cc, xor4(Z, Xp), ks, Zn);
-                        uint4 X = make_uint4(0, 0, 0, 0);
-                        if (fast) {
-                            const uint4 o = xor4(blk, ks);
-                            gstore16(jb.dst + pos, o);
-                            X = DEC ? blk : o;
-                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
-                        } else if (valid) {
-                            blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type, jb.aligned);
-                            const uint4 o = mask_block(xor4(blk, ks), pos, jb.aead_len);
-                            store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
-                            X = DEC ? blk : o;
-                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
-                        }
-                        if (lp) {
-                            if (cc == (int32_t) m)
-                                X = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
-                            if (live && cc <= (int32_t) m) { Z = Zn; Xp = X; }    /* the chain ends at LEN */
-                        } else {
-                            if (live && cc == 0) X = xor4(X, *fold);
-                            if (live) { Z = Zn; Xp = X; }
-                        }
-                    }
-                };
-                uint32_t j = 0;
-                for (; j < jl; j++) general(j);
+                for (int i = lane; i < 512; i += 64) dst[i] = src[i];
+                asm volatile("" ::: "memory");
+            } else {
+                uint32_t *cur = &ctl[iter & 1];
+                if (my_slot != 0xffffffffu) atomicMin(cur, my_slot);
+                __syncthreads();
+                s = __builtin_amdgcn_readfirstlane(*cur);
+                if (s == 0xffffffffu) break;
+                if (tid == 0) ctl[(iter + 1) & 1] = 0xffffffffu;
+                /* stage the slot's GHASH tables and round keys -- with lane powers
+                 * (tm bit 3) only the Horner multiplier's: the tree tables H^1 ..
+                 * H^(L/2) are not read (G5: its 13 KiB table alone; 4-bit: H^L) */
                 {
-                    const uint8_t *sp = jb.src + (size_t) (BL * j + q - z) * 16;
-                    uint8_t *dp = jb.dst + (size_t) (BL * j + q - z) * 16;
-                    /* 2 / 4 lanes per record (the paired passes over small
-                     * records): a record's 128-byte line spans G = 128 / (16 L)
-                     * steps, and 32 records per wave keep 4 MiB of such lines
-                     * live per XCD -- the L2's size -- so lines were fetched
-                     * and written back part-used.  Load G steps' blocks
-                     * together and store them together: each line is touched
-                     * once per direction. */
-                    if constexpr (PAIR && L <= 4 && B == 1 && TLSREC_GCM_LINE_GROUPS) {
-                        constexpr int G = 128 / (16 * L);
-                        /* single steps up to a group boundary: groups then
-                         * start on a line for records without front padding
-                         * (z = 0: whole-block AEAD lengths, 128-byte slots) */
-                        for (; j < jh && j % G != 0; j++) {
-                            const int32_t cc = (int32_t) (BL * j + q) - (int32_t) z;
-                            const uint4 blk = gload16(sp);
+                    const uint4 *src = a.ghtab + (size_t) s * KEY_TABLE_WORDS;
+                    uint4 *dst = reinterpret_cast<uint4 *>(lds + LY::GH);
+                    const int t0 = (WP && !CID && (a.tm & 8u)) ? (G5 ? LY::NT : LY::NT - 1) : 0;
+                    for (int i = tid + t0 * 512; i < LY::NT * 512; i += NTHR) dst[i] = src[i];
+                    if constexpr (G5) {
+                        uint4 *d5 = reinterpret_cast<uint4 *>(lds + LY::HG5);
+                        for (int i = tid; i < KEY_G5_WORDS; i += NTHR) d5[i] = src[KEY_G5_OFF + i];
+                    }
+                }
+                __syncthreads();
+            }
+            const uint8_t *gp = WP ? reinterpret_cast<const uint8_t *>(a.ghtab + (size_t) s * KEY_TABLE_WORDS) : lds + LY::GH;
+            /* H as a value (wave passes, tm bit 2): the AAD fold and the final multiplies */
+            uint4 h1v = make_uint4(0, 0, 0, 0);
+            if constexpr (WP)
+                if (a.tm & 4u) __builtin_memcpy(&h1v, a.slots[s].h, 16);
+            /* Round keys through the constant address space: scalar loads.  (Read
+             * through a.slots they compile to vector loads + vmcnt(0) waits in
+             * every round, since the kernel's own stores might alias the table.) */
+            const kconst_u32 *rk = (const kconst_u32 *) (uintptr_t) (ARIA ? a.slots[s].ark : a.slots[s].rkr);
+            const tlsrec_key_material km = a.slots[s].km;
+
+            /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
+            {
+                uint4 ej0 = make_uint4(0, 0, 0, 0);
+                bool mine = my_slot == s;
+                uint32_t nw[3] = { 0, 0, 0 };
+                if (mine) {
+                    const tlsrec_batch_rec d = dsrc[my_d];
+                    tlsrec_plan p;
+                    make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+                    nonce_words<DEC>(p, d, km, a.in, nw);
+                    /* only this pass's records: with many keys of few records
+                     * each, most of a wave's 64 positions belong to other passes
+                     * (masked lanes issue no table reads) */
+                    if constexpr (ARIA)
+                        ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+                    else
+                        ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+                }
+                reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
+            }
+            /* lanes of this wave read other lanes' E(J0): the wave's own LDS
+             * writes complete before its later reads (in-order LDS queue). */
+
+            /* ---- record rounds: L lanes per record, R records per wave ----
+             * The pass's records hold a contiguous run [k0, k1] of this wave's
+             * chunk positions (positions are in key order); the rounds start at
+             * its first one (r05), so a key whose run does not begin on a multiple
+             * of R takes ceil(run / R) rounds instead of one more, half empty --
+             * with 16 KiB records, 23 per key: 3 rounds of 4 per half instead of 4 */
+            const uint64_t runm = __ballot(my_slot == s);
+            const uint32_t k0 = runm ? (uint32_t) __builtin_ctzll(runm) : 0u;
+            const uint32_t k1 = runm ? 64u - (uint32_t) __builtin_clzll(runm) : 0u;   /* one past the last */
+            for (uint32_t rr = k0; rr < k1; rr += R) {
+                const uint32_t slot_in_chunk = rr + (uint32_t) g;
+                const uint32_t owner_slot = __shfl(my_slot, (int) slot_in_chunk & 63);
+                const bool active = slot_in_chunk < a.rpw && owner_slot == s;
+                /* a key's records sit in a contiguous run of each wave's chunk
+                 * positions: rounds holding none of them are skipped (wave-uniform,
+                 * no barrier inside the round) -- with many keys of few records
+                 * each, the pass would otherwise walk all rpw positions */
+                if (__ballot(active) == 0) continue;
+                const uint64_t ridx = (uint32_t) __shfl((int) my_rec, (int) slot_in_chunk & 63);
+                const uint64_t didx = (uint32_t) __shfl((int) my_d, (int) slot_in_chunk & 63);
+                /* Only what the AEAD loop needs stays live across it; the plan is
+                 * re-derived from the (cached) descriptor afterwards. */
+                GcmJob jb;
+                jb.run = false;
+                if (active) {
+                    const tlsrec_batch_rec d = dsrc[didx];
+                    tlsrec_plan p;
+                    make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+                    if (p.status != 0) {
+                        if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
+                    } else {
+                        jb.setup<DEC>(p, d, km, a.in, a.out);
+                        /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
+                         * into the block the AAD fold multiplies by H below */
+                        if (CID && p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
+                    }
+                }
+                const uint32_t m = jb.run ? (jb.aead_len + 15) >> 4 : 0;   /* GHASH C blocks */
+                const uint32_t mm = m ? m : 1;
+                constexpr uint32_t BL = (uint32_t) (B * L);
+                /* Lane powers (tm bit 3; not with CIDs): the whole GHASH input A, C_1 ..
+                 * C_m, LEN in the lane layout -- C_1 at position 0 (line-aligned, no
+                 * front padding), LEN at position m, and A at position -1, i.e. the
+                 * block lane L-1's chain holds before its first one (its Xp starts
+                 * as A: no step, no multiply).  A lane's chain stops at the record's
+                 * end, so lane q's Horner sum needs one multiply, by H^(d+1) with d
+                 * = (m - q) mod L its last block's distance to LEN (the key's powers
+                 * as values, KEY_HPOW_OFF), and an XOR over the record's lanes gives
+                 * GHASH: no AAD fold, no lane tree, no final multiplies (8 sequential
+                 * multiplies per record at L = 32 before, 4 at L = 2). */
+                /* (m a multiple of BL: LEN would open a step of its own; lane 0
+                 * takes it at the tail instead, Y_0 = Y_0 H^L + LEN, one multiply) */
+                /* wave passes only: as a run-time flag in the 16-wave key-pass
+                 * kernels it cost c2 5 % with the flag off (the hot loop carries
+                 * the LEN position test and its registers; same box, r04p/q:
+                 * 737 -> 700 GiB/s), and on it was no faster (r04e) */
+                const bool lp = WP && !CID && (a.tm & 8u);
+                const bool lenx = lp && m % BL == 0;
+                const uint32_t z = lp ? 0u : (BL - mm % BL) % BL;           /* front padding: position of C_1 */
+                const uint32_t J = jb.run ? (lp ? (lenx ? m / BL : (m + BL) / BL) : (mm + z) / BL) : 0;
+                const uint32_t Jmax = wave_max(J);
+                /* AAD folded into the first ciphertext block: X(C_0) ^= AAD*H (or
+                 * X = AAD when there is no ciphertext); kept in LDS, not VGPRs --
+                 * only the step with cc == 0 reads it. */
+                uint4 *fold = reinterpret_cast<uint4 *>(lds + LY::FOLD) + (PAIR ? wave * LY::FOLDN + g : wave * 64 + lane);
+                /* the lane that holds block 0 (cc == 0) */
+                if (!lp && jb.run && (uint32_t) q == z % L) {
+                    uint4 f = jb.aadw;
+                    if (m) {
+                        if constexpr (WP)   /* tm bit 2: by H as a value -- the key's H^1 table is 8 KiB of
+                                             * global memory, and a multiply touches 32 lines of it */
+                            f = (a.tm & 4u) ? gf_mul_v(f, h1v) : gmul<0>(gp, f);
+                        else
+                            f = gmul<0>(gp, f);
+                    }
+                    *fold = f;
+                }
+                /* Pipelined Horner: step j computes Z = (Z ^ X_(j-1)) * H^L, which
+                 * does not depend on step j's keystream, so its table reads share
+                 * the AES rounds' phases (aes_ghash); after the loop Y = Z ^ X_last. */
+                uint4 Z = make_uint4(0, 0, 0, 0), Xp = make_uint4(0, 0, 0, 0);
+                if (lp && jb.run && q == L - 1) Xp = jb.aadw;              /* A: position -1, lane L-1's chain */
+                /* TLS 1.3 inner type: position + 1 of the last non-zero output block */
+                uint32_t nzpos = 0;
+                /* a readable 16-byte address for lanes with nothing to load */
+                const uint8_t *safe = jb.run ? jb.src : reinterpret_cast<const uint8_t *>(a.recs);
+                /* Body steps [1, jh): every lane of the wave holds a full, aligned
+                 * block inside its record's content (wave-uniform bound), so they run
+                 * without masks or branches.  Step 0 (AAD fold, front padding) and
+                 * the tail (partial blocks, ragged lengths) take the general step. */
+                uint32_t jh = 0;
+                {
+                    const uint32_t mfast = (jb.run && jb.aligned) ? jb.content_len / 16 : 0;
+                    uint32_t h = jb.run ? (mfast + z) / BL : 0;
+                    h = wave_min(h);
+                    jh = h > 1 ? h : 0;
+                }
+                const uint32_t jl = jh ? 1u : Jmax;
+                auto steps = [&](auto cached) {
+                    constexpr bool CACHED = decltype(cached)::value;
+                    CtrCache ccache;
+                    if constexpr (CACHED) ccache = ctr_cache<LY::AES>(lds, lanebase, rk, jb.nw0, jb.nw1, jb.nw2);
+                    auto crypt = [&](int32_t cc, uint4 y, uint4 &ks, uint4 &Zn) {
+                        const uint32_t ctrw = bswap32((uint32_t) cc + 2u);
+                        if constexpr (CACHED) {
+                            aes_ghash<NR, LY::AES, HPI, 2, 1, G5>(lds, hor, lanebase, rk, ccache, ctrw, y, ks, Zn);
+                        } else {
+                            if constexpr (ARIA)
+                                ks = alt_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                            else
+                                ks = aes_encrypt<NR, LY::AES>(lds, lanebase, rk, make_uint4(jb.nw0, jb.nw1, jb.nw2, ctrw));
+                            if constexpr (G5)
+                                Zn = gmul5(hor, y);
+                            else
+                                Zn = gmul<HPI>(hor, y);
+                        }
+                    };
+                    auto general = [&](uint32_t j) {
+                        const bool live = jb.run && j < J;
+    #pragma unroll
+                        for (int b = 0; b < B; b++) {
+                            const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                            const bool valid = live && cc >= 0 && (uint32_t) cc < m;
+                            const uint32_t pos = (uint32_t) cc * 16;
+                            /* full, aligned interior block: plain 16-byte load/store */
+                            const bool fast = valid && jb.aligned && pos + 16 <= jb.content_len;
+                            uint4 blk = gload16(fast ? jb.src + pos : safe);
                             uint4 ks, Zn;
                             crypt(cc, xor4(Z, Xp), ks, Zn);
-                            const uint4 o = xor4(blk, ks);
-                            gstore16(dp, o);
-                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
-                            Z = Zn;
-                            Xp = DEC ? blk : o;
+                            uint4 X = make_uint4(0, 0, 0, 0);
+                            if (fast) {
+                                const uint4 o = xor4(blk, ks);
+                                gstore16(jb.dst + pos, o);
+                                X = DEC ? blk : o;
+                                if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                            } else if (valid) {
+                                blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type, jb.aligned);
+                                const uint4 o = mask_block(xor4(blk, ks), pos, jb.aead_len);
+                                store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
+                                X = DEC ? blk : o;
+                                if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
+                            }
+                            if (lp) {
+                                if (cc == (int32_t) m)
+                                    X = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
+                                if (live && cc <= (int32_t) m) { Z = Zn; Xp = X; }    /* the chain ends at LEN */
+                            } else {
+                                if (live && cc == 0) X = xor4(X, *fold);
+                                if (live) { Z = Zn; Xp = X; }
+                            }
+                        }
+                    };
+                    uint32_t j = 0;
+                    for (; j < jl; j++) general(j);
+                    {
+                        const uint8_t *sp = jb.src + (size_t) (BL * j + q - z) * 16;
+                        uint8_t *dp = jb.dst + (size_t) (BL * j + q - z) * 16;
+                        /* 2 / 4 lanes per record (the paired passes over small
+                         * records): a record's 128-byte line spans G = 128 / (16 L)
+                         * steps, and 32 records per wave keep 4 MiB of such lines
+                         * live per XCD -- the L2's size -- so lines were fetched
+                         * and written back part-used.  Load G steps' blocks
+                         * together and store them together: each line is touched
+                         * once per direction. */
+                        if constexpr (PAIR && L <= 4 && B == 1 && TLSREC_GCM_LINE_GROUPS) {
+                            constexpr int G = 128 / (16 * L);
+                            /* single steps up to a group boundary: groups then
+                             * start on a line for records without front padding
+                             * (z = 0: whole-block AEAD lengths, 128-byte slots) */
+                            for (; j < jh && j % G != 0; j++) {
+                                const int32_t cc = (int32_t) (BL * j + q) - (int32_t) z;
+                                const uint4 blk = gload16(sp);
+                                uint4 ks, Zn;
+                                crypt(cc, xor4(Z, Xp), ks, Zn);
+                                const uint4 o = xor4(blk, ks);
+                                gstore16(dp, o);
+                                if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
+                                Z = Zn;
+                                Xp = DEC ? blk : o;
+                                sp += 16 * BL;
+                                dp += 16 * BL;
+                            }
+                            for (; j + G <= jh; j += G) {
+                                uint4 blk[G], out[G];
+    #pragma unroll
+                                for (int t = 0; t < G; t++) blk[t] = gload16(sp + 16 * BL * t);
+    #pragma unroll
+                                for (int t = 0; t < G; t++) {
+                                    const int32_t cc = (int32_t) (BL * (j + t) + q) - (int32_t) z;
+                                    uint4 ks, Zn;
+                                    crypt(cc, xor4(Z, Xp), ks, Zn);
+                                    out[t] = xor4(blk[t], ks);
+                                    if (DEC && jb.inner && (out[t].x | out[t].y | out[t].z | out[t].w))
+                                        nzpos = (uint32_t) cc * 16 + 1;
+                                    Z = Zn;
+                                    Xp = DEC ? blk[t] : out[t];
+                                }
+    #pragma unroll
+                                for (int t = 0; t < G; t++) gstore16(dp + 16 * BL * t, out[t]);
+                                sp += 16 * BL * G;
+                                dp += 16 * BL * G;
+                            }
+                        }
+                        for (; j < jh; j++) {
+    #pragma unroll
+                            for (int b = 0; b < B; b++) {
+                                const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
+                                const uint4 blk = gload16(sp + 16 * L * b);
+                                uint4 ks, Zn;
+                                crypt(cc, xor4(Z, Xp), ks, Zn);
+                                const uint4 o = xor4(blk, ks);
+                                gstore16(dp + 16 * L * b, o);
+                                if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
+                                Z = Zn;
+                                Xp = DEC ? blk : o;
+                            }
                             sp += 16 * BL;
                             dp += 16 * BL;
                         }
-                        for (; j + G <= jh; j += G) {
-                            uint4 blk[G], out[G];
-#pragma unroll
-                            for (int t = 0; t < G; t++) blk[t] = gload16(sp + 16 * BL * t);
-#pragma unroll
-                            for (int t = 0; t < G; t++) {
-                                const int32_t cc = (int32_t) (BL * (j + t) + q) - (int32_t) z;
-                                uint4 ks, Zn;
-                                crypt(cc, xor4(Z, Xp), ks, Zn);
-                                out[t] = xor4(blk[t], ks);
-                                if (DEC && jb.inner && (out[t].x | out[t].y | out[t].z | out[t].w))
-                                    nzpos = (uint32_t) cc * 16 + 1;
-                                Z = Zn;
-                                Xp = DEC ? blk[t] : out[t];
-                            }
-#pragma unroll
-                            for (int t = 0; t < G; t++) gstore16(dp + 16 * BL * t, out[t]);
-                            sp += 16 * BL * G;
-                            dp += 16 * BL * G;
-                        }
                     }
-                    for (; j < jh; j++) {
-#pragma unroll
-                        for (int b = 0; b < B; b++) {
-                            const int32_t cc = (int32_t) (BL * j + L * b + q) - (int32_t) z;
-                            const uint4 blk = gload16(sp + 16 * L * b);
-                            uint4 ks, Zn;
-                            crypt(cc, xor4(Z, Xp), ks, Zn);
-                            const uint4 o = xor4(blk, ks);
-                            gstore16(dp + 16 * L * b, o);
-                            if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = (uint32_t) cc * 16 + 1;
-                            Z = Zn;
-                            Xp = DEC ? blk : o;
-                        }
-                        sp += 16 * BL;
-                        dp += 16 * BL;
-                    }
+                    for (; j < Jmax; j++) general(j);
+                };
+                /* counters stay below 2^16 (any TLS record): cached rounds 1-2 */
+                if constexpr (ARIA) {
+                    steps(std::integral_constant<bool, false>());   /* no cached rounds for ARIA */
+                } else {
+                    if (wave_max(m) + 2 < 65536u)
+                        steps(std::integral_constant<bool, true>());
+                    else
+                        steps(std::integral_constant<bool, false>());
                 }
-                for (; j < Jmax; j++) general(j);
-            };
-            /* counters stay below 2^16 (any TLS record): cached rounds 1-2 */
-            if constexpr (ARIA) {
-                steps(std::integral_constant<bool, false>());   /* no cached rounds for ARIA */
-            } else {
-                if (wave_max(m) + 2 < 65536u)
-                    steps(std::integral_constant<bool, true>());
-                else
-                    steps(std::integral_constant<bool, false>());
-            }
-            uint4 Y = xor4(Z, Xp);
-            /* lane powers: this lane's H^(L - q), read while the tail runs */
-            uint4 hq = make_uint4(0, 0, 0, 0), hl = make_uint4(0, 0, 0, 0);
-            if (lp) hq = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (m + (uint32_t) (L - q)) % L];
-            if (lenx && q == 0) hl = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1)];
-            uint32_t nzkey = 0;
-            if (DEC && jb.inner && nzpos) {
-                /* the lane's last non-zero plaintext block, as written above */
-                const uint32_t pos = nzpos - 1;
-                nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
-            }
-            /* tree: sum_q Y_q H^(L-q) */
-            /* L = 8 and 32 (the paired passes of DTLS / stream records, 16 per
-             * key, and of k4) too: their tree read the key's H^1 .. H^16 tables
-             * from HBM, 8 KiB each, for a handful of records per key */
-            if (lp) {
-                if (__ballot(lenx && q == 0))                        /* LEN after a whole last step */
-                    if (lenx && q == 0)
-                        Y = xor4(gf_mul_v(Y, hl), make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8)));
-                Y = group_xor4<L>(gf_mul_v(Y, hq));                  /* GHASH, in every lane of the record */
-            } else if constexpr (WP && L >= 2 && L <= 32) {
-                if (a.tm & (L == 16 ? 1u : 2u)) {
-                    const SlotState &ss = a.slots[s];
-                    uint4 h1;
-                    __builtin_memcpy(&h1, ss.h, 16);                 /* H: bytes at a 4-byte-aligned offset */
-                    const uint4 P[5] = { h1,
-                                         make_uint4(ss.hpow[0][0], ss.hpow[0][1], ss.hpow[0][2], ss.hpow[0][3]),
-                                         make_uint4(ss.hpow[1][0], ss.hpow[1][1], ss.hpow[1][2], ss.hpow[1][3]),
-                                         make_uint4(ss.hpow[2][0], ss.hpow[2][1], ss.hpow[2][2], ss.hpow[2][3]),
-                                         make_uint4(ss.hpow[3][0], ss.hpow[3][1], ss.hpow[3][2], ss.hpow[3][3]) };
-                    Y = gtree_v<L / 2>(P, Y, lane, q);
+                uint4 Y = xor4(Z, Xp);
+                /* lane powers: this lane's H^(L - q), read while the tail runs */
+                uint4 hq = make_uint4(0, 0, 0, 0), hl = make_uint4(0, 0, 0, 0);
+                if (lp) hq = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (m + (uint32_t) (L - q)) % L];
+                if (lenx && q == 0) hl = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1)];
+                uint32_t nzkey = 0;
+                if (DEC && jb.inner && nzpos) {
+                    /* the lane's last non-zero plaintext block, as written above */
+                    const uint32_t pos = nzpos - 1;
+                    nzkey = last_nonzero_key(load_block(jb.dst, pos, jb.aead_len, jb.aead_len, 0, false), pos);
+                }
+                /* tree: sum_q Y_q H^(L-q) */
+                /* L = 8 and 32 (the paired passes of DTLS / stream records, 16 per
+                 * key, and of k4) too: their tree read the key's H^1 .. H^16 tables
+                 * from HBM, 8 KiB each, for a handful of records per key */
+                if (lp) {
+                    if (__ballot(lenx && q == 0))                        /* LEN after a whole last step */
+                        if (lenx && q == 0)
+                            Y = xor4(gf_mul_v(Y, hl), make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8)));
+                    Y = group_xor4<L>(gf_mul_v(Y, hq));                  /* GHASH, in every lane of the record */
+                } else if constexpr (WP && L >= 2 && L <= 32) {
+                    if (a.tm & (L == 16 ? 1u : 2u)) {
+                        const SlotState &ss = a.slots[s];
+                        uint4 h1;
+                        __builtin_memcpy(&h1, ss.h, 16);                 /* H: bytes at a 4-byte-aligned offset */
+                        const uint4 P[5] = { h1,
+                                             make_uint4(ss.hpow[0][0], ss.hpow[0][1], ss.hpow[0][2], ss.hpow[0][3]),
+                                             make_uint4(ss.hpow[1][0], ss.hpow[1][1], ss.hpow[1][2], ss.hpow[1][3]),
+                                             make_uint4(ss.hpow[2][0], ss.hpow[2][1], ss.hpow[2][2], ss.hpow[2][3]),
+                                             make_uint4(ss.hpow[3][0], ss.hpow[3][1], ss.hpow[3][2], ss.hpow[3][3]) };
+                        Y = gtree_v<L / 2>(P, Y, lane, q);
+                    } else {
+                        Y = gtree<L / 2>(gp, Y, lane, q);
+                    }
                 } else {
                     Y = gtree<L / 2>(gp, Y, lane, q);
                 }
-            } else {
-                Y = gtree<L / 2>(gp, Y, lane, q);
-            }
-            if (!lp && q == 0) {                                     /* the group leader's sum */
-                uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
-                if (WP && (a.tm & 4u)) {
-                    Y = gf_mul_v(Y, h1v);                            /* T */
-                    Y = gf_mul_v(xor4(Y, lenw), h1v);                /* GHASH */
-                } else {
-                    Y = gmul<0>(gp, Y);                              /* T */
-                    Y = gmul<0>(gp, xor4(Y, lenw));                  /* GHASH */
-                }
-            }
-            if (!jb.run) continue;
-            const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
-            const uint4 tag = xor4(Y, ej0);
-            const tlsrec_batch_rec d = dsrc[didx];
-            tlsrec_plan p;
-            make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
-            if (!DEC) {
-                if (q == 0) {
-                    store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
-                    if (p.explicit_iv && p.post_status == 0) {
-                        uint8_t *e = a.out + d.buf_off + p.data_offset;
-                        for (int i = 0; i < 8; i++) e[i] = d.ctr[i];
+                if (!lp && q == 0) {                                     /* the group leader's sum */
+                    uint4 lenw = make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8));
+                    if (WP && (a.tm & 4u)) {
+                        Y = gf_mul_v(Y, h1v);                            /* T */
+                        Y = gf_mul_v(xor4(Y, lenw), h1v);                /* GHASH */
+                    } else {
+                        Y = gmul<0>(gp, Y);                              /* T */
+                        Y = gmul<0>(gp, xor4(Y, lenw));                  /* GHASH */
                     }
+                }
+                if (!jb.run) continue;
+                const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
+                const uint4 tag = xor4(Y, ej0);
+                const tlsrec_batch_rec d = dsrc[didx];
+                tlsrec_plan p;
+                make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+                if (!DEC) {
+                    if (q == 0) {
+                        store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
+                        if (p.explicit_iv && p.post_status == 0) {
+                            uint8_t *e = a.out + d.buf_off + p.data_offset;
+                            for (int i = 0; i < 8; i++) e[i] = d.ctr[i];
+                        }
+                        tlsrec_batch_res r;
+                        r.status = p.post_status;
+                        r.data_offset = p.data_offset;
+                        r.data_len = p.data_len;
+                        r.type = p.type;
+                        r.cid_len = p.cid_set ? p.cid_len : 0;
+                        r.reserved[0] = r.reserved[1] = 0;
+                        a.res[ridx] = r;
+                    }
+                } else {
+                    uint4 want = load_block(jb.src, jb.aead_len, jb.aead_len + 16, jb.aead_len + 16, 0, false);
+                    uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
+                    diff = group_or<L>(q == 0 ? diff : 0u);               /* the group leader's verdict, to all */
+                    uint32_t key = group_max<L>(nzkey);
                     tlsrec_batch_res r;
-                    r.status = p.post_status;
                     r.data_offset = p.data_offset;
                     r.data_len = p.data_len;
-                    r.type = p.type;
-                    r.cid_len = p.cid_set ? p.cid_len : 0;
+                    r.type = d.type;
+                    r.cid_len = 0;
                     r.reserved[0] = r.reserved[1] = 0;
-                    a.res[ridx] = r;
-                }
-            } else {
-                uint4 want = load_block(jb.src, jb.aead_len, jb.aead_len + 16, jb.aead_len + 16, 0, false);
-                uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
-                diff = group_or<L>(q == 0 ? diff : 0u);               /* the group leader's verdict, to all */
-                uint32_t key = group_max<L>(nzkey);
-                tlsrec_batch_res r;
-                r.data_offset = p.data_offset;
-                r.data_len = p.data_len;
-                r.type = d.type;
-                r.cid_len = 0;
-                r.reserved[0] = r.reserved[1] = 0;
-                if (diff != 0) {
-                    /* PSA wipes the whole output buffer on a bad tag */
-                    zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
-                    r.status = TLSREC_E_INVALID_MAC;
-                } else if (p.inner) {                                /* ssl_msg.c:1809-1829 */
-                    if (key == 0) {
-                        r.status = TLSREC_E_INVALID_RECORD;
+                    if (diff != 0) {
+                        /* PSA wipes the whole output buffer on a bad tag */
+                        zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
+                        r.status = TLSREC_E_INVALID_MAC;
+                    } else if (p.inner) {                                /* ssl_msg.c:1809-1829 */
+                        if (key == 0) {
+                            r.status = TLSREC_E_INVALID_RECORD;
+                        } else {
+                            r.status = 0;
+                            r.data_len = (key >> 8) - 1;
+                            r.type = (uint8_t) (key & 0xff);
+                        }
                     } else {
                         r.status = 0;
-                        r.data_len = (key >> 8) - 1;
-                        r.type = (uint8_t) (key & 0xff);
                     }
-                } else {
-                    r.status = 0;
+                    if (q == 0) a.res[ridx] = r;
                 }
-                if (q == 0) a.res[ridx] = r;
             }
+            my_slot = (my_slot == s) ? 0xffffffffu : my_slot;
         }
-        my_slot = (my_slot == s) ? 0xffffffffu : my_slot;
-    }
+    };
+    uint32_t my_slot = 0xffffffffu, my_rec = 0, my_d = 0;
+    membership(PAIR ? wg_base + (uint64_t) pr * 2 * a.rpw : 0, count, my_slot, my_rec, my_d);
+    if (tid == 0) { ctl[0] = 0xffffffffu; ctl[1] = 0xffffffffu; }
+    if (PAIR && tid >= 4 && tid < 32) ctl[tid] = 0;     /* pair minima [4, 20), barrier counters [20, 28) */
+    __syncthreads();
+    passes(my_slot, my_rec, my_d);
 }
 
 /* ======================================================================

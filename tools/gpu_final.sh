@@ -1,5 +1,5 @@
 #!/bin/bash
-# End-of-round measurement on one box, r04 (each part under the 20-minute limit):
+# End-of-round measurement on one box (each part under the 20-minute limit):
 #   tools/gpu_final.sh rows    -- -m gpu suite, smoke, every DESIGN row
 #   tools/gpu_final.sh prof1   -- rocprofv3 stats + PMC (incl. sized reads): c2 c3 c4s k4
 #   tools/gpu_final.sh prof2   -- the same for c4, c2s, DTLS 1.4 KiB AES-128-GCM, stream 1.4 KiB
@@ -27,6 +27,7 @@ rows)
     row $c 400 python3 bench.py --config $c --no-e2e && summ $c || exit 1
   done &&
   row stream16 300 python3 tools/bench_stream.py --conns 65536 --recs 16 && cat $O/stream16.json &&
+  row count_gpus 60 python3 -c "import bench, json; print(json.dumps({'count_gpus': bench.count_gpus()}))" && cat $O/count_gpus.json &&
   row stream4 300 python3 tools/bench_stream.py --conns 65536 --recs 4 && cat $O/stream4.json &&
   row stream16s 300 python3 tools/bench_stream.py --conns 65536 --recs 16 --content 1400 && cat $O/stream16s.json &&
   row stream_cp 300 python3 tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3 && cat $O/stream_cp.json &&
@@ -47,6 +48,7 @@ prof2)
   PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2s --config c2s > $O/prof_c2s.log 2>&1 || { echo "c2s failed"; tail -5 $O/prof_c2s.log; exit 1; }
   profiles/run_profile.sh ${T}_dtls_small --cmd tools/bench_dtls.py --steps 3 > $O/prof_dtls.log 2>&1 || { echo "dtls failed"; tail -5 $O/prof_dtls.log; exit 1; }
   profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
+  profiles/run_profile.sh ${T}_stream16 --cmd tools/bench_stream.py --conns 65536 --recs 16 --steps 3 > $O/prof_stream16.log 2>&1 || { echo "stream16 failed"; tail -5 $O/prof_stream16.log; exit 1; }
   echo prof2 done
   ;;
 *) echo "usage: tools/gpu_final.sh rows|prof1|prof2"; exit 2;;
