@@ -1054,7 +1054,9 @@ static int host_batch(tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_ba
     uint8_t *zc = NULL;
     {
         hipPointerAttribute_t at;
-        if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+        const char *zce = getenv("TLSREC_HOST_ZC");      /* =0: copy back even to pinned memory (measurement) */
+        if (!(zce && atoi(zce) == 0) && hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost &&
+            at.devicePointer)
             zc = (uint8_t *) at.devicePointer;
         else
             (void) hipGetLastError();    /* pageable memory: clear the sticky error */
