@@ -34,7 +34,13 @@ rows)
   row dtls_small 300 python3 tools/bench_dtls.py && cat $O/dtls_small.json &&
   row dtls_cp 300 python3 tools/bench_dtls.py --cipher 3 && cat $O/dtls_cp.json &&
   row dtls16k 300 python3 tools/bench_dtls.py --content 16384 --recs 4 --cipher 2 && cat $O/dtls16k.json &&
-  row keysched 300 python3 tools/bench_keysched.py && cat $O/keysched.json
+  row keysched 300 python3 tools/bench_keysched.py && cat $O/keysched.json &&
+  make -s -C tests/c abi_host &&
+  : > $O/latency.jsonl &&
+  for a in "2 1.3 16383" "2 1.3 1400" "3 1.3 1400" "1 1.2 1400" "2 1.3 100"; do
+    timeout -k 10 120 ./tests/c/abi_host latency $a 2000 >> $O/latency.jsonl || exit 1
+  done && for t in 1 16 32; do timeout -k 10 120 ./tests/c/abi_host threads $t 2000 gcm_chacha >> $O/latency.jsonl || exit 1; done &&
+  cat $O/latency.jsonl
   ;;
 prof1)
   PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2 > $O/prof_c2.log 2>&1 || { echo "c2 failed"; tail -5 $O/prof_c2.log; exit 1; }
