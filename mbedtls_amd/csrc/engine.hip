@@ -644,6 +644,7 @@ struct BatchOpt {
     uint32_t avg_bytes = 0;
     bool prefilled = false;
     bool coalesced = false;
+    const uint64_t *src_off = nullptr;   /* encrypt: contents at in + src_off[i] (tlsrec__batch_src) */
 };
 
 static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
@@ -798,6 +799,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         if (L == 2 && !wp) L = 4;     /* 2 lanes: wave passes only */
         const int waves = pair ? 16 : (wp ? 8 : (kt->has_cid ? 16 : gcm_waves()));
         a.rpw = (opt.coalesced && wp) ? 1u : pick_rpw(n, (uint32_t) waves, 64 / L, (uint32_t) cu);
+        a.src_off = dec ? nullptr : opt.src_off;
         a.capacity = cap;
         a.cipher = (uint32_t) cipher;
         a.g5 = gcm_g5();
@@ -834,6 +836,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.in = in;
         a.out = out;
         a.rpw = pick_rpw(n, (uint32_t) ARIA_GCM_WAVES, 8u, (uint32_t) cu);
+        a.src_off = nullptr;
         a.capacity = cap;
         a.cipher = (uint32_t) c;
         a.g5 = 0;
@@ -887,6 +890,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         a.capacity = cap;
         a.cid = kt->has_cid;
         a.skip = skip;
+        a.src_off = dec ? nullptr : opt.src_off;
         uint64_t per_wg = (uint64_t) CP_WAVES * a.rpw;
         uint32_t grid = (uint32_t) ((n + per_wg - 1) / per_wg);
         if (tlsrec__launch_chachapoly(&a, dec, L, grid, st) != hipSuccess) rc = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
@@ -925,6 +929,24 @@ extern "C" int tlsrec_batch_decrypt_sized(const tlsrec_keytab *kt, const tlsrec_
     BatchOpt o;
     o.avg_bytes = mean_record_bytes;
     return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 1, o);
+}
+
+extern "C" int tlsrec__keytab_src_ok(const tlsrec_keytab *kt)
+{
+    const uint32_t ok = (1u << TLSREC_CIPHER_AES_128_GCM) | (1u << TLSREC_CIPHER_AES_192_GCM) |
+                        (1u << TLSREC_CIPHER_AES_256_GCM) | (1u << TLSREC_CIPHER_CHACHA20_POLY1305);
+    return kt && !kt->has_cid && (kt->cipher_mask & ~ok) == 0;   /* (the CID kernel variants read in place) */
+}
+
+extern "C" int tlsrec__batch_src(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
+                                 uint32_t n, const uint8_t *in_arena, uint8_t *out_arena, void *stream,
+                                 uint32_t avg_bytes, const uint64_t *src_off)
+{
+    if (!tlsrec__keytab_src_ok(kt) || !src_off) return TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    BatchOpt o;
+    o.avg_bytes = avg_bytes;
+    o.src_off = src_off;
+    return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 0, o);
 }
 
 extern "C" int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,

@@ -654,7 +654,10 @@ __device__ __forceinline__ uint32_t ks_half(uint32_t c, uint32_t g)
  * and at 2 waves the c3 shape lost what the 3 saved quarter rounds gain;
  * capped at 168 the compiler spills 6-12 registers outside the step loop
  * (same box: c3 1 224 -> 1 220, c3d 1 195 -> 1 204, 16 KiB 1 637 -> 1 677 GiB/s) */
-template <int L, bool DEC, bool CID = false>
+/* SRC (r05, encrypt): the contents at a.in + a.src_off[i] (the stream / DTLS
+ * send path, tlsrec__batch_src), partial blocks read byte-wise; a template
+ * flag, not a run-time test: as one, it cost c3 1.5 % (same box) */
+template <int L, bool DEC, bool CID = false, bool SRC = false>
 __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(3))) void tlsrec_chachapoly_kernel(CpArgs a)
 {
     constexpr int R = 64 / L;
@@ -802,15 +805,18 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(3)))
             src = a.in + d.buf_off + p.aead_pos;
             dst = a.out + d.buf_off + p.aead_pos;
             content_len = DEC ? aead_len : p.content_len;
+            if constexpr (SRC) src = a.in + a.src_off[ridx];   /* the content in the caller's buffer */
         }
+        /* partial blocks 16 B wide (in place), or byte-wise from a caller's buffer */
+        constexpr bool wide = !SRC;
         const uint8_t inner_type = run ? p.inner_type : 0;
         const bool tls13 = run && p.inner;   /* TLS 1.3 or DTLS 1.2 + CID inner plaintext */
         /* a readable 16-byte address for slots with nothing to load, in a
          * line the step's other lanes read anyway: the record start for the
          * front padding of step 0, its last content bytes for the tail (the
          * start would be a second HBM trip by then) */
-        const uint8_t *safe0 = run ? src : reinterpret_cast<const uint8_t *>(a.recs);
-        const uint8_t *safe = run ? src + (content_len >= 16 ? (content_len - 16) & ~15u : 0u) : safe0;
+        const uint8_t *safe0 = run ? (wide ? src : dst) : reinterpret_cast<const uint8_t *>(a.recs);
+        const uint8_t *safe = run && wide ? src + (content_len >= 16 ? (content_len - 16) & ~15u : 0u) : safe0;
         /* slot (L*t + q) of step j is record block 4(L j - z) + L t + q */
         const int32_t base0 = (int32_t) q - 4 * (int32_t) z;
 
@@ -877,7 +883,7 @@ __global__ __launch_bounds__(CP_THREADS) __attribute__((amdgpu_waves_per_eu(3)))
                     if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                     x = p_from_words(DEC ? ct[t] : o);
                 } else if (valid) {
-                    const uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, true);
+                    const uint4 blk = load_block(src, pos, content_len, aead_len, inner_type, wide);
                     const uint4 o = mask_block(xor4(blk, K[t]), pos, aead_len);
                     store_block(dst, pos, aead_len, o, true);
                     if (DEC && tls13 && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
@@ -1039,6 +1045,8 @@ static hipError_t launch_cp_t(const CpArgs &a, uint32_t grid, hipStream_t st)
             hipLaunchKernelGGL((tlsrec_chachapoly_kernel<2, DEC, true>), dim3(grid), dim3(CP_THREADS), 0, st, a);
         else
             return hipErrorInvalidValue;
+    } else if (!DEC && a.src_off) {   /* stream / DTLS send (tlsrec__batch_src) */
+        hipLaunchKernelGGL((tlsrec_chachapoly_kernel<L, false, false, true>), dim3(grid), dim3(CP_THREADS), 0, st, a);
     } else {
         hipLaunchKernelGGL((tlsrec_chachapoly_kernel<L, DEC>), dim3(grid), dim3(CP_THREADS), 0, st, a);
     }

@@ -261,9 +261,14 @@ __global__ void __launch_bounds__(256) out_map_kernel(uint32_t n, const uint32_t
 /* One wave per record (4 per workgroup): header, descriptor, and the
  * plaintext copied into the record's slot of the output stream with 16-byte
  * accesses at any byte alignment (unaligned-access mode, see kernels.hip). */
+/* srcoff (r05): instead of copying the application data into the output
+ * stream, record j's content offset in `in` goes to srcoff[j] and the AEAD
+ * kernels read it there (tlsrec__batch_src) -- one pass over the data instead
+ * of a copy and an in-place pass */
 __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs,
                                                         uint32_t total, const SlotState *slots, uint32_t cap,
-                                                        const uint8_t *in, uint8_t *out, tlsrec_batch_rec *recs)
+                                                        const uint8_t *in, uint8_t *out, tlsrec_batch_rec *recs,
+                                                        uint64_t *srcoff)
 {
     const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= total) return;
@@ -289,15 +294,19 @@ __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out 
         }
         return;
     }
-    const uint8_t *src = in + si.in_off + src_off;
-    uint8_t *dst = out + pos + 5 + sh.head;
-    const uint32_t nv = len / 16;
-    for (uint32_t v = lane; v < nv; v += 64) {
-        uint4 w;
-        __builtin_memcpy(&w, src + 16 * v, 16);
-        __builtin_memcpy(dst + 16 * v, &w, 16);
+    if (srcoff) {
+        if (lane == 0) srcoff[j] = si.in_off + src_off;
+    } else {
+        const uint8_t *src = in + si.in_off + src_off;
+        uint8_t *dst = out + pos + 5 + sh.head;
+        const uint32_t nv = len / 16;
+        for (uint32_t v = lane; v < nv; v += 64) {
+            uint4 w;
+            __builtin_memcpy(&w, src + 16 * v, 16);
+            __builtin_memcpy(dst + 16 * v, &w, 16);
+        }
+        for (uint32_t b = nv * 16 + lane; b < len; b += 64) dst[b] = src[b];
     }
-    for (uint32_t b = nv * 16 + lane; b < len; b += 64) dst[b] = src[b];
     if (lane == 0) {
         const uint32_t body = out_body(sh, len);
         uint8_t *h = out + pos;
@@ -712,7 +721,7 @@ __device__ __forceinline__ void dtls_seq(uint8_t ctr[8], const uint8_t base[8], 
 __global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream_out *s, uint32_t n,
                                                              const uint32_t *offs, uint32_t total,
                                                              const SlotState *slots, uint32_t cap, const uint8_t *in,
-                                                             uint8_t *out, tlsrec_batch_rec *recs)
+                                                             uint8_t *out, tlsrec_batch_rec *recs, uint64_t *srcoff)
 {
     const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= total) return;
@@ -737,15 +746,19 @@ __global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream
         }
         return;
     }
-    const uint8_t *src = in + si.in_off + src_off;
-    uint8_t *dst = out + pos + hdr + sh.head;
-    const uint32_t nv = len / 16;
-    for (uint32_t v = lane; v < nv; v += 64) {
-        uint4 w;
-        __builtin_memcpy(&w, src + 16 * v, 16);
-        __builtin_memcpy(dst + 16 * v, &w, 16);
+    if (srcoff) {                                 /* (out_frame_kernel) */
+        if (lane == 0) srcoff[j] = si.in_off + src_off;
+    } else {
+        const uint8_t *src = in + si.in_off + src_off;
+        uint8_t *dst = out + pos + hdr + sh.head;
+        const uint32_t nv = len / 16;
+        for (uint32_t v = lane; v < nv; v += 64) {
+            uint4 w;
+            __builtin_memcpy(&w, src + 16 * v, 16);
+            __builtin_memcpy(dst + 16 * v, &w, 16);
+        }
+        for (uint32_t b = nv * 16 + lane; b < len; b += 64) dst[b] = src[b];
     }
-    for (uint32_t b = nv * 16 + lane; b < len; b += 64) dst[b] = src[b];
     if (lane == 0) {
         const uint32_t body = dtls_body(sh, cid, len);
         uint8_t *h = out + pos;
@@ -828,6 +841,14 @@ struct Scratch {
     void *scan_tmp = nullptr;
     size_t scan_bytes = 0;
 };
+}
+
+/* the send paths read the application data in place (r05; TLSREC_STREAM_SRC=0
+ * copies it into the output stream first, as r04 did) */
+static bool src_env(void)
+{
+    const char *e = getenv("TLSREC_STREAM_SRC");
+    return !(e && atoi(e) == 0);
 }
 
 static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
@@ -945,10 +966,20 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
     if (r == 0 && total) {
         hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs, sc.counts,
                            recs);
+        /* AES-GCM / ChaCha20-Poly1305 tables: the AEAD reads the application
+         * data in place (tlsrec__batch_src); other AEADs: copy, then in place */
+        uint64_t *srcoff = nullptr;
+        tlsrec_scratch_lease sl = { nullptr, nullptr };
+        if (tlsrec__keytab_src_ok(kt) && src_env() &&
+            tlsrec__scratch_acquire(st, 3, (size_t) total * sizeof(uint64_t), &sl) == 0)
+            srcoff = (uint64_t *) sl.mem;
         hipLaunchKernelGGL(out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
-                           total, slots, cap, in_arena, out_arena, recs);
+                           total, slots, cap, in_arena, out_arena, recs, srcoff);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
+        if (r == 0)
+            r = srcoff ? tlsrec__batch_src(kt, recs, res, total, in_arena, out_arena, stream, avg, srcoff)
+                       : tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
+        if (srcoff) tlsrec__scratch_release(&sl);
     }
     if (r == 0) {
         hipLaunchKernelGGL(out_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
@@ -1054,10 +1085,20 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
     if (r == 0 && total) {
         hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs, sc.counts,
                            recs);
+        /* AES-GCM / ChaCha20-Poly1305 tables: the AEAD reads the application
+         * data in place (tlsrec__batch_src); other AEADs: copy, then in place */
+        uint64_t *srcoff = nullptr;
+        tlsrec_scratch_lease sl = { nullptr, nullptr };
+        if (tlsrec__keytab_src_ok(kt) && src_env() &&
+            tlsrec__scratch_acquire(st, 3, (size_t) total * sizeof(uint64_t), &sl) == 0)
+            srcoff = (uint64_t *) sl.mem;
         hipLaunchKernelGGL(dtls_out_frame_kernel, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams, sc.offs,
-                           total, slots, cap, in_arena, out_arena, recs);
+                           total, slots, cap, in_arena, out_arena, recs, srcoff);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
+        if (r == 0)
+            r = srcoff ? tlsrec__batch_src(kt, recs, res, total, in_arena, out_arena, stream, avg, srcoff)
+                       : tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
+        if (srcoff) tlsrec__scratch_release(&sl);
     }
     if (r == 0) {
         hipLaunchKernelGGL(dtls_out_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,

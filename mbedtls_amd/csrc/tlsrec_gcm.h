@@ -105,6 +105,7 @@ __device__ __noinline__ void gtab4_build_half(uint8_t *tab, const uint4 *pp, int
  * VGPRs across the loop). */
 struct GcmJob {
     bool run, aligned, inner;   /* inner: TLS 1.3 / DTLS 1.2 + CID inner plaintext */
+    bool wide_tail;             /* partial blocks read 16 B wide (in place); false: byte-wise (GcmArgs::src_off) */
     uint8_t inner_type;
     uint32_t aead_len, content_len, aad_len;
     uint32_t nw0, nw1, nw2;
@@ -134,6 +135,7 @@ struct GcmJob {
          * headers -- take the wide path; the wide read of a block never
          * leaves the record buffer (tag / tag room follows the AEAD data) */
         aligned = true;
+        wide_tail = true;
         run = true;
     }
 };
@@ -384,6 +386,11 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                         if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
                     } else {
                         jb.setup<DEC>(p, d, km, a.in, a.out);
+                        if constexpr (!DEC)
+                            if (a.src_off) {           /* the content in the caller's buffer (stream send) */
+                                jb.src = a.in + a.src_off[ridx];
+                                jb.wide_tail = false;
+                            }
                         /* DTLS 1.2 + CID: AAD of 2..4 blocks, Horner-folded
                          * into the block the AAD fold multiplies by H below */
                         if (CID && p.aad_len > 16) jb.aadw = gcm_cid_aad_fold(gp, jb.aadw, p, d, a.slots[s].cid);
@@ -437,7 +444,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 /* TLS 1.3 inner type: position + 1 of the last non-zero output block */
                 uint32_t nzpos = 0;
                 /* a readable 16-byte address for lanes with nothing to load */
-                const uint8_t *safe = jb.run ? jb.src : reinterpret_cast<const uint8_t *>(a.recs);
+                const uint8_t *safe = jb.run ? (jb.wide_tail ? jb.src : jb.dst) : reinterpret_cast<const uint8_t *>(a.recs);
                 /* Body steps [1, jh): every lane of the wave holds a full, aligned
                  * block inside its record's content (wave-uniform bound), so they run
                  * without masks or branches.  Step 0 (AAD fold, front padding) and
@@ -488,7 +495,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                                 X = DEC ? blk : o;
                                 if (DEC && jb.inner && (o.x | o.y | o.z | o.w)) nzpos = pos + 1;
                             } else if (valid) {
-                                blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type, jb.aligned);
+                                blk = load_block(jb.src, pos, jb.content_len, jb.aead_len, jb.inner_type,
+                                                 jb.aligned && jb.wide_tail);
                                 const uint4 o = mask_block(xor4(blk, ks), pos, jb.aead_len);
                                 store_block(jb.dst, pos, jb.aead_len, o, jb.aligned);
                                 X = DEC ? blk : o;

@@ -91,6 +91,9 @@ struct GcmArgs {
     const tlsrec_batch_rec *srecs;   /* with perm: the descriptors in perm order (srecs[p] = recs[perm[p]],
                                         written by the bucket scatter), so a key pass reads its records'
                                         descriptors from one contiguous run instead of a line per record */
+    const uint64_t *src_off = nullptr;  /* encrypt, r05: record i's content starts at in + src_off[i] (not in + buf_off
+                                 + data_offset); its tail is read byte-wise, never past the content (the
+                                 stream / DTLS send path reads the caller's application data in place) */
 };
 
 struct CpArgs {
@@ -106,6 +109,7 @@ struct CpArgs {
     uint32_t capacity;
     uint32_t cid;             /* the key table holds DTLS connection IDs: CID kernel variant */
     uint32_t skip;            /* test hook, as GcmArgs::skip */
+    const uint64_t *src_off = nullptr;   /* encrypt: as GcmArgs::src_off */
 };
 
 /* Bucket pass: key index of a record = AES-128-GCM slot, AES-256-GCM slot,
@@ -173,6 +177,15 @@ void tlsrec__scratch_release(tlsrec_scratch_lease *lease);
  * caller that knows the batch's mean record size (the stream / DTLS layers) */
 int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
                         const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec, uint32_t avg_bytes);
+/* encrypt with each record's content read from in_arena + src_off[i] (GcmArgs::
+ * src_off) and the records written to out_arena at buf_off: the stream / DTLS
+ * send path without a copy of the application data.  Only for key tables of
+ * AES-GCM and ChaCha20-Poly1305 keys without connection IDs
+ * (tlsrec__keytab_src_ok). */
+int tlsrec__batch_src(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
+                      const uint8_t *in_arena, uint8_t *out_arena, void *stream, uint32_t avg_bytes,
+                      const uint64_t *src_off);
+int tlsrec__keytab_src_ok(const tlsrec_keytab *kt);
 hipError_t tlsrec__launch_bucket_zero(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_count(const tlsrec::BucketArgs *a, hipStream_t st);
 hipError_t tlsrec__launch_bucket_scatter(const tlsrec::BucketArgs *a, hipStream_t st);

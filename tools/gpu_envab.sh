@@ -14,6 +14,8 @@ for row in "$@"; do
     stream16s) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 16 --content 1400) ;;
     stream4) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 4) ;;
     stream16) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 16) ;;
+    stream_cp) cmd=(python3 tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3) ;;
+    dtls_cp) cmd=(python3 tools/bench_dtls.py --cipher 3) ;;
     *) cmd=(python3 bench.py --config $row --no-cpu --no-e2e --verify 16) ;;
   esac
   k=0
