@@ -36,6 +36,7 @@ struct tlsrec_keytab {
     uint32_t cipher_mask;     /* 1 << TLSREC_CIPHER_* of every loaded slot */
     uint32_t nloaded;         /* slots holding a key */
     volatile uint32_t has_cid; /* some slot was given a DTLS connection ID: launch the CID kernels */
+    uint8_t *d_dummy;         /* GcmArgs::dummy: 64 KiB the idle lanes of a wave-pass round load and store */
     HostPipe *pipe;
     pthread_mutex_t pipe_mu;
 };
@@ -82,7 +83,8 @@ extern "C" int tlsrec_keytab_create(tlsrec_keytab **out, uint32_t capacity)
         hipMalloc((void **) &kt->d_slots, sizeof(SlotState) * (size_t) capacity) != hipSuccess ||
         hipMalloc((void **) &kt->d_ghtab, sizeof(uint4) * (size_t) KEY_TABLE_WORDS * capacity) != hipSuccess ||
         hipMalloc((void **) &kt->d_cipher, (size_t) capacity) != hipSuccess ||
-        hipMalloc((void **) &kt->d_stage, sizeof(tlsrec_key_material) * (size_t) capacity) != hipSuccess) {
+        hipMalloc((void **) &kt->d_stage, sizeof(tlsrec_key_material) * (size_t) capacity) != hipSuccess ||
+        hipMalloc((void **) &kt->d_dummy, GCM_DUMMY_BYTES) != hipSuccess) {
         tlsrec_keytab_free(kt);
         return TLSREC_ERR_SSL_ALLOC_FAILED;
     }
@@ -133,8 +135,10 @@ extern "C" void tlsrec_keytab_free(tlsrec_keytab *kt)
         /* zeroize key material (ssl_msg.c:6084-6099 zeroizes transforms) */
         hipMemset(kt->d_slots, 0, sizeof(SlotState) * (size_t) kt->capacity);
         hipMemset(kt->d_ghtab, 0, sizeof(uint4) * (size_t) KEY_TABLE_WORDS * kt->capacity);
+        if (kt->d_dummy) hipMemset(kt->d_dummy, 0, GCM_DUMMY_BYTES);   /* idle lanes' keystream under the keys */
         hipDeviceSynchronize();
     }
+    hipFree(kt->d_dummy);
     hipFree(kt->d_slots);
     hipFree(kt->d_ghtab);
     hipFree(kt->d_cipher);
@@ -729,6 +733,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;
+        a.dummy = kt->d_dummy;
         a.recs = recs;
         a.res = res;
         a.n = n;
@@ -826,6 +831,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         GcmArgs a;
         a.slots = kt->d_slots;
         a.ghtab = kt->d_ghtab;
+        a.dummy = kt->d_dummy;
         a.recs = recs;
         a.res = res;
         a.n = n;

@@ -452,11 +452,39 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 uint32_t jh = 0;
                 {
                     const uint32_t mfast = (jb.run && jb.aligned) ? jb.content_len / 16 : 0;
-                    uint32_t h = jb.run ? (mfast + z) / BL : 0;
-                    h = wave_min(h);
-                    jh = h > 1 ? h : 0;
+                    if constexpr (WP && DEC) {
+                        /* (r05) a round whose wave holds idle lanes -- a key run
+                         * that does not fill it -- still takes the body over the
+                         * running lanes' full blocks: the idle lanes load and
+                         * store a dummy buffer (GcmArgs::dummy) and their
+                         * results are never used; the bound keeps their
+                         * addresses inside it.  Decrypt only: compiled into the
+                         * encrypt kernels it cost the DTLS / stream send rows
+                         * 3-4 % (same box), whose rounds are full anyway. */
+                        uint32_t h = jb.run ? (mfast + z) / BL : 0xffffffffu;
+                        h = wave_min(h);
+                        if (__ballot(!jb.run)) {
+                            constexpr uint32_t hmax = GCM_DUMMY_BYTES / (16 * BL) - 4;
+                            h = a.dummy ? (h < hmax ? h : hmax) : 0;
+                            if (!jb.run) {
+                                jb.src = a.dummy;
+                                jb.dst = a.dummy;
+                                jb.nw0 = jb.nw1 = jb.nw2 = 0;
+                                jb.inner = false;
+                            }
+                        }
+                        jh = h > 1 ? h : 0;
+                    } else {
+                        uint32_t h = jb.run ? (mfast + z) / BL : 0;
+                        h = wave_min(h);
+                        jh = h > 1 ? h : 0;
+                    }
                 }
-                const uint32_t jl = jh ? 1u : Jmax;
+                /* with lane powers step 0 holds no AAD fold and no front
+                 * padding (C_1 at position 0): when it is full it joins the
+                 * body (r05; decrypt -- in the encrypt kernels it cost the
+                 * DTLS / stream send rows 3 %) */
+                const uint32_t jl = jh ? ((DEC && lp) ? 0u : 1u) : Jmax;
                 auto steps = [&](auto cached) {
                     constexpr bool CACHED = decltype(cached)::value;
                     CtrCache ccache;

@@ -69,6 +69,8 @@ static_assert(sizeof(tlsrec_batch_res) == 16, "batch result layout");
  * positions [0, n) of the descriptor array itself (identity order: a table
  * holding a single key).  lo/hi live in device memory so the launches need
  * no host synchronisation. */
+constexpr uint32_t GCM_DUMMY_BYTES = 65536;
+
 struct GcmArgs {
     const SlotState *slots;
     const uint4 *ghtab;
@@ -91,6 +93,8 @@ struct GcmArgs {
     const tlsrec_batch_rec *srecs;   /* with perm: the descriptors in perm order (srecs[p] = recs[perm[p]],
                                         written by the bucket scatter), so a key pass reads its records'
                                         descriptors from one contiguous run instead of a line per record */
+    uint8_t *dummy = nullptr;  /* r05: GCM_DUMMY_BYTES of device memory the idle lanes of a wave-pass round
+                                  load from and store to, so the round still runs the mask-free body */
     const uint64_t *src_off = nullptr;  /* encrypt, r05: record i's content starts at in + src_off[i] (not in + buf_off
                                  + data_offset); its tail is read byte-wise, never past the content (the
                                  stream / DTLS send path reads the caller's application data in place) */

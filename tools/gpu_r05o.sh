@@ -1,0 +1,17 @@
+#!/bin/bash
+# r05: step 0 in the body under lane powers; idle lanes of a round on a dummy buffer
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r05o; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu \
+  tests/test_evp_parity_gpu.py tests/test_gpu_parity.py tests/test_gpu_parity_edges.py tests/test_stream_gpu.py tests/test_dtls_gpu.py tests/test_fail_closed_gpu.py > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+tail -1 $O/tests.txt
+for K in 43691 26214 22310 19065 11038; do
+  for lib in ablib/libtlsrec_r05e.so mbedtls_amd/libtlsrec.so mbedtls_amd/libtlsrec.so ablib/libtlsrec_r05e.so; do
+    tag=$(basename $lib .so)
+    TLSREC_LIBRARY=$GRAFT_REPO_ROOT/$lib timeout -k 10 300 python3 bench.py --config c2s --keys $K --no-cpu --no-e2e --verify 16 > $O/k$K.$tag.json 2> $O/k$K.$tag.err || { tail -3 $O/k$K.$tag.err; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('rpk', (1<<20) // int(sys.argv[2]), sys.argv[3], d['value'], d['check']['bad_records'])" $O/k$K.$tag.json $K $tag
+  done
+done
+tools/gpu_ab_lib.sh r05o/lib ablib/libtlsrec_r05e.so mbedtls_amd/libtlsrec.so c2 c4s k4 c2 || exit 1
+tools/gpu_envab.sh r05o/rows TLSREC_LIBRARY=$GRAFT_REPO_ROOT/ablib/libtlsrec_r05e.so TLSREC_LIBRARY=$GRAFT_REPO_ROOT/mbedtls_amd/libtlsrec.so dtls_small stream16s stream16 || exit 1
