@@ -416,3 +416,32 @@ def test_key_pass_tree_modes_vs_openssl_evp(monkeypatch, cipher, ver, nkeys, n):
     match OpenSSL byte for byte"""
     monkeypatch.setenv("TLSREC_GCM_TREEMUL", "9")
     _evp_case(cipher, ver, nkeys, n)
+
+
+_SMALL16 = (2048, 16, (1000, 1500), 1300)     # DTLS / stream shape: paired passes, 8 lanes
+_SMALL40 = (1024, 40, (1000, 1500), 1300)     # paired passes, lane model
+_SMALL64 = (512, 64, (1000, 1500), 1300)      # c4s's records per key
+_BIG4 = (2048, 4, (12000, 16383), 14000)      # k4's shape: paired passes, 32 lanes
+_BIG16 = (512, 16, (12000, 16383), 14000)     # paired passes, 16 lanes
+
+
+@pytest.mark.parametrize("var,val,shape", [
+    ("TLSREC_GCM_G5", "0", (1, 1, None, 0)),
+    ("TLSREC_GCM_HBUILD", "0", _SMALL16), ("TLSREC_GCM_HBUILD", "0", _BIG4),
+    ("TLSREC_GCM_PAIR", "0", _SMALL16), ("TLSREC_GCM_PAIR", "0", _BIG4),
+    ("TLSREC_GCM_PAIR_L", "2", _SMALL40), ("TLSREC_GCM_PAIR_L", "4", _SMALL40), ("TLSREC_GCM_PAIR_L", "8", _SMALL40),
+    ("TLSREC_GCM_PAIR_BIG_MAX", "12", _BIG16),
+    ("TLSREC_GCM_PAIR_SMALL_MIN", "200", _SMALL64), ("TLSREC_GCM_PAIR_SMALL_MAX", "13", _SMALL16),
+], ids=lambda x: x if isinstance(x, str) else (f"{x[0]}x{x[1]}" if isinstance(x, tuple) else str(x)))
+def test_engine_overrides_vs_openssl_evp(monkeypatch, var, val, shape):
+    """The measurement overrides of the engine's kernel choice (INTEGRATION
+    §5) select kernels the default rules use elsewhere or not at all (the
+    4-bit Horner table for a single key, the Horner table staged from HBM,
+    the 8-wave wave passes instead of the pairs, forced pair lanes, the
+    16-wave key passes at the pairs' records per key): every record of both
+    directions against OpenSSL under each."""
+    nkeys, rpk, lens, mean = shape
+    n = 30_000 if nkeys == 1 else nkeys * rpk
+    monkeypatch.setenv(var, val)
+    _evp_case(M.CIPHER_AES_256_GCM, M.VERSION_TLS1_3, nkeys, n, lens=lens, mean_bytes=mean)
+    _evp_case(M.CIPHER_AES_128_GCM, M.VERSION_TLS1_2, nkeys, n, lens=lens, mean_bytes=mean)

@@ -295,6 +295,27 @@ def test_many_keys_small_records_wave_passes(cipher):
     c.close()
 
 
+def test_send_copy_path_matches_oracle(monkeypatch):
+    """TLSREC_STREAM_SRC=0: the send path copies the application data into
+    the record arena and encrypts there (the r04 path, still taken by CID
+    and ARIA / Camellia tables) instead of reading it in place; the same
+    streams as the default path, checked against the oracle."""
+    monkeypatch.setenv("TLSREC_STREAM_SRC", "0")
+    slots = _slots(43)
+    c = Conns(slots)
+    rng = np.random.default_rng(11)
+    jobs = []
+    for i in range(40):
+        n = int(rng.choice([0, 1, 15, 1400, 16383, 16385, 40000]))
+        frag = int(rng.choice([0, 1000, 4096]))
+        jobs.append((i % 20, prng_bytes(3000 + i, n), int(rng.integers(0, 1 << 40)), frag, 23))
+    got = c.encrypt(jobs)
+    for (slot, pt, ctr, frag, typ), (r, out) in zip(jobs, got):
+        st, want, nrec, ctr2 = O.stream_encrypt(c.ot[slot], pt, typ, ctr.to_bytes(8, "big"), frag or 16384)
+        assert (int(r["status"]), int(r["nrec"]), out, bytes(r["out_ctr"])) == (st, nrec, want, ctr2)
+    c.close()
+
+
 def test_send_counter_wrap_encrypts_nothing_past_the_wrap():
     """out_ctr = 2^64 - 2, three records: the reference writes the records with
     sequence numbers 2^64-2 and 2^64-1, then stops with COUNTER_WRAPPING
