@@ -621,9 +621,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 }
                 uint4 Y = xor4(Z, Xp);
                 /* lane powers: this lane's H^(L - q), read while the tail runs */
-                uint4 hq = make_uint4(0, 0, 0, 0), hl = make_uint4(0, 0, 0, 0);
+                uint4 hq = make_uint4(0, 0, 0, 0);
                 if (lp) hq = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (m + (uint32_t) (L - q)) % L];
-                if (lenx && q == 0) hl = a.ghtab[(size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1)];
                 uint32_t nzkey = 0;
                 if (DEC && jb.inner && nzpos) {
                     /* the lane's last non-zero plaintext block, as written above */
@@ -635,9 +634,13 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                  * key, and of k4) too: their tree read the key's H^1 .. H^16 tables
                  * from HBM, 8 KiB each, for a handful of records per key */
                 if (lp) {
-                    if (__ballot(lenx && q == 0))                        /* LEN after a whole last step */
+                    /* LEN after a whole last step: one more Horner step, by the
+                     * H^L table the pass holds in LDS (r05; a table-free multiply
+                     * by the value H^L before: ~1 000 VALU instructions per
+                     * round, for every 16 KiB record of k4 / DTLS) */
+                    if (__ballot(lenx && q == 0))
                         if (lenx && q == 0)
-                            Y = xor4(gf_mul_v(Y, hl), make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8)));
+                            Y = xor4(gmul<HPI>(hor, Y), make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8)));
                     Y = group_xor4<L>(gf_mul_v(Y, hq));                  /* GHASH, in every lane of the record */
                 } else if constexpr (WP && L >= 2 && L <= 32) {
                     if (a.tm & (L == 16 ? 1u : 2u)) {
