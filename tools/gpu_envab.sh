@@ -2,7 +2,8 @@
 # Same-box environment-variable A/B (runs a, b, b, a):
 #   tools/gpu_envab.sh <outdir> "VAR=a" "VAR=b" <row>...
 # row = a bench.py config (c4s, k4, ...) or one of dtls_small, stream16s,
-# stream4 (tools/bench_dtls.py / bench_stream.py shapes of DESIGN 5.0).
+# stream4, stream16, stream_cp, dtls_cp, dtls16k (tools/bench_dtls.py /
+# bench_stream.py shapes of DESIGN 5.0).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -16,6 +17,7 @@ for row in "$@"; do
     stream16) cmd=(python3 tools/bench_stream.py --conns 65536 --recs 16) ;;
     stream_cp) cmd=(python3 tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3) ;;
     dtls_cp) cmd=(python3 tools/bench_dtls.py --cipher 3) ;;
+    dtls16k) cmd=(python3 tools/bench_dtls.py --content 16384 --recs 4 --cipher 2) ;;
     *) cmd=(python3 bench.py --config $row --no-cpu --no-e2e --verify 16) ;;
   esac
   k=0
