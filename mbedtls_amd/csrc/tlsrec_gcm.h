@@ -263,6 +263,26 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     const uint8_t *hor = WP ? lds + LY::GH + (PAIR ? pr : wave) * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
     uint32_t phase = 0;                                  /* PAIR barrier count */
     auto passes = [&](uint32_t my_slot, uint32_t my_rec, uint32_t my_d) __attribute__((always_inline)) {
+        if constexpr (PAIR) {
+            /* E_K(J0) of the lane's own record under its own key, once, before
+             * the passes (r05): per key pass it cost a whole SIMD AES for the
+             * few lanes of that key -- with 16 records per key, one AES per
+             * round of 8 records.  The lane reads its slot's round keys as
+             * vectors; the LDS slot keeps the value across the passes. */
+            uint4 ej0 = make_uint4(0, 0, 0, 0);
+            if (my_slot != 0xffffffffu) {
+                const SlotState *ss = &a.slots[my_slot];
+                const tlsrec_key_material km = ss->km;
+                const tlsrec_batch_rec d = dsrc[my_d];
+                tlsrec_plan p;
+                make_plan<DEC, CID>(p, d, km, ss, a.in);
+                uint32_t nw[3];
+                nonce_words<DEC>(p, d, km, a.in, nw);
+                ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, (const uint32_t *) ss->rkr,
+                                               make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+            }
+            reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
+        }
         for (int iter = 0;; iter++) {
             uint32_t s;
             if constexpr (PAIR) {
@@ -332,7 +352,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const tlsrec_key_material km = a.slots[s].km;
 
             /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
-            {
+            if constexpr (!PAIR) {
                 uint4 ej0 = make_uint4(0, 0, 0, 0);
                 bool mine = my_slot == s;
                 uint32_t nw[3] = { 0, 0, 0 };
