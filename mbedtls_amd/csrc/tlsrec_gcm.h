@@ -263,7 +263,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     const uint8_t *hor = WP ? lds + LY::GH + (PAIR ? pr : wave) * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
     uint32_t phase = 0;                                  /* PAIR barrier count */
     auto passes = [&](uint32_t my_slot, uint32_t my_rec, uint32_t my_d) __attribute__((always_inline)) {
-        if constexpr (PAIR) {
+        if constexpr (WP) {
             /* E_K(J0) of the lane's own record under its own key, once, before
              * the passes (r05): per key pass it cost a whole SIMD AES for the
              * few lanes of that key -- with 16 records per key, one AES per
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const tlsrec_key_material km = a.slots[s].km;
 
             /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
-            if constexpr (!PAIR) {
+            if constexpr (!WP) {
                 uint4 ej0 = make_uint4(0, 0, 0, 0);
                 bool mine = my_slot == s;
                 uint32_t nw[3] = { 0, 0, 0 };
