@@ -261,9 +261,14 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
     /* Horner multiplier table H^L (hor) and the per-record tables H^1..H^(L/2) (gp) */
     constexpr int HPI = WP ? 0 : LOGL;                   /* H^L table index from hor */
     const uint8_t *hor = WP ? lds + LY::GH + (PAIR ? pr : wave) * 8192 : (G5 ? lds + LY::HG5 : lds + LY::GH);
+    /* E_K(J0) once per lane before the passes (r05) -- every AES kernel but
+     * the single-key G5 one, whose one pass covers all its lanes anyway (in
+     * the 16-wave key passes: c4 +0.6 %, and the ARIA / Camellia kernels
+     * 0 / -1.2 % same box, so those keep the per-pass AES) */
+    constexpr bool EJ0_ONCE = WP || (!G5 && !ARIA);
     uint32_t phase = 0;                                  /* PAIR barrier count */
     auto passes = [&](uint32_t my_slot, uint32_t my_rec, uint32_t my_d) __attribute__((always_inline)) {
-        if constexpr (WP) {
+        if constexpr (EJ0_ONCE) {
             /* E_K(J0) of the lane's own record under its own key, once, before
              * the passes (r05): per key pass it cost a whole SIMD AES for the
              * few lanes of that key -- with 16 records per key, one AES per
@@ -278,8 +283,12 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 make_plan<DEC, CID>(p, d, km, ss, a.in);
                 uint32_t nw[3];
                 nonce_words<DEC>(p, d, km, a.in, nw);
-                ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, (const uint32_t *) ss->rkr,
-                                               make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+                if constexpr (ARIA)
+                    ej0 = alt_encrypt<NR, LY::AES>(lds, lanebase, (const uint32_t *) ss->ark,
+                                                   make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
+                else
+                    ej0 = aes_encrypt<NR, LY::AES>(lds, lanebase, (const uint32_t *) ss->rkr,
+                                                   make_uint4(nw[0], nw[1], nw[2], bswap32(1u)));
             }
             reinterpret_cast<uint4 *>(lds + LY::EJ0)[wave * 64 + lane] = ej0;
         }
@@ -352,7 +361,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
             const tlsrec_key_material km = a.slots[s].km;
 
             /* ---- pre-pass: E_K(J0) for each record of this wave's chunk ---- */
-            if constexpr (!WP) {
+            if constexpr (!EJ0_ONCE) {
                 uint4 ej0 = make_uint4(0, 0, 0, 0);
                 bool mine = my_slot == s;
                 uint32_t nw[3] = { 0, 0, 0 };
