@@ -2,6 +2,7 @@
 # End-of-round measurement on one box (each part under the 20-minute limit):
 #   tools/gpu_final.sh rows    -- -m gpu suite, smoke, every DESIGN row
 #   tools/gpu_final.sh prof1   -- rocprofv3 stats + PMC (incl. sized reads): c2 c3 c4s k4
+#   tools/gpu_final.sh prof1b  -- prof1 for c4s and k4 only
 #   tools/gpu_final.sh prof2   -- the same for c4, c2s, DTLS 1.4 KiB AES-128-GCM, stream 1.4 KiB
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -50,6 +51,11 @@ prof1)
   PMC_RECORDS=262144 profiles/run_profile.sh ${T}_k4 --config k4 > $O/prof_k4.log 2>&1 || { echo "k4 failed"; tail -5 $O/prof_k4.log; exit 1; }
   echo prof1 done
   ;;
+prof1b)   # prof1 without c2 / c3 (their kernels unchanged since the last prof1)
+  PMC_RECORDS=4194304 profiles/run_profile.sh ${T}_c4s --config c4s > $O/prof_c4s.log 2>&1 || { echo "c4s failed"; tail -5 $O/prof_c4s.log; exit 1; }
+  PMC_RECORDS=262144 profiles/run_profile.sh ${T}_k4 --config k4 > $O/prof_k4.log 2>&1 || { echo "k4 failed"; tail -5 $O/prof_k4.log; exit 1; }
+  echo prof1b done
+  ;;
 prof2)
   PMC_RECORDS=4194304 profiles/run_profile.sh ${T}_c4 --config c4 > $O/prof_c4.log 2>&1 || { echo "c4 failed"; tail -5 $O/prof_c4.log; exit 1; }
   PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2s --config c2s > $O/prof_c2s.log 2>&1 || { echo "c2s failed"; tail -5 $O/prof_c2s.log; exit 1; }
@@ -58,5 +64,5 @@ prof2)
   profiles/run_profile.sh ${T}_stream16 --cmd tools/bench_stream.py --conns 65536 --recs 16 --steps 3 > $O/prof_stream16.log 2>&1 || { echo "stream16 failed"; tail -5 $O/prof_stream16.log; exit 1; }
   echo prof2 done
   ;;
-*) echo "usage: tools/gpu_final.sh rows|prof1|prof2"; exit 2;;
+*) echo "usage: tools/gpu_final.sh rows|prof1|prof1b|prof2"; exit 2;;
 esac
