@@ -23,6 +23,22 @@
 #define TLSREC_CLMUL_FN static inline
 #endif
 
+/* a ^ b ^ c ^ d on 64-bit values: two three-input XORs per word on the
+ * device (gfx950 v_bitop3_b32), which the compiler does not form itself here */
+TLSREC_CLMUL_FN uint64_t tlsrec_xor4_64(uint64_t a, uint64_t b, uint64_t c, uint64_t d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32(
+        __builtin_amdgcn_bitop3_b32((uint32_t) a, (uint32_t) b, (uint32_t) c, 0x96), (uint32_t) d, 0u, 0x96);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32(
+        __builtin_amdgcn_bitop3_b32((uint32_t) (a >> 32), (uint32_t) (b >> 32), (uint32_t) (c >> 32), 0x96),
+        (uint32_t) (d >> 32), 0u, 0x96);
+    return ((uint64_t) hi << 32) | lo;
+#else
+    return a ^ b ^ c ^ d;
+#endif
+}
+
 /* carry-less 32 x 32 -> 64: bit class c of x (bits = c mod 4) times bit
  * class d of y lands on class c + d; at most 8 terms meet at a bit, so their
  * integer sum stays below 16 and never carries into the next bit of the
@@ -31,22 +47,32 @@ TLSREC_CLMUL_FN uint64_t tlsrec_clmul32(uint32_t x, uint32_t y)
 {
     const uint64_t x0 = x & 0x11111111u, x1 = x & 0x22222222u, x2 = x & 0x44444444u, x3 = x & 0x88888888u;
     const uint64_t y0 = y & 0x11111111u, y1 = y & 0x22222222u, y2 = y & 0x44444444u, y3 = y & 0x88888888u;
-    const uint64_t z0 = (x0 * y0) ^ (x1 * y3) ^ (x2 * y2) ^ (x3 * y1);
-    const uint64_t z1 = (x0 * y1) ^ (x1 * y0) ^ (x2 * y3) ^ (x3 * y2);
-    const uint64_t z2 = (x0 * y2) ^ (x1 * y1) ^ (x2 * y0) ^ (x3 * y3);
-    const uint64_t z3 = (x0 * y3) ^ (x1 * y2) ^ (x2 * y1) ^ (x3 * y0);
-    return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) | (z2 & 0x4444444444444444ull) |
-           (z3 & 0x8888888888888888ull);
+    const uint64_t z0 = tlsrec_xor4_64(x0 * y0, x1 * y3, x2 * y2, x3 * y1);
+    const uint64_t z1 = tlsrec_xor4_64(x0 * y1, x1 * y0, x2 * y3, x3 * y2);
+    const uint64_t z2 = tlsrec_xor4_64(x0 * y2, x1 * y1, x2 * y0, x3 * y3);
+    const uint64_t z3 = tlsrec_xor4_64(x0 * y3, x1 * y2, x2 * y1, x3 * y0);
+    /* class c of the product from z_c: three masked merges under the disjoint
+     * class masks (one v_bitop3_b32 per word each) instead of four ANDs and
+     * three ORs */
+    uint64_t r = z3;
+    r = (z2 & 0x4444444444444444ull) | (r & ~0x4444444444444444ull);
+    r = (z1 & 0x2222222222222222ull) | (r & ~0x2222222222222222ull);
+    r = (z0 & 0x1111111111111111ull) | (r & ~0x1111111111111111ull);
+    return r;
 }
 
 /* GCM bytes (little-endian word of bytes 4k..4k+3) <-> polynomial word k
  * (bit j = coefficient of x^(32k+j)): reverse the bits of each byte */
 TLSREC_CLMUL_FN uint32_t tlsrec_brev8x4(uint32_t w)
 {
+#if defined(__clang__)
+    return __builtin_bswap32(__builtin_bitreverse32(w));     /* v_bfrev_b32 + v_perm_b32 */
+#else
     w = ((w >> 1) & 0x55555555u) | ((w & 0x55555555u) << 1);
     w = ((w >> 2) & 0x33333333u) | ((w & 0x33333333u) << 2);
     w = ((w >> 4) & 0x0F0F0F0Fu) | ((w & 0x0F0F0F0Fu) << 4);
     return w;
+#endif
 }
 
 /* 64 x 64 -> 128 (Karatsuba over 32-bit halves); a, b: 2 words, r: 4 words */

@@ -156,7 +156,10 @@ __device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, cons
  * P[k] = H^(2^k) held as values (k <= 4: L <= 32): for the wave passes, whose
  * per-record tables otherwise come from HBM (a key's H^8, H^4, H^2 tables, 24
  * KiB, for 4 records of 16 KiB at L = 16). */
-__device__ __forceinline__ uint4 gf_mul_v(uint4 x, uint4 p)
+/* Out of line (r05): inlined, its ~600 instructions shifted the register
+ * allocation and schedule of the record loop around it (a faster multiply
+ * cost k4 1.2 % through a 5-instruction longer step loop, same box). */
+__device__ __noinline__ uint4 gf_mul_v(uint4 x, uint4 p)
 {
     const uint32_t a[4] = { x.x, x.y, x.z, x.w }, b[4] = { p.x, p.y, p.z, p.w };
     uint32_t r[4];

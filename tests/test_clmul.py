@@ -1,5 +1,5 @@
 """CPU test of the table-free GF(2^128) multiply (mbedtls_amd/csrc/tlsrec_clmul.h):
-tests/c/libclmul_check.so (gcc) against the oracle's bitwise orc_gf128_mul
+tests/c/libclmul_check.so (gcc; and ROCm's clang) against the oracle's bitwise orc_gf128_mul
 (the GCM multiply of SP 800-38D 6.3) on random and edge operands, the
 identity element and commutativity."""
 import ctypes
@@ -11,13 +11,17 @@ import pytest
 from tests.prng import prng_bytes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "tests", "c", "libclmul_check.so")
+CLANG = "/opt/rocm/llvm/bin/clang"
 
 
-@pytest.fixture(scope="module")
-def libs():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c"), "libclmul_check.so"], check=True)
-    c = ctypes.CDLL(LIB)
+@pytest.fixture(scope="module", params=["libclmul_check.so", "libclmul_check_clang.so"], ids=["gcc", "clang"])
+def libs(request):
+    """gcc builds the portable branches of tlsrec_clmul.h; ROCm's clang the
+    __clang__ ones the kernels compile (the bit reversal by builtins)"""
+    if request.param.endswith("_clang.so") and not os.path.exists(CLANG):
+        pytest.skip("no ROCm clang")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c"), request.param], check=True)
+    c = ctypes.CDLL(os.path.join(ROOT, "tests", "c", request.param))
     import oracle as O
     return c, O
 
