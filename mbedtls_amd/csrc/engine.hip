@@ -679,7 +679,13 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     } yg{ st, !opt.coalesced };
     if (yg.on) tlsrec__server_yield();
     BucketScratch bs;
-    const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced;
+    /* (r05) a table of ChaCha20-Poly1305 keys only needs no grouping either:
+     * its kernel walks records in arrival order, with or without the bucket
+     * pass's permutation, and flags unusable slots in identity order -- the
+     * count / scan / scatter kernels cost 5-6 % of a 1 M-record stream or
+     * DTLS batch */
+    const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced ||
+                          kt->cipher_mask == (1u << TLSREC_CIPHER_CHACHA20_POLY1305);
     if (identity) {
         if (!prefilled && tlsrec__launch_res_guard(res, n, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else {
