@@ -284,6 +284,37 @@ def test_dispositions_match_oracle():
     tab.close()
 
 
+def test_many_datagrams_per_connection():
+    """More datagrams per connection than the receive walks' lane group (16,
+    stream.hip DG_G): 37 and 50 datagrams of one to three records, a bad MAC
+    and a replay among them, and a connection with none -- record order and
+    dispositions against the oracle"""
+    slots = [(M.CIPHER_AES_128_GCM, prng_bytes(13, 16), prng_bytes(14, 16), b""),
+             (M.CIPHER_CHACHA20_POLY1305, prng_bytes(15, 32), prng_bytes(16, 16), b"")]
+    tab = Table(slots)
+
+    def rec(slot, seq, n):
+        st, w, _, _ = O.dtls_encrypt(tab.ot[slot], prng_bytes(seq + 97 * slot, n), 23, ctr(1, seq), 16384)
+        assert st == 0
+        return w
+
+    grams0, seq = [], 0
+    for k in range(37):
+        g = b""
+        for _ in range(1 + k % 3):
+            g += rec(0, seq, 40 + 13 * (seq % 7))
+            seq += 1
+        grams0.append(g)
+    bad = bytearray(grams0[20])
+    bad[30] ^= 0x04
+    grams0[20] = bytes(bad)
+    grams0.append(grams0[5])                       # a replayed datagram
+    grams1 = [rec(1, k, 100 + k) for k in range(50)]
+    conns = [(0, {"in_epoch": 1}, grams0), (1, {"in_epoch": 1}, []), (1, {"in_epoch": 1}, grams1)]
+    check_vs_oracle(tab, conns, tab.decrypt(conns))
+    tab.close()
+
+
 def test_tls13_slot_is_bad_input():
     tab = Table([(M.CIPHER_AES_128_GCM, bytes(16), bytes(16), b"")], tls=M.VERSION_TLS1_3)
     t12 = O.Transform(O.TLS1_2, O.AES_128_GCM, bytes(16), bytes(16), bytes(16), bytes(16))
