@@ -206,6 +206,56 @@ def inner_len(content, tls):
     return content
 
 
+ROOFLINE_SCOPE = ("per GPU: achieved / frac / kernel_ms_avg are rank 0's kernel; per_rank lists every rank's, "
+                  "frac_min_over_ranks the slowest GPU's")
+
+
+def rank_timing(dist, wall, kern_ms, dev):
+    """The step wall time as the max over ranks, and every rank's average
+    kernel time (HIP events on its own launch stream), all-gathered so that
+    rank 0's line carries them.  dist None: one process."""
+    import torch
+    avg = float(np.mean(kern_ms)) if len(kern_ms) else 0.0
+    if dist is None:
+        return wall, [avg]
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    mine = torch.tensor([avg], dtype=torch.float64, device=dev)
+    allk = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(allk, mine)
+    return float(t.item()), [float(x.item()) for x in allk]
+
+
+def per_rank_roofline(kern_ms_ranks, alg_bytes_per_launch):
+    """Each rank's achieved GB/s and fraction of the HBM peak from its own
+    average kernel time, plus the minimum fraction (the slowest GPU)."""
+    rows = []
+    for r, ms in enumerate(kern_ms_ranks):
+        ach = alg_bytes_per_launch / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        rows.append({"rank": r, "kernel_ms_avg": round(ms, 4), "achieved": round(ach, 2),
+                     "frac": round(ach / HBM_PEAK_GBS, 4)})
+    return {"per_rank": rows, "frac_min": min(x["frac"] for x in rows) if rows else None,
+            "kernel_ms_max": max(x["kernel_ms_avg"] for x in rows) if rows else None}
+
+
+def rank0_legs(dist, rank, run_cpu, run_e2e):
+    """The CPU baseline and the host-buffer (e2e) legs, on rank 0 at every
+    world size, outside the timed region: all ranks meet at a barrier, rank 0
+    runs the legs while the others wait at a second one (so the legs share
+    the box with idle GPUs only).  run_* None: the leg is switched off."""
+    if dist is not None:
+        dist.barrier()
+    cpu = e2e = None
+    try:
+        if rank == 0:
+            cpu = run_cpu() if run_cpu else None
+            e2e = run_e2e() if run_e2e else None
+    finally:
+        if dist is not None:
+            dist.barrier()
+    return cpu, e2e
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -343,10 +393,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    wall, kern_ranks = rank_timing(dist if distributed else None, wall, kern_ms, dev)
 
     # ---- correctness of what was timed ----------------------------------------
     st = res_dev.view(torch.int32)[0::4]
@@ -399,6 +446,7 @@ def main():
         alg_desc = content + wire + 40 + 16
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
     achieved = alg_per_rec * n / kern_avg_s / 1e9
+    per_rank = per_rank_roofline(kern_ranks, alg_per_rec * n)
     # HBM traffic per launch: PMC FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE
     # per record, measured by profiles/run_profile.sh on this config and
     # committed as profiles/traffic_<config>.json, scaled to this launch (not
@@ -438,17 +486,17 @@ def main():
     payload_total = float(n) * inner * world
     value = payload_total / steps_s / 2**30
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(cname, ver, content, inner, wire, stride, km, args.cpu_seconds, direction)
-
-    # records in host memory: pinned socket buffers -> device -> pinned (the
-    # boundary the reference's callers hand over, ssl_msg.c:1855 / :2058);
-    # reported beside the device-resident value, never as it
-    e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = end_to_end(M, kt, recs, arena, out_arena, n, stride, lead, head, content, wire, inner, direction,
-                         args.e2e_records)
+    # the CPU leg and the host-buffer leg run on rank 0 at every world size,
+    # after the timed region (the other ranks wait at a barrier): records in
+    # host memory are pinned socket buffers -> device -> pinned (the boundary
+    # the reference's callers hand over, ssl_msg.c:1855 / :2058), reported
+    # beside the device-resident value, never as it
+    run_cpu = None if args.no_cpu else (
+        lambda: cpu_baseline(cname, ver, content, inner, wire, stride, km, args.cpu_seconds, direction))
+    run_e2e = None if args.no_e2e else (
+        lambda: end_to_end(M, kt, recs, arena, out_arena, n, stride, lead, head, content, wire, inner, direction,
+                           args.e2e_records))
+    cpu, e2e = rank0_legs(dist if distributed else None, rank, run_cpu, run_e2e)
 
     if world > 1 and args.config == "c2":
         # BASELINE configs[4] (c5): the c2 shard on every rank, keys broadcast over RCCL
@@ -472,7 +520,7 @@ def main():
                    "lanes_per_record": args.lanes or "auto", "slot_align": args.align, "aead_region_offset": lead + head,
                    "parallelism": f"shard{world}"},
         "records_per_s": round(n * world / steps_s, 1),
-        "roofline": {"bound": "hbm", "limiter": (f"{ceiling['limiter']} ({ceiling['busy_frac']:.0%} busy, measured)"
+        "roofline": {"bound": "hbm", "scope": ROOFLINE_SCOPE, "limiter": (f"{ceiling['limiter']} ({ceiling['busy_frac']:.0%} busy, measured)"
                                                  if ceiling else None),
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -484,7 +532,9 @@ def main():
                      "algorithmic_bytes_per_record_with_descriptors": alg_desc,
                      "frac_with_descriptors": round(alg_desc * n / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                      "kernel_ms_avg": round(kern_avg_s * 1e3, 4),
-                     "timing": "HIP events on the launch stream around each timed step"},
+                     "timing": "HIP events on the launch stream around each timed step",
+                     "per_rank": per_rank["per_rank"], "frac_min_over_ranks": per_rank["frac_min"],
+                     "kernel_ms_max_over_ranks": per_rank["kernel_ms_max"]},
         "cpu_baseline": cpu,
         "e2e": e2e,
         "check": {"bad_records": bad, "oracle_sample_ok": oracle_ok},

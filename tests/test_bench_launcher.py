@@ -48,6 +48,32 @@ def test_launcher_forms_a_world_of_n_ranks(world):
     assert len({r["pid"] for r in j["ranks"]}) == world     # one process per rank
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_multi_rank_line_carries_cpu_baseline_and_per_rank_roofline(world):
+    """at N > 1 the line keeps the CPU leg (rank 0, after the
+    timed region, the other ranks held at a barrier until it ends) and the
+    roofline is per GPU -- every rank's kernel time all-gathered, per-rank
+    fractions and their minimum; the wall time is the max over ranks."""
+    p = _launch(world, [str(world), "-1", "line"], timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    j = json.loads(lines[0])
+    assert j["world_size"] == world
+    assert j["wall"] == pytest.approx(0.1 * world)
+    assert j["kernel_ms"] == [10.0 + r for r in range(world)]
+    rows = j["roofline"]["per_rank"]
+    assert [r["rank"] for r in rows] == list(range(world))
+    assert j["roofline"]["frac_min"] == min(r["frac"] for r in rows) == rows[-1]["frac"]
+    assert j["roofline"]["kernel_ms_max"] == 10.0 + world - 1
+    cpu = j["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["legs"]
+    assert j["e2e"] == {"value": 1.0, "what": "stub"}
+    assert j["cpu_ran_on_this_rank"]
+    # no rank left the second barrier before rank 0's CPU leg had started
+    assert min(j["left_barrier"]) >= j["cpu_started"]
+
+
 def test_launcher_fails_when_a_rank_fails():
     """rank 1 exits 3 before joining; rank 0 would wait in the rendezvous
     forever -- the launcher stops it and returns the failing code"""
