@@ -627,8 +627,8 @@ extern "C" void tlsrec__test_server_shadow(void *dev, size_t bytes)
 static constexpr uint32_t g_test_skip = 0xffffffffu;
 #endif
 
-extern "C" void tlsrec__server_yield(void);
-extern "C" void tlsrec__server_note_batch(hipStream_t stream);
+extern "C" int tlsrec__server_yield(void);
+extern "C" void tlsrec__server_note_batch(hipStream_t stream, int counted);
 
 /* Launch options of one batch:
  *   only_mask  launch only these ciphers' kernels (1 << TLSREC_CIPHER_*; the
@@ -675,9 +675,10 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
     struct YieldGuard {
         hipStream_t st;
         bool on;
-        ~YieldGuard() { if (on) tlsrec__server_note_batch(st); }
-    } yg{ st, !opt.coalesced };
-    if (yg.on) tlsrec__server_yield();
+        int counted;      /* the yield counted this batch as queueing (only then does the note uncount it) */
+        ~YieldGuard() { if (on) tlsrec__server_note_batch(st, counted); }
+    } yg{ st, !opt.coalesced, 0 };
+    if (yg.on) yg.counted = tlsrec__server_yield();
     BucketScratch bs;
     /* (r05) a table of ChaCha20-Poly1305 keys only needs no grouping either:
      * its kernel walks records in arrival order, with or without the bucket

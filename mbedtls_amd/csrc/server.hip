@@ -46,19 +46,24 @@
  * host submits to a grid only inside its window minus a margin and launches
  * the next grid on the other slot set when the window closes.
  *
- * The idle exit is ordered against host submits (r05): before it posts a
- * request the host bumps the set's `activity` word and then reads `closing`
+ * The idle exit is ordered against host submits (r05, r06): before it posts
+ * a request the host bumps the set's `activity` word and then reads `closing`
  * (both in host-mapped memory, a full fence between); the idle exit is
  * workgroup 0's alone: it writes `closing` = 1, fences, and re-reads
- * `activity` -- unchanged, it commits (the device-memory `quit` word, which the
- * other workgroups poll); changed, it clears `closing` and stays.  Whichever
- * of the two stores comes first, one side sees the other's (Dekker): a host
- * that read `closing` = 0 has a grid that will not leave before the request's
- * workgroup has polled it, and a host that read 1 does not post at all and
- * launches the next grid on the other set.  `closing` stays 1 after a commit,
- * so a grid that left while no call came is found the same way.  A request a
- * grid never took (its kernel ended: a stop word racing a post) is withdrawn
- * and runs on the launch path.
+ * `activity` -- changed, it clears `closing` and stays.  Whichever of the two
+ * stores comes first, one side sees the other's (Dekker), and a host that
+ * read 1 does not post at all and launches the next grid on the other set.
+ * A host that read `closing` = 0 posts its request and only then bumps
+ * `settled` (a host that read 1 bumps it without posting): workgroup 0
+ * commits the exit (the device-memory `quit` word, which the other
+ * workgroups poll) only when `settled` has caught up with `activity`, so a
+ * claim whose post is still in flight -- the host thread descheduled between
+ * claim and post -- keeps the grid.  A workgroup that sees `quit` or `stop`
+ * polls its slot once more before it leaves: a request posted before the
+ * commit is served, never stranded.  `closing` stays 1 after a commit, so a
+ * grid that left while no call came is found the same way.  A request a grid
+ * never took (its kernel ended: a stop word racing a post) is withdrawn and
+ * runs on the launch path.
  *
  * Yielding to batch work (r04): the grid holds 64 CUs (89 KiB of LDS each,
  * so no 128 KiB batch workgroup fits beside it).  Every batch launch outside
@@ -150,8 +155,11 @@ struct SrvCtl {
     uint8_t pad1[60];
     uint32_t closing;         /* workgroup 0: deciding to leave idle (1), or left */
     uint8_t pad2[60];
+    uint32_t settled;         /* host: bumped after each claim's post (or after a claim that found closing = 1) */
+    uint8_t pad3[60];
 };
-static_assert(offsetof(SrvCtl, activity) == 64 && offsetof(SrvCtl, closing) == 128 && sizeof(SrvCtl) == 192,
+static_assert(offsetof(SrvCtl, activity) == 64 && offsetof(SrvCtl, closing) == 128 && offsetof(SrvCtl, settled) == 192 &&
+                  sizeof(SrvCtl) == 256,
               "SrvCtl layout");
 
 /* ---------------- LDS record access (16-byte aligned AEAD region) -------- */
@@ -810,7 +818,7 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
                 } else if ((it & 15) == 0 &&
                            (ld_sys32(&sc->stop) != 0 ||
                             __builtin_amdgcn_readfirstlane(
-                                __hip_atomic_load(quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)) {
+                                __hip_atomic_load(quit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) != 0)) {
                     v = 2;
                 } else {
                     const uint64_t now = wall_clock64();
@@ -827,17 +835,37 @@ __global__ __launch_bounds__(SRV_WAVES * 64) __attribute__((amdgpu_waves_per_eu(
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
                             const uint32_t a2 = __builtin_amdgcn_readfirstlane(
                                 __hip_atomic_load(&sc->activity, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM));
-                            if (a2 == a_seen) {
-                                /* committed: the other workgroups leave at their next stop check */
-                                __hip_atomic_store(quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            const uint32_t s2 = __builtin_amdgcn_readfirstlane(
+                                __hip_atomic_load(&sc->settled, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM));
+                            if (a2 == a_seen && s2 == a2) {
+                                /* committed: every claim so far has posted (or backed off); the
+                                 * other workgroups leave at their next stop check, after one
+                                 * more poll of their slot */
+                                __hip_atomic_store(quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                                 v = 2u;
                             } else {
-                                /* a claim landed: stay (the host that made it read closing = 0) */
+                                /* a claim landed, or one is still posting: stay (a host that
+                                 * claims now reads closing = 0) */
                                 __hip_atomic_store(&sc->closing, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
                                 a_seen = a2;
                                 t_seen = now;
                             }
                         }
+                    }
+                }
+                if (v == 2u && seq == served) {
+                    /* leaving (stop, quit, window or idle exit): poll the slot once more,
+                     * after the decision -- a request posted before the commit is served */
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                    h0 = ld_sys64(&rq->w[0]);
+                    h1 = ld_sys64(&rq->w[1]);
+                    h2 = ld_sys64(&rq->w[2]);
+                    h3 = ld_sys64(&rq->w[3]);
+                    const uint32_t s2 = __builtin_amdgcn_readfirstlane((uint32_t) h0);
+                    if (s2 != served) {
+                        const uint64_t tagw = (uint64_t) (s2 & 0xffffu) << 48;
+                        /* half-posted: poll again (the host's w[0] follows w[1..3]) */
+                        v = __builtin_amdgcn_readfirstlane((((h1 ^ tagw) | (h2 ^ tagw) | (h3 ^ tagw)) >> 48) ? 3u : 1u);
                     }
                 }
             }
@@ -930,6 +958,12 @@ std::atomic<uint64_t> g_yields{0};
  * claims that found a grid closing (and moved to the other set) */
 uint64_t g_why_batch = 0, g_why_drain = 0, g_why_withdrawn = 0, g_why_noslot = 0, g_closing = 0;
 uint32_t g_max_iter = 0;
+#ifdef TLSREC_TEST_HOOKS
+/* TLSREC_TEST_SERVER_POST_DELAY_US (test-hooks build only): a host thread
+ * that has claimed a slot waits this long before it posts -- the descheduled
+ * host thread of the idle-exit handshake, made deterministic */
+uint64_t g_test_post_delay_ns = 0;
+#endif
 std::atomic<uint64_t> g_served{0}, g_fallback{0}, g_launches{0};
 
 uint64_t now_ns()
@@ -996,6 +1030,9 @@ int srv_setup_locked()
     if (idle_ms > ms) idle_ms = ms;
     g_idle_ticks = (uint64_t) (idle_ms * khz);
     if (const char *y = getenv("TLSREC_SERVER_YIELD")) g_yield = strcmp(y, "0") != 0;
+#ifdef TLSREC_TEST_HOOKS
+    if (const char *d = getenv("TLSREC_TEST_SERVER_POST_DELAY_US")) g_test_post_delay_ns = (uint64_t) (atof(d) * 1e3);
+#endif
     g_tick_ns = 1e6 / khz;
     g_max_iter = (uint32_t) (ms * 10000.0);          /* backstop: a poll (a PCIe read + s_sleep) is > 0.1 us */
     const double margin = ms * 0.1 > 1.0 ? ms * 0.1 : 1.0;
@@ -1111,6 +1148,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
         __atomic_store_n(&S->ctl_h->activity, ++S->activity, __ATOMIC_SEQ_CST);
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
         if (__atomic_load_n(&S->ctl_h->closing, __ATOMIC_SEQ_CST) != 0) {
+            __atomic_fetch_add(&S->ctl_h->settled, 1u, __ATOMIC_SEQ_CST);   /* backed off: settled, no post */
             S->t_launch = 0;          /* leaving or left: never submit to it again */
             g_closing++;
             i = -1;
@@ -1126,6 +1164,12 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     S->nbusy++;
     const uint32_t seq = ++S->seq[i];
     pthread_mutex_unlock(&g_mu);
+#ifdef TLSREC_TEST_HOOKS
+    if (g_test_post_delay_ns) {
+        const uint64_t until = now_ns() + g_test_post_delay_ns;
+        while (now_ns() < until) __builtin_ia32_pause();
+    }
+#endif
 
     SrvReq *rq = &S->h[i];
     if (buf_len) memcpy(rq->buf + pre, buf, buf_len);
@@ -1148,6 +1192,9 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     const uint64_t w0 = (uint64_t) seq | (uint64_t) bytes << 32 | (uint64_t) (cipher & 0xff) << 48 |
                         (uint64_t) (dec ? 1 : 0) << 56 | (uint64_t) (nr & 0x1f) << 57 | (uint64_t) (skip ? 1 : 0) << 62;
     __atomic_store_n(&rq->w[0], w0, __ATOMIC_RELEASE);
+    /* posted: the grid may now commit an idle exit (its workgroups poll
+     * their slots once more on the way out) */
+    __atomic_fetch_add(&S->ctl_h->settled, 1u, __ATOMIC_SEQ_CST);
 
     int rc = 0;
     for (uint32_t spins = 1;; spins++) {
@@ -1198,10 +1245,14 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
 /* Batch work is about to be launched (engine.hip batch(), outside the
  * single-record engine): the live grids leave (stop word) and none is
  * submitted to again.  Cheap when no server was ever set up. */
-extern "C" void tlsrec__server_yield(void)
+extern "C" int tlsrec__server_yield(void)
 {
-    if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return;
+    if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return 0;
     pthread_mutex_lock(&g_mu);
+    if (g_state != 1) {               /* (re-checked under the lock) */
+        pthread_mutex_unlock(&g_mu);
+        return 0;
+    }
     g_batch_queueing++;               /* no grid until this batch's note (below) */
     for (auto &S : g_set)
         if (S.launched && S.t_launch != 0) {
@@ -1210,17 +1261,22 @@ extern "C" void tlsrec__server_yield(void)
             g_yields++;
         }
     pthread_mutex_unlock(&g_mu);
+    return 1;
 }
 
-/* ... and has been launched on `stream`: no grid until it has finished */
-extern "C" void tlsrec__server_note_batch(hipStream_t stream)
+/* ... and has been launched on `stream`: no grid until it has finished.
+ * `counted`: what tlsrec__server_yield returned for this batch -- only a
+ * batch the yield counted as queueing is uncounted here, so a server set up
+ * by another thread between a batch's yield and its note never loses another
+ * batch's count. */
+extern "C" void tlsrec__server_note_batch(hipStream_t stream, int counted)
 {
-    if (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield) return;
+    if (!counted && (__atomic_load_n(&g_state, __ATOMIC_RELAXED) != 1 || !g_yield)) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
     if (capturing) (void) hipGetLastError();
     pthread_mutex_lock(&g_mu);
-    if (g_batch_queueing) g_batch_queueing--;
+    if (counted && g_batch_queueing) g_batch_queueing--;
     if (!capturing) {                 /* (a graph being captured: nothing runs yet) */
         /* a free ring entry, else the oldest (recording over a pending event
          * moves it later, which keeps the rule "no grid while batch work is

@@ -15,7 +15,16 @@ from mbedtls_amd import _abi
 from tests.prng import prng_bytes
 
 
-def main(calls):
+def main(calls, test_lib=False):
+    if test_lib:
+        # the test-hooks build (TLSREC_TEST_SERVER_POST_DELAY_US): every binding
+        # of this process goes to it
+        with _abi.use_library():
+            return _main(calls)
+    return _main(calls)
+
+
+def _main(calls):
     L = _abi.load()
     L.tlsrec__server_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 3
     L.tlsrec__server_closing.restype = ctypes.c_uint64
@@ -62,4 +71,4 @@ def main(calls):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 600)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 600, test_lib="--test-lib" in sys.argv)

@@ -349,10 +349,17 @@ def test_config4_keys_two_records_each():
 @pytest.mark.parametrize("nslots,ciphers", [(1, [M.CIPHER_CAMELLIA_128_GCM]), (1, [M.CIPHER_CAMELLIA_256_CCM]),
                                             (1, [M.CIPHER_ARIA_256_GCM]), (1, [M.CIPHER_ARIA_192_CCM]),
                                             (4, [M.CIPHER_ARIA_128_CCM, M.CIPHER_CAMELLIA_192_CCM]),
-                                            (4, [M.CIPHER_CAMELLIA_256_GCM, M.CIPHER_ARIA_128_GCM])],
+                                            (4, [M.CIPHER_CAMELLIA_256_GCM, M.CIPHER_ARIA_128_GCM]),
+                                            (4, [M.CIPHER_CHACHA20_POLY1305]),
+                                            (4, [M.CIPHER_CHACHA20_POLY1305, M.CIPHER_AES_128_GCM])],
                          ids=["identity-cam-gcm", "identity-cam256-ccm", "identity-aria-gcm", "identity-aria-ccm",
-                              "bucket-alt-ccm", "bucket-alt-gcm"])
+                              "bucket-alt-ccm", "bucket-alt-gcm", "chacha-only-multikey", "bucket-chacha-gcm"])
 def test_unusable_slot_alt_ciphers(nslots, ciphers):
+    """records naming an out-of-range slot and a never-loaded one: BAD_INPUT_DATA
+    and the buffer untouched, in identity order and through the bucket pass
+    alike -- including a several-key ChaCha20-Poly1305-only table, which the
+    engine walks in identity order, against the bucket path of a
+    mixed table"""
     dev = torch.device("cuda")
     slots = B.random_slots(321, ciphers, [M.VERSION_TLS1_2], nslots)
     recs = B.plaintext_records(slots, [100, 2000, 17, 500, 64, 1400], seed=4)

@@ -96,10 +96,14 @@ def test_served_records_match_oracle(cipher, ver):
     calls = 2 * len(LENGTHS) * 3
     why = _why()
     # The grid's idle exit is ordered against submits (server.hip, the
-    # activity / closing handshake): a call never posts to a grid that is
-    # leaving, so nothing is withdrawn, and a call that finds the grid gone
-    # launches the next one instead of taking the launch path.
-    assert why[2] == 0, f"withdrawn requests: {why}"
+    # activity / closing / settled handshake): a call never posts to a grid
+    # that is leaving, and a grid never leaves idle while a claim is still
+    # posting, so nothing is withdrawn by the idle exit; a call that finds the
+    # grid gone launches the next one instead of taking the launch path.  (A
+    # host thread descheduled past the end of a grid's 20-ms window can still
+    # see its request withdrawn -- it then runs on the launch path, and its
+    # bytes were checked against the oracle above like every other call's.)
+    assert why[2] <= 2, f"withdrawn requests: {why}"
     assert f1 - f0 <= 2, ("calls went back to the launch path (batch pending, set not drained, "
                           f"withdrawn, no slot so far: {why})")
     assert s1 - s0 >= calls - 2, "the record server did not serve these calls"
@@ -132,6 +136,28 @@ def test_idle_boundary_submits_are_never_withdrawn():
     assert r["fallback"] <= 2, r
     assert r["served"] >= r["calls"] - 2, r
     assert r["launches"] >= 20, r      # the grids left idle and were relaunched many times
+
+
+def test_idle_exit_waits_for_a_claim_still_posting():
+    """a host thread that claimed a slot but has not posted yet
+    (here held 300 us between claim and post by the test-hooks build's
+    TLSREC_TEST_SERVER_POST_DELAY_US, six times the 50-us idle limit) keeps
+    the grid: workgroup 0 commits the idle exit only when every claim has
+    settled, so no request is withdrawn and every call is served by a grid."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, TLSREC_SERVER_IDLE_MS="0.05", TLSREC_TEST_SERVER_POST_DELAY_US="300")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-m", "tests._server_idle_child", "200", "--test-lib"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["errors"] == [], r["errors"][:4]
+    assert r["why"][2] == 0, r
+    assert r["fallback"] <= 2, r
+    assert r["served"] >= r["calls"] - 2, r
 
 
 @pytest.mark.parametrize("cipher", SERVED)
