@@ -77,6 +77,7 @@
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -942,6 +943,12 @@ uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr
          g_tr_b1 = 0;
 double g_tick_ns = 10.0;
 uint64_t g_submit_ns = 0, g_life_ticks = 0, g_idle_ticks = 0;
+/* a waiting host thread spins this long, then yields its CPU between polls
+ * (TLSREC_SERVER_SPIN_US; < 0: spin only): with more calling threads than
+ * CPUs, pure spinning kept the threads whose requests were done -- and the
+ * one holding the slot lock -- off the CPUs (r05: 32 threads on the box's 16
+ * CPUs served 137 K round trips/s against 218 K with 16) */
+int64_t g_spin_ns = 20000;
 /* batch work (tlsrec__server_yield / _note_batch): no grid while any is
  * queued or pending.  Batches may run on several streams at once: each
  * records its own event in a small ring, and the batches between their yield
@@ -1030,6 +1037,7 @@ int srv_setup_locked()
     if (idle_ms > ms) idle_ms = ms;
     g_idle_ticks = (uint64_t) (idle_ms * khz);
     if (const char *y = getenv("TLSREC_SERVER_YIELD")) g_yield = strcmp(y, "0") != 0;
+    if (const char *sp = getenv("TLSREC_SERVER_SPIN_US")) g_spin_ns = (int64_t) (atof(sp) * 1e3);
 #ifdef TLSREC_TEST_HOOKS
     if (const char *d = getenv("TLSREC_TEST_SERVER_POST_DELAY_US")) g_test_post_delay_ns = (uint64_t) (atof(d) * 1e3);
 #endif
@@ -1062,6 +1070,17 @@ int srv_setup_locked()
 
 bool kernel_done(SrvSet &S) { return !S.launched || hipEventQuery(S.ev) != hipErrorNotReady; }
 
+/* every slot of S that a host thread holds has its request answered (done ==
+ * the posted sequence number); an unanswered one is about to be withdrawn by
+ * its thread, and a new grid must not serve it behind that thread's back */
+bool held_slots_served(SrvSet &S)
+{
+    if (S.nbusy == 0) return true;
+    for (int k = 0; k < SRV_SLOTS; k++)
+        if (S.busy[k] && __atomic_load_n(&S.h[k].done, __ATOMIC_ACQUIRE) != S.seq[k]) return false;
+    return true;
+}
+
 /* Under g_mu: the set to submit to, launching the next grid when the current
  * one's window has closed; NULL = not now (the caller takes the launch path). */
 SrvSet *srv_current_locked(uint64_t now)
@@ -1083,8 +1102,13 @@ SrvSet *srv_current_locked(uint64_t now)
         g_batch_pending &= ~(1u << k);
     }
     SrvSet *N = &g_set[g_cur ^ 1];
-    /* the other set must be drained: its grid ended, no host thread in it */
-    if (N->nbusy != 0 || !kernel_done(*N)) {
+    /* the other set must be drained: its grid ended, and every slot a host
+     * thread still holds was served -- its thread, descheduled past the
+     * window (more calling threads than CPUs), only reads its result back,
+     * which the next grid never touches: it serves a slot only when a new
+     * sequence number is posted there (r06: waiting for those threads to run
+     * sent 30-90 of 128 K calls at 32 threads to the launch path) */
+    if (!kernel_done(*N) || !held_slots_served(*N)) {
         g_why_drain++;
         return nullptr;
     }
@@ -1197,9 +1221,11 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     __atomic_fetch_add(&S->ctl_h->settled, 1u, __ATOMIC_SEQ_CST);
 
     int rc = 0;
+    const uint64_t t_post = g_spin_ns >= 0 ? now_ns() : 0;
     for (uint32_t spins = 1;; spins++) {
         if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
         __builtin_ia32_pause();
+        if (g_spin_ns >= 0 && (spins & 63) == 0 && now_ns() - t_post > (uint64_t) g_spin_ns) sched_yield();
         hipError_t eq;
         if ((spins & 4095) == 0 && (eq = hipEventQuery(S->ev)) != hipErrorNotReady) {
             /* the grid has ended: served just before, or never taken */

@@ -88,6 +88,13 @@ def lib():
                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
                                               ctypes.c_void_p]
         L.orc_bench_records_multi.restype = ctypes.c_double
+        L.orc_bench_stream_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.orc_bench_stream_rows.restype = ctypes.c_double
+        L.orc_bench_keysched.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_bench_keysched.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -627,6 +634,10 @@ def evp_lib():
         L.evp_mixed_records.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
         L.evp_mixed_records.restype = ctypes.c_double
+        L.evp_mixed_stream.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.c_void_p]
+        L.evp_mixed_stream.restype = ctypes.c_double
         L.evp_call_profile.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.evp_call_profile.restype = ctypes.c_int
         L.evp_check_records.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p,
@@ -662,6 +673,32 @@ def bench_multi(transforms, direction: int, arena, stride: int, data_len: int, n
                                          threads, status.ctypes.data)
 
 
+def bench_stream_rows(transforms, dtls: bool, direction: int, inp, in_stride: int, in_len: int, out,
+                      out_stride: int, max_frag: int, threads: int, status) -> float:
+    """Time orc_bench_stream_rows (oracle/rows_bench.c): connection c under
+    transforms[c] sends (direction 1) its in_len bytes of application data as
+    max_frag records (orc_stream_encrypt / orc_dtls_encrypt) or receives (0)
+    its in_len wire bytes in place (orc_stream_decrypt / orc_dtls_decrypt;
+    DTLS: max_frag = one datagram's wire size).  Seconds."""
+    arr = (ctypes.c_void_p * len(transforms))(*[ctypes.addressof(t._mem) for t in transforms])
+    return lib().orc_bench_stream_rows(arr, len(transforms), int(bool(dtls)), direction, inp.ctypes.data, in_stride,
+                                       in_len, out.ctypes.data if out is not None else None, out_stride, max_frag,
+                                       threads, status.ctypes.data)
+
+
+def bench_keysched(alg: int, secrets, count: int, update: bool, keylen: int, threads: int):
+    """Time orc_bench_keysched: per connection KeyUpdate (optional) then
+    HKDF-Expand-Label key / iv (ssl_tls13_keys.c:219-291).  Returns (seconds,
+    out keys (count, keylen + 12), status)."""
+    import numpy as np
+    sec = np.ascontiguousarray(secrets, dtype=np.uint8)
+    out = np.zeros((count, keylen + 12), dtype=np.uint8)
+    st = np.zeros(count, dtype=np.int32)
+    t = lib().orc_bench_keysched(alg, sec.ctypes.data, count, int(bool(update)), keylen, threads, out.ctypes.data,
+                                 st.ctypes.data)
+    return t, out, st
+
+
 class EvpMixed:
     """evp_mixed_*: one OpenSSL EVP context per connection (the c4 / c4s CPU
     leg).  ciphers: uint8 array (AES_128_GCM / AES_256_GCM / CHACHA20_POLY1305
@@ -684,6 +721,17 @@ class EvpMixed:
         """n records on the threads given at construction"""
         return evp_lib().evp_mixed_records(self._h, direction, arena.ctypes.data, stride, data_len, n,
                                            status.ctypes.data)
+
+    def stream(self, dtls: bool, direction: int, inp, in_stride: int, in_len: int, out, out_stride: int,
+               max_frag: int, status) -> float:
+        """evp_mixed_stream: connection c's records sent (direction 1: in_len
+        bytes of application data -> max_frag records in `out`) or received
+        (0: in_len wire bytes decrypted in place; DTLS: max_frag = one
+        datagram's wire size), the stream (ssl_msg.c:4700-4907 / :2648-2793)
+        or DTLS 1.2 framing around one EVP AEAD per record.  Seconds."""
+        return evp_lib().evp_mixed_stream(self._h, int(bool(dtls)), direction, inp.ctypes.data, in_stride, in_len,
+                                          out.ctypes.data if out is not None else None, out_stride, max_frag,
+                                          status.ctypes.data)
 
     def close(self):
         if self._h:

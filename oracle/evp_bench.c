@@ -64,8 +64,10 @@ static EVP_CIPHER *eb_fetch(OSSL_LIB_CTX *lc, int c)
 
 /* One record through an EVP context that already holds its connection's key:
  * the framing of mbedtls_ssl_encrypt_buf / _decrypt_buf around one AEAD. */
-static int32_t eb_record(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, const uint8_t *iv, uint8_t *buf,
-                         size_t data_len, uint64_t seq)
+/* v0 v1: the version bytes of the TLS 1.2 AAD (3 3; DTLS 1.2 writes fe fd,
+ * and its 8-byte sequence is epoch || seq48) */
+static int32_t eb_record_v(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, const uint8_t *iv, uint8_t *buf,
+                           size_t data_len, uint64_t seq, uint8_t v0, uint8_t v1)
 {
     const int explicit_iv = !tls13 && cipher != EB_CHACHA20_POLY1305;   /* ivlen != fixed_ivlen, :739-743 */
     uint8_t ctr[8], nonce[12], aad[13];
@@ -97,7 +99,7 @@ static int32_t eb_record(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, co
             aadlen = 5;
         } else {
             memcpy(aad, ctr, 8);
-            aad[8] = 23; aad[9] = 3; aad[10] = 3; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
+            aad[8] = 23; aad[9] = v0; aad[10] = v1; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
             aadlen = 13;
         }
         ok = EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 1) == 1 &&
@@ -121,7 +123,7 @@ static int32_t eb_record(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, co
         aadlen = 5;
     } else {
         memcpy(aad, ctr, 8);
-        aad[8] = 23; aad[9] = 3; aad[10] = 3; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
+        aad[8] = 23; aad[9] = v0; aad[10] = v1; aad[11] = (uint8_t) (len >> 8); aad[12] = (uint8_t) len;
         aadlen = 13;
     }
     ok = EVP_CipherInit_ex(ctx, NULL, NULL, NULL, nonce, 0) == 1 &&
@@ -140,6 +142,12 @@ static int32_t eb_record(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, co
         return k == 0 ? -0x7200 : 0;
     }
     return 0;
+}
+
+static int32_t eb_record(EVP_CIPHER_CTX *ctx, int cipher, int tls13, int dir, const uint8_t *iv, uint8_t *buf,
+                         size_t data_len, uint64_t seq)
+{
+    return eb_record_v(ctx, cipher, tls13, dir, iv, buf, data_len, seq, 3, 3);
 }
 
 static void *eb_worker(void *arg)
@@ -458,4 +466,186 @@ int evp_check_records(int mode, int cipher, int tls13, uint32_t nkeys, const uin
     }
     for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
     return 0;
+}
+
+/* ---- the SURVEY §8(f) rows: record framing of a connection around EVP -----
+ * tools/bench_stream.py / bench_dtls.py's "evp" CPU leg.  Connection c (its
+ * key context made by evp_mixed_create, served by thread c % threads) sends
+ * or receives its records in order, as one thread serving that socket would:
+ *   stream receive: the header walk of ssl_get_next_record
+ *     (ssl_parse_record_header ssl_msg.c:3561-3776: type, version, length
+ *     checks), decrypt_buf (one EVP AEAD), the zero-length and counter rules of
+ *     ssl_prepare_record_content (:3914-3966);
+ *   stream send: mbedtls_ssl_write_record (:2648-2793): max_frag records, the
+ *     5-byte header, encrypt_buf (one EVP AEAD), counter increment;
+ *   DTLS receive: the 13-byte header (epoch, explicit 48-bit sequence), the
+ *     anti-replay window check and update (mbedtls_ssl_dtls_replay_check /
+ *     _update, :4240-4330), decrypt_buf;
+ *   DTLS send: the 13-byte header with epoch || seq, encrypt_buf.
+ * status[c]: 0, or the first error of the connection. */
+typedef struct {
+    const eb_mixed *m;
+    int dtls, dir, t;
+    uint8_t *in;
+    size_t in_stride, in_len;
+    uint8_t *out;
+    size_t out_stride, max_frag;
+    int32_t *status;
+} eb_rjob;
+
+static int32_t eb_stream_recv(const eb_mixed *m, uint32_t c, uint8_t *b, size_t len)
+{
+    size_t pos = 0;
+    uint64_t seq = 0;
+    int nb_zero = 0;
+    while (len - pos >= 5) {
+        uint8_t *h = b + pos;
+        if (h[0] < 20 || h[0] > 23) return -0x7200;                 /* ssl_check_record_type */
+        if (((h[1] << 8) | h[2]) > 0x0304) return -0x7200;
+        const size_t dlen = ((size_t) h[3] << 8) | h[4];
+        if (dlen == 0) return -0x7200;
+        if (5 + dlen > 5 + 16384 + 256) return -0x7100;
+        if (len - pos < 5 + dlen) break;
+        const int32_t r = eb_record(m->ctx[c], m->cipher[c], m->tls13, 0, m->iv[c], h + 5, dlen, seq);
+        if (r) return r;
+        /* TLS 1.3: eb_record strips the padding (an all-zero inner plaintext is
+         * INVALID_RECORD); no zero-length application data in this workload */
+        nb_zero = 0;
+        if (++seq == 0) return -0x6B80;                              /* COUNTER_WRAPPING */
+        pos += 5 + dlen;
+    }
+    (void) nb_zero;
+    return pos == len ? 0 : -0x7200;
+}
+
+static int32_t eb_stream_send(const eb_mixed *m, uint32_t c, const uint8_t *pt, size_t len, uint8_t *out,
+                              size_t cap, size_t max_frag)
+{
+    size_t off = 0, pos = 0;
+    uint64_t seq = 0;
+    const int tls13 = m->tls13;
+    const int explicit_iv = !tls13 && m->cipher[c] != EB_CHACHA20_POLY1305;
+    while (off < len) {
+        const size_t n = len - off < max_frag ? len - off : max_frag;
+        const size_t inner = tls13 ? n + 1 + (16 - (n + 1) % 16) % 16 : n;
+        const size_t body = (explicit_iv ? 8 : 0) + inner + 16;
+        if (pos + 5 + body > cap) return -0x6A00;                    /* BUFFER_TOO_SMALL */
+        uint8_t *h = out + pos;
+        memcpy(h + 5 + (explicit_iv ? 8 : 0), pt + off, n);
+        const int32_t r = eb_record(m->ctx[c], m->cipher[c], tls13, 1, m->iv[c], h + 5, n, seq);
+        if (r) return r;
+        h[0] = 23;
+        h[1] = 3;
+        h[2] = 3;
+        h[3] = (uint8_t) (body >> 8);
+        h[4] = (uint8_t) body;
+        pos += 5 + body;
+        off += n;
+        seq++;
+    }
+    return 0;
+}
+
+static int32_t eb_dtls_recv(const eb_mixed *m, uint32_t c, uint8_t *b, size_t len, size_t dgram)
+{
+    uint64_t top = 0, window = 0;
+    int any = 0;
+    size_t nd = 0, accepted = 0;
+    for (size_t d = 0; d + dgram <= len; d += dgram, nd++) {
+        uint8_t *h = b + d;
+        if (h[0] < 20 || h[0] > 23 || h[1] != 0xfe || h[2] != 0xfd) continue;   /* dropped datagram */
+        const uint16_t epoch = (uint16_t) (h[3] << 8 | h[4]);
+        uint64_t rs = 0;
+        for (int k = 5; k < 11; k++) rs = rs << 8 | h[k];
+        const size_t dlen = ((size_t) h[11] << 8) | h[12];
+        if (epoch != 1 || 13 + dlen > dgram) continue;
+        /* anti-replay check */
+        if (any && rs + 64 <= top) continue;
+        if (any && rs <= top && (window >> (top - rs)) & 1) continue;
+        const int32_t r = eb_record_v(m->ctx[c], m->cipher[c], 0, 0, m->iv[c], h + 13, dlen,
+                                      (uint64_t) epoch << 48 | rs, 0xfe, 0xfd);
+        if (r == -0x7180) continue;                                   /* bad MAC: dropped (badmac_limit 0) */
+        if (r) return r;
+        /* anti-replay update */
+        if (!any || rs > top) {
+            const uint64_t shift = any ? rs - top : 64;
+            window = shift >= 64 ? 1 : (window << shift) | 1;
+            top = rs;
+            any = 1;
+        } else {
+            window |= (uint64_t) 1 << (top - rs);
+        }
+        accepted++;
+    }
+    /* the bench workload is all-valid: a dropped datagram is an error here */
+    return accepted == nd ? 0 : -0x7200;
+}
+
+static int32_t eb_dtls_send(const eb_mixed *m, uint32_t c, const uint8_t *pt, size_t len, uint8_t *out, size_t cap,
+                            size_t max_frag)
+{
+    size_t off = 0, pos = 0;
+    uint64_t seq = 0;
+    const int explicit_iv = m->cipher[c] != EB_CHACHA20_POLY1305;
+    while (off < len) {
+        const size_t n = len - off < max_frag ? len - off : max_frag;
+        const size_t body = (explicit_iv ? 8 : 0) + n + 16;
+        if (pos + 13 + body > cap) return -0x6A00;
+        uint8_t *h = out + pos;
+        const uint64_t ctr = (uint64_t) 1 << 48 | seq;                /* epoch 1 */
+        memcpy(h + 13 + (explicit_iv ? 8 : 0), pt + off, n);
+        const int32_t r = eb_record_v(m->ctx[c], m->cipher[c], 0, 1, m->iv[c], h + 13, n, ctr, 0xfe, 0xfd);
+        if (r) return r;
+        h[0] = 23;
+        h[1] = 0xfe;
+        h[2] = 0xfd;
+        for (int k = 0; k < 8; k++) h[3 + k] = (uint8_t) (ctr >> (56 - 8 * k));
+        h[11] = (uint8_t) (body >> 8);
+        h[12] = (uint8_t) body;
+        pos += 13 + body;
+        off += n;
+        seq++;
+    }
+    return 0;
+}
+
+static void *eb_rworker(void *arg)
+{
+    eb_rjob *j = (eb_rjob *) arg;
+    const eb_mixed *m = j->m;
+    for (uint32_t c = (uint32_t) j->t; c < m->nconn; c += (uint32_t) m->threads) {
+        uint8_t *in = j->in + (size_t) c * j->in_stride;
+        uint8_t *out = j->out ? j->out + (size_t) c * j->out_stride : NULL;
+        int32_t r;
+        if (j->dir)
+            r = j->dtls ? eb_dtls_send(m, c, in, j->in_len, out, j->out_stride, j->max_frag)
+                        : eb_stream_send(m, c, in, j->in_len, out, j->out_stride, j->max_frag);
+        else
+            r = j->dtls ? eb_dtls_recv(m, c, in, j->in_len, j->max_frag) : eb_stream_recv(m, c, in, j->in_len);
+        j->status[c] = r;
+    }
+    return NULL;
+}
+
+/* dir 1 = send (in: in_len bytes of application data per connection, out:
+ * its records), 0 = receive (in: in_len wire bytes per connection, decrypted
+ * in place; DTLS: max_frag = the wire size of one datagram).  Seconds. */
+double evp_mixed_stream(const eb_mixed *m, int dtls, int dir, uint8_t *in, size_t in_stride, size_t in_len,
+                        uint8_t *out, size_t out_stride, size_t max_frag, int32_t *status)
+{
+    const int threads = m->threads;
+    pthread_t tid[512];
+    eb_rjob jobs[512];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int i = 0; i < threads; i++) {
+        jobs[i] = (eb_rjob) { m, dtls, dir, i, in, in_stride, in_len, out, out_stride, max_frag, status };
+        if (pthread_create(&tid[i], NULL, eb_rworker, &jobs[i]) != 0) {
+            for (int k = 0; k < i; k++) pthread_join(tid[k], NULL);
+            return -1.0;
+        }
+    }
+    for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    return (double) (b.tv_sec - a.tv_sec) + 1e-9 * (double) (b.tv_nsec - a.tv_nsec);
 }

@@ -143,13 +143,24 @@ static int cmp_d(const void *a, const void *b)
  * grid launches */
 void tlsrec__engine_stats(uint64_t *batches, uint64_t *records);
 void tlsrec__server_stats(uint64_t *served, uint64_t *fallback, uint64_t *launches);
+void tlsrec__server_why(uint64_t out[4]);
+uint64_t tlsrec__server_closing(void);
 
 static void print_server_stats(void)
 {
     uint64_t s = 0, f = 0, l = 0;
+    uint64_t why[4] = { 0, 0, 0, 0 };
     tlsrec__server_stats(&s, &f, &l);
-    printf(", \"server_served\": %llu, \"server_fallback\": %llu, \"server_launches\": %llu}\n",
-           (unsigned long long) s, (unsigned long long) f, (unsigned long long) l);
+    tlsrec__server_why(why);
+    /* why: launch-path fallbacks by reason (batch work pending, other set not
+     * drained, withdrawn, no free slot); closing: claims that found a grid
+     * leaving idle */
+    printf(", \"server_served\": %llu, \"server_fallback\": %llu, \"server_launches\": %llu, "
+           "\"server_why\": {\"batch\": %llu, \"drain\": %llu, \"withdrawn\": %llu, \"noslot\": %llu}, "
+           "\"server_closing\": %llu}\n",
+           (unsigned long long) s, (unsigned long long) f, (unsigned long long) l, (unsigned long long) why[0],
+           (unsigned long long) why[1], (unsigned long long) why[2], (unsigned long long) why[3],
+           (unsigned long long) tlsrec__server_closing());
 }
 
 static int latency(char **a)

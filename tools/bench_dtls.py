@@ -26,7 +26,10 @@ def main():
     ap.add_argument("--content", type=int, default=1400)
     ap.add_argument("--cipher", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of each CPU leg's sample")
+    ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
+    from tools import rowlib
     import torch
     import mbedtls_amd as M
     from mbedtls_amd import dtls as D
@@ -76,6 +79,7 @@ def main():
         return (time.perf_counter() - t0) / a.steps
 
     t_enc = timed(lambda: D.encrypt(kt, dout, C, tin, tout, recs, res, n, sres))
+    ms_enc, _ = rowlib.event_timed(lambda: D.encrypt(kt, dout, C, tin, tout, recs, res, n, sres), a.steps)
     so = sres.cpu().numpy().view(S.STREAM_OUT_RES)
     assert (so["status"] == 0).all() and (so["out_len"] == per_out).all()
     import oracle as O
@@ -110,16 +114,33 @@ def main():
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t_dec = float(np.mean(times[1:]))
+    ms_dec, _ = rowlib.event_timed(lambda: D.decrypt(kt, din, C, tdg, n, work, recs, res, disp, n, cres), a.steps,
+                                   prep=lambda: work.copy_(tout))
     ci = cres.cpu().numpy().view(D.DTLS_IN_RES)
     assert (ci["status"] == 0).all() and (ci["naccepted"] == R).all() and (ci["window_top"] == R - 1).all()
     payload = float(C) * per_in
-    for name, t in (("dtls_encrypt", t_enc), ("dtls_decrypt", t_dec)):
+    # SURVEY 8(d)'s rule with the 13-B headers: send reads the application data
+    # and writes the datagrams; receive reads the datagrams and writes each
+    # record's plaintext and a 4-B status
+    alg = {"dtls_encrypt": C * (per_in + per_out), "dtls_decrypt": C * (per_out + R * (L + 4))}
+    rules = {"dtls_encrypt": "application data read + datagrams (13-B headers, explicit nonces, ciphertext, tags) "
+                             "written",
+             "dtls_decrypt": "datagrams (13-B headers, explicit nonces, ciphertext, tags) read + plaintext and a "
+                             "4-B status per record written"}
+    kernels = {"dtls_encrypt": "DTLS frame + tlsrec_gcm_kernel / tlsrec_chachapoly_kernel",
+               "dtls_decrypt": "datagram header walk / anti-replay + AEAD kernel + in-order finish"}
+    for name, t, ms in (("dtls_encrypt", t_enc, ms_enc), ("dtls_decrypt", t_dec, ms_dec)):
+        cpu = None if a.no_cpu else rowlib.cpu_stream_legs(True, a.cipher, L, R,
+                                                           "send" if name == "dtls_encrypt" else "receive",
+                                                           a.cpu_seconds)
         print(json.dumps({"metric": f"DTLS 1.2 {name} throughput (device-resident, datagram framing and "
                                     "anti-replay included)",
                           "value": round(payload / t / 2**30, 3), "unit": "GiB/s",
                           "records_per_s": round(n / t), "ms_per_call": round(t * 1e3, 3),
                           "config": {"connections": C, "datagrams_per_connection": R, "content_bytes": L,
                                      "cipher": a.cipher, "protocol": "DTLS 1.2"},
+                          "roofline": rowlib.roofline(alg[name], ms, rules[name], kernels[name]),
+                          "cpu_baseline": cpu,
                           "check": {"oracle_sample_ok": bool(ok)}}), flush=True)
 
 

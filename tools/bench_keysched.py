@@ -25,7 +25,10 @@ def main():
     ap.add_argument("--cipher", type=int, default=2)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--update", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of the CPU sample")
+    ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
+    from tools import rowlib
     import torch
     import mbedtls_amd as M
     from mbedtls_amd import keysched as K
@@ -45,25 +48,23 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / a.steps
     ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    # CPU restatement on one core for scale (derive of 1024 connections)
     import oracle as O
     alg = O.SHA384 if a.cipher == 2 else O.SHA256
-    H = O.hash_len(alg)
-    raw = prng_array(0x5EC, 1024 * 48).tobytes()
-    c0 = time.perf_counter()
-    for i in range(1024):
-        s = raw[48 * i:48 * i + H]
-        if a.update:
-            s = O.tls13_update_traffic_secret(alg, s)
-        O.tls13_hkdf_expand_label(alg, s, b"key", b"", 32 if a.cipher != 1 else 16)
-        O.tls13_hkdf_expand_label(alg, s, b"iv", b"", 12)
-    cpu = 1024 / (time.perf_counter() - c0)
+    keylen = 16 if a.cipher == 1 else 32
+    cpu = None if a.no_cpu else rowlib.cpu_keysched_leg(alg, keylen, bool(a.update), a.cpu_seconds)
+    # algorithmic bytes per connection: the 48-B secret read (and written back
+    # after a KeyUpdate), the key-table slot written -- its 1 KiB state (round
+    # keys, H, H powers) and the 70 KiB of GHASH tables the GCM kernels read
+    slot = 1024 + (7 * 512 + 26 * 32 + 64) * 16
+    per = 48 * (2 if a.update else 1) + slot
     print(json.dumps({"metric": "TLS 1.3 traffic-key derivations into the key table per second",
                       "value": round(a.count / (ms / 1e3)), "unit": "connections/s", "count": a.count,
                       "cipher": a.cipher, "key_update": a.update, "ms_per_batch_events": round(ms, 4),
                       "ms_per_batch_wall": round(wall * 1e3, 4),
-                      "cpu_baseline": {"value": round(cpu), "unit": "connections/s", "cores": 1, "kind": "port",
-                                       "sample": "1024 connections, oracle/keysched.c via ctypes"}}))
+                      "roofline": rowlib.roofline(per * a.count, ms, "per connection: secret read (and written after "
+                                                  "a KeyUpdate) + the key-table slot written (1 KiB state + 70 KiB "
+                                                  "GHASH tables)", "tls13 derive + key setup"),
+                      "cpu_baseline": cpu}))
 
 
 if __name__ == "__main__":

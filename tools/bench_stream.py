@@ -26,7 +26,10 @@ def main():
     ap.add_argument("--content", type=int, default=16384)
     ap.add_argument("--cipher", type=int, default=2)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall-time target of each CPU leg's sample")
+    ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
+    from tools import rowlib
     import torch
     import mbedtls_amd as M
     from mbedtls_amd import stream as S
@@ -71,6 +74,7 @@ def main():
         return (time.perf_counter() - t0) / a.steps
 
     t_enc = timed(lambda: S.encrypt(kt, dout, C, tin, tout, recs, res, n, sres))
+    ms_enc, _ = rowlib.event_timed(lambda: S.encrypt(kt, dout, C, tin, tout, recs, res, n, sres), a.steps)
     so = sres.cpu().numpy().view(S.STREAM_OUT_RES)
     assert (so["status"] == 0).all() and (so["out_len"] == per_out).all()
     # oracle check of a few connections' record streams
@@ -106,15 +110,33 @@ def main():
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t_dec = float(np.mean(times))
+    ms_dec, _ = rowlib.event_timed(lambda: S.decrypt(kt, din, C, work, recs, res, n, sres), a.steps,
+                                   prep=lambda: work.copy_(tout))
     si = sres.cpu().numpy().view(S.STREAM_IN_RES)
     assert (si["status"] == 0).all()
     payload = float(C) * per_in
-    for name, t in (("stream_encrypt", t_enc), ("stream_decrypt", t_dec)):
+    # SURVEY 8(d)'s rule with the 5-B headers: send reads the application data
+    # and writes the records (headers, ciphertext, tags); receive reads the
+    # records and writes each record's inner plaintext (content + type byte)
+    # and a 4-B status
+    inner = L + 1
+    alg = {"stream_encrypt": C * (per_in + per_out), "stream_decrypt": C * (per_out + R * (inner + 4))}
+    rules = {"stream_encrypt": "application data read + records (5-B headers, ciphertext, tags) written",
+             "stream_decrypt": "records (5-B headers, ciphertext, tags) read + inner plaintext and a 4-B status "
+                               "per record written"}
+    kernels = {"stream_encrypt": "stream frame + tlsrec_gcm_kernel / tlsrec_chachapoly_kernel",
+               "stream_decrypt": "stream header walk / descriptors + AEAD kernel + in-order finish"}
+    for name, t, ms in (("stream_encrypt", t_enc, ms_enc), ("stream_decrypt", t_dec, ms_dec)):
+        cpu = None if a.no_cpu else rowlib.cpu_stream_legs(False, a.cipher, L, R,
+                                                           "send" if name == "stream_encrypt" else "receive",
+                                                           a.cpu_seconds)
         print(json.dumps({"metric": f"TLS record-stream {name} throughput (device-resident, framing included)",
                           "value": round(payload / t / 2**30, 3), "unit": "GiB/s",
                           "records_per_s": round(n / t), "ms_per_call": round(t * 1e3, 3),
                           "config": {"connections": C, "records_per_connection": R, "content_bytes": L,
                                      "cipher": a.cipher, "tls": "1.3"},
+                          "roofline": rowlib.roofline(alg[name], ms, rules[name], kernels[name]),
+                          "cpu_baseline": cpu,
                           "check": {"oracle_sample_ok": bool(ok)}}), flush=True)
 
 

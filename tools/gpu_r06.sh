@@ -20,5 +20,16 @@ base)
   row stream16s 300 python3 tools/bench_stream.py --conns 65536 --recs 16 --content 1400 && cat $O/stream16s.json &&
   row dtls_small 300 python3 tools/bench_dtls.py && cat $O/dtls_small.json
   ;;
-*) echo "usage: tools/gpu_r06.sh base"; exit 2;;
+srv)   # record server: GPU tests, then threads 1/16/32, spin-only (old) vs spin-then-yield (new), ABAB
+  timeout -k 10 300 python -u -m pytest tests/test_server_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/srv_tests.txt 2>&1 \
+      || { echo "server tests failed"; tail -20 $O/srv_tests.txt; exit 1; }
+  tail -1 $O/srv_tests.txt
+  : > $O/threads.jsonl
+  for rep in 1 2; do for spin in -1 2 20; do for t in 16 32; do
+    TLSREC_SERVER_SPIN_US=$spin timeout -k 10 120 ./tests/c/abi_host threads $t 2000 gcm_chacha > $O/t.json || exit 1
+    python3 -c "import json,sys; d=json.loads(open('$O/t.json').read()); d['spin_us']=$spin; d['rep']=$rep; print(json.dumps(d))" >> $O/threads.jsonl
+  done; done; done
+  cat $O/threads.jsonl
+  ;;
+*) echo "usage: tools/gpu_r06.sh base|srv"; exit 2;;
 esac
