@@ -65,7 +65,7 @@ if "pmc_fetch" in out and "pmc_write" in out:
     d["hbm_write_bytes_per_record"] = out["pmc_write"]["hbm_write_bytes"] / records
 if "pmc_rdreq" in out and "hbm_read_bytes_sized" in out["pmc_rdreq"] and "pmc_write" in out:
     # L2->fabric reads by request size (32/64/128 B): the byte count that
-    # tools/probes/fetch_calib pins for every access shape (profiles/r04a)
+    # tools/probes/fetch_calib pins for every access shape (profiles/archive/r04a)
     d["hbm_read_bytes_per_record_sized"] = out["pmc_rdreq"]["hbm_read_bytes_sized"] / records
     d["hbm_bytes_per_record_sized"] = (out["pmc_rdreq"]["hbm_read_bytes_sized"] +
                                        out["pmc_write"]["hbm_write_bytes"]) / records
