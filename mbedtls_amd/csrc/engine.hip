@@ -290,6 +290,14 @@ static int gcm_pair_env(void)
     return e ? atoi(e) : 1;
 }
 
+/* TLSREC_GROUPED=0: the stream / DTLS layers' batches go through the
+ * bucket pass as in r05 (BatchOpt::grouped; A/B and the tests' second path) */
+static bool grouped_env(void)
+{
+    const char *e = getenv("TLSREC_GROUPED");
+    return !(e && atoi(e) == 0);
+}
+
 /* key-ordered descriptor copy for the GCM kernels (bucket scatter):
  * TLSREC_GCM_SRECS=1.  Off by default: same box, k4 665 vs 665-666, c4s 836
  * vs 840-843, c4 1032 vs 1035 GiB/s (profiles/r04h) -- the scattered 40-byte
@@ -648,6 +656,8 @@ struct BatchOpt {
     uint32_t avg_bytes = 0;
     bool prefilled = false;
     bool coalesced = false;
+    bool grouped = false;                /* a key's records are contiguous (the stream / DTLS layers: a connection's
+                                            records in order): no bucket pass, the kernels walk them in place */
     const uint64_t *src_off = nullptr;   /* encrypt: contents at in + src_off[i] (tlsrec__batch_src) */
 };
 
@@ -685,8 +695,15 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
      * pass's permutation, and flags unusable slots in identity order -- the
      * count / scan / scatter kernels cost 5-6 % of a 1 M-record stream or
      * DTLS batch */
-    const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced ||
+    /* (r06) records already grouped by key -- the stream and DTLS layers emit
+     * each connection's records together -- need no bucket pass either: the
+     * GCM passes find a key's run of records where they lie (the bucket
+     * count / scan / scatter kernels were ~90 us of a 1 M-record call);
+     * TLSREC_GROUPED=0 sends them through the bucket pass as before */
+    const bool grouped = opt.grouped && grouped_env();
+    const bool identity = kt->nloaded == 1 || n == 1 || opt.coalesced || grouped ||
                           kt->cipher_mask == (1u << TLSREC_CIPHER_CHACHA20_POLY1305);
+    const bool keyrun = !identity || grouped;     /* the many-keys launch shapes apply */
     if (identity) {
         if (!prefilled && tlsrec__launch_res_guard(res, n, st) != hipSuccess) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else {
@@ -775,9 +792,9 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         const bool small4 = small && !small2 && (uint64_t) n >= (uint64_t) cu * 8 * 16;
         const bool light = rpk < 12 || (avg_bytes != 0 && rpk < 48 && (uint64_t) rpk * avg_bytes < 65536u) ||
                            small2 || small4;
-        if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && light)
+        if (auto_l && !kt->has_cid && keyrun && nr != 12 && wpe != 0 && light)
             L = small2 ? 2 : (small4 ? 4 : ((rpk >= 3 && Lfill <= 16) ? 16 : 64));
-        bool wp = !kt->has_cid && !identity && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
+        bool wp = !kt->has_cid && keyrun && (L == 2 || L == 4 || L == 16 || L == 64) && nr != 12 &&
                   (wpe == 1 || (wpe != 0 && light));
         if (opt.coalesced && n > 1 && auto_l && !kt->has_cid && nr != 12) {
             L = 64;        /* a wave per record, 64 lanes on it: each wave its own record's key, in parallel */
@@ -797,7 +814,7 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         /* (r05: small records up to 255 per key, L by the round-fill model of
          * tlsrec__gcm_pair_small_l) */
         bool pair = false;
-        if (auto_l && !kt->has_cid && !identity && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0) {
+        if (auto_l && !kt->has_cid && keyrun && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0) {
             int Lp = 0;
             const bool small_pair = avg_bytes <= 4096 && rpk >= gcm_pair_small_min() && rpk < gcm_pair_small_max();
             if (small_pair) Lp = (int) tlsrec__gcm_pair_small_l(rpk);
@@ -959,6 +976,7 @@ extern "C" int tlsrec__batch_src(const tlsrec_keytab *kt, const tlsrec_batch_rec
     BatchOpt o;
     o.avg_bytes = avg_bytes;
     o.src_off = src_off;
+    o.grouped = true;                    /* (the stream / DTLS send paths' records, connection by connection) */
     return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, 0, o);
 }
 
@@ -968,6 +986,7 @@ extern "C" int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_r
 {
     BatchOpt o;
     o.avg_bytes = avg_bytes;
+    o.grouped = true;                    /* (the stream / DTLS layers' records, connection by connection) */
     return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, dec, o);
 }
 

@@ -398,26 +398,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void t
  * Atomics are wave-aggregated when the wave's records share one key (a
  * batch already grouped by key costs one atomic per wave).
  * ==================================================================== */
+/* (r06) a slot's counter within its class block: slots of an aligned
+ * 1 024-slot block transposed as 32 x 32, so that the 32 consecutive slots a
+ * wave of round-robin records names fall on 32 different 128-byte lines
+ * (their atomics no longer queue on one line); the tail past the last full
+ * block keeps its order.  A permutation of the block: only the order of the
+ * keys' runs in perm changes, never a record's key. */
+__device__ __forceinline__ uint32_t slot_ctr(uint32_t slot, uint32_t cap)
+{
+    if (slot >= (cap & ~1023u)) return slot;
+    return (slot & ~1023u) | ((slot & 31u) << 5) | ((slot >> 5) & 31u);
+}
+
 __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec_batch_rec &d, uint32_t i)
 {
     if (d.slot >= a.capacity) return 0xffffffffu;
     const int c = a.cipher_of[d.slot];
     constexpr uint32_t S = CP_SPREAD;
+    const uint32_t slot = slot_ctr(d.slot, a.capacity);
     switch (c) {
-        case TLSREC_CIPHER_AES_128_GCM: return d.slot;
-        case TLSREC_CIPHER_AES_256_GCM: return a.capacity + d.slot;
-        case TLSREC_CIPHER_AES_192_GCM: return 2 * a.capacity + d.slot;
-        case TLSREC_CIPHER_CHACHA20_POLY1305: return 4 * a.capacity + ((i >> 6) & (S - 1));   /* the wave's counter */
+        case TLSREC_CIPHER_AES_128_GCM: return slot;
+        case TLSREC_CIPHER_AES_256_GCM: return a.capacity + slot;
+        case TLSREC_CIPHER_AES_192_GCM: return 2 * a.capacity + slot;
+        case TLSREC_CIPHER_CHACHA20_POLY1305:   /* the wave's counter, one per line */
+            return 4 * a.capacity + ((i >> 6) & (CP_COUNTERS - 1)) * CP_STRIDE;
         /* ARIA-GCM classes after the ChaCha counters: 4 cap + S + (0..2) cap + slot */
-        case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + S + d.slot;
-        case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + S + d.slot;
-        case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + S + d.slot;
+        case TLSREC_CIPHER_ARIA_128_GCM: return 4 * a.capacity + S + slot;
+        case TLSREC_CIPHER_ARIA_192_GCM: return 5 * a.capacity + S + slot;
+        case TLSREC_CIPHER_ARIA_256_GCM: return 6 * a.capacity + S + slot;
         /* Camellia-GCM classes after ARIA's: (7, 8, 9) cap + S + slot */
-        case TLSREC_CIPHER_CAMELLIA_128_GCM: return 7 * a.capacity + S + d.slot;
-        case TLSREC_CIPHER_CAMELLIA_192_GCM: return 8 * a.capacity + S + d.slot;
-        case TLSREC_CIPHER_CAMELLIA_256_GCM: return 9 * a.capacity + S + d.slot;
+        case TLSREC_CIPHER_CAMELLIA_128_GCM: return 7 * a.capacity + S + slot;
+        case TLSREC_CIPHER_CAMELLIA_192_GCM: return 8 * a.capacity + S + slot;
+        case TLSREC_CIPHER_CAMELLIA_256_GCM: return 9 * a.capacity + S + slot;
         default:
-            return (tlsrec_cipher_is_ccm(c) || tlsrec_cipher_is_alt_ccm(c)) ? 3 * a.capacity + d.slot : 0xffffffffu;
+            return (tlsrec_cipher_is_ccm(c) || tlsrec_cipher_is_alt_ccm(c)) ? 3 * a.capacity + slot : 0xffffffffu;
     }
 }
 

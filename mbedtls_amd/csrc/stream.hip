@@ -66,12 +66,18 @@ __device__ __forceinline__ uint32_t slot_minor(const SlotState *slots, uint32_t 
     return k.cipher ? k.tls_minor : 0;
 }
 
-/* add v to *sum: a wave-wide sum, one atomic per wave */
+/* add v to the batch's byte count: a wave-wide sum, one atomic per wave, on
+ * one of BYTES_SPREAD counters a 128-byte line apart (by workgroup).  (r06:
+ * on a single counter the atomics of every wave queued on one L2 line -- a
+ * lane-group count kernel of 64 K waves spent 0.8 ms there, the r05 one-lane
+ * kernels ~40 us of their 50.) */
+constexpr int BYTES_SPREAD = 64;
+constexpr int BYTES_STRIDE = 16;       /* u64 words: one 128-byte line per counter */
 __device__ __forceinline__ void wave_add_bytes(unsigned long long *sum, unsigned long long v)
 {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(sum, v);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(sum + (blockIdx.x % BYTES_SPREAD) * BYTES_STRIDE, v);
 }
 
 /* ---------------- receive ---------------------------------------------- */
@@ -159,31 +165,55 @@ __global__ void in_finish_kernel(const tlsrec_stream_in *s, uint32_t n, const ui
     uint32_t nbz = si.nb_zero, nrec = 0, consumed = 0;
     int32_t st = 0;
     const uint32_t first = offs[i], cnt = counts[i];
-    uint32_t k = 0;
-    for (; k < cnt; k++) {
-        const tlsrec_batch_rec &d = recs[first + k];
-        tlsrec_batch_res r = res[first + k];
-        if (d.slot == NO_SLOT) {                  /* TLS 1.3 CCS passes as received */
-            r.status = 0;
-            r.data_offset = 5;
-            r.data_len = d.data_len;
-            r.type = d.type;
-            res[first + k] = r;
-        } else {
-            if (r.status) { st = r.status; break; }
-            if (r.type < 20 || r.type > 23) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; }   /* type re-check :3914-3917 */
-            if (r.data_len == 0) {                /* :3888-3906 */
-                if (minor == 3 && r.type != TLSREC_MSG_APPLICATION_DATA) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; }
-                if (++nbz > 3) { st = TLSREC_ERR_SSL_INVALID_MAC; break; }
-            } else {
-                nbz = 0;
+    /* records in chunks of FK: the chunk's descriptors and results are loaded
+     * before the in-order rules run over them (r06: one record's loads at a
+     * time left the lane waiting on memory once per record) */
+    constexpr uint32_t FK = 4;
+    bool broke = false;
+    for (uint32_t k0 = 0; k0 < cnt && !broke; k0 += FK) {
+        tlsrec_batch_res rr[FK];
+        uint64_t doff[FK];
+        uint32_t dslot[FK], dlen[FK], dblen[FK];
+        uint8_t dtype[FK];
+#pragma unroll
+        for (uint32_t t = 0; t < FK; t++) {
+            if (k0 + t < cnt) {
+                const tlsrec_batch_rec &d = recs[first + k0 + t];
+                rr[t] = res[first + k0 + t];
+                doff[t] = d.buf_off;
+                dslot[t] = d.slot;
+                dlen[t] = d.data_len;
+                dblen[t] = d.buf_len;
+                dtype[t] = d.type;
             }
-            if (++ctr == 0) { st = TLSREC_ERR_SSL_COUNTER_WRAPPING; break; }   /* :3954-3963 */
         }
-        if (r.data_len > 16384) { st = TLSREC_ERR_SSL_INVALID_RECORD; break; } /* IN_CONTENT_LEN, :4011-4014 */
-        nrec++;
-        consumed = (uint32_t) (d.buf_off - si.off) + d.buf_len;
+#pragma unroll
+        for (uint32_t t = 0; t < FK; t++) {
+            if (broke || k0 + t >= cnt) break;
+            tlsrec_batch_res r = rr[t];
+            if (dslot[t] == NO_SLOT) {            /* TLS 1.3 CCS passes as received */
+                r.status = 0;
+                r.data_offset = 5;
+                r.data_len = dlen[t];
+                r.type = dtype[t];
+                res[first + k0 + t] = r;
+            } else {
+                if (r.status) { st = r.status; broke = true; break; }
+                if (r.type < 20 || r.type > 23) { st = TLSREC_ERR_SSL_INVALID_RECORD; broke = true; break; }   /* type re-check :3914-3917 */
+                if (r.data_len == 0) {            /* :3888-3906 */
+                    if (minor == 3 && r.type != TLSREC_MSG_APPLICATION_DATA) { st = TLSREC_ERR_SSL_INVALID_RECORD; broke = true; break; }
+                    if (++nbz > 3) { st = TLSREC_ERR_SSL_INVALID_MAC; broke = true; break; }
+                } else {
+                    nbz = 0;
+                }
+                if (++ctr == 0) { st = TLSREC_ERR_SSL_COUNTER_WRAPPING; broke = true; break; }   /* :3954-3963 */
+            }
+            if (r.data_len > 16384) { st = TLSREC_ERR_SSL_INVALID_RECORD; broke = true; break; } /* IN_CONTENT_LEN, :4011-4014 */
+            nrec++;
+            consumed = (uint32_t) (doff[t] - si.off) + dblen[t];
+        }
     }
+    const uint32_t k = broke ? 0u : cnt;
     if (st == 0 && k == cnt) st = stops[i].status;
     tlsrec_stream_in_res o;
     memset(&o, 0, sizeof(o));
@@ -195,6 +225,141 @@ __global__ void in_finish_kernel(const tlsrec_stream_in *s, uint32_t n, const ui
     o.nb_zero = (uint8_t) nbz;
     o.nparsed = cnt;
     sres[i] = o;
+}
+
+/* ---------------- receive, lane-group framing (r06) ---------------------
+ * in_count_kernel / in_emit_kernel with RG lanes per connection (a group)
+ * instead of one: the header walk of walk_in, speculatively parallel -- from
+ * position p the group's lanes j read the header a run of equal-length
+ * records would put at p + j (5 + dlen0), dlen0 the length of the header at
+ * p; the leading lanes whose headers pass walk_in's checks with that length
+ * are records (each one's predecessor is a record of length dlen0), the
+ * first that does not is where the next round starts.  The same records and
+ * the same stop as the serial walk; a stream of full-size records takes
+ * ceil(records / RG) rounds of two dependent loads, where one lane per
+ * connection took a serial chain of one dependent load per record (1 M
+ * headers of 64 K connections: 16 loads in a row per lane, 4 waves per CU).
+ * (A single-pass form with a decoupled look-back over 16-connection tiles
+ * measured 7 ms for 256 K connections: thread 0's serial look-back over
+ * tiles that had published only their aggregates; not kept) */
+constexpr int RG = 16;                         /* lanes per connection */
+constexpr int RX_THREADS = 256;
+constexpr int RX_CONNS = RX_THREADS / RG;      /* connections per workgroup */
+
+/* the group's 16 bits of a wave ballot (group-uniform control flow) */
+__device__ __forceinline__ uint32_t group_ballot(bool b, int lane)
+{
+    return (uint32_t) (__ballot(b) >> (lane & ~(RG - 1))) & 0xffffu;
+}
+
+struct RxHdr {
+    bool ok;                  /* a record of the run */
+    uint32_t pos, type, dlen;
+    uint8_t v0, v1;
+};
+
+/* the header at q checked as walk_in does, and of length want */
+__device__ __forceinline__ RxHdr rx_header(const uint8_t *base, uint32_t len, uint64_t q, uint32_t want, int32_t *err)
+{
+    RxHdr h = { false, (uint32_t) q, 0, 0, 0, 0 };
+    *err = 0;
+    if (q + 5 > len) return h;                                         /* out of bytes: wait */
+    const uint8_t *p = base + q;
+    h.type = p[0];
+    h.v0 = p[1];
+    h.v1 = p[2];
+    h.dlen = ((uint32_t) p[3] << 8) | p[4];
+    const uint32_t ver = ((uint32_t) h.v0 << 8) | h.v1;
+    if (h.type < 20 || h.type > 23 || ver > (uint32_t) MAX_VERSION || h.dlen == 0)
+        *err = TLSREC_ERR_SSL_INVALID_RECORD;                          /* :3529-3539, :3723-3726 */
+    else if (5 + h.dlen > TLSREC_MAX_IN_RECORD)
+        *err = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    else
+        h.ok = (uint64_t) len - q >= 5 + h.dlen && h.dlen == want;
+    return h;
+}
+
+/* walk_in with the group: f(k, h, ccs_before) on the lane holding record k,
+ * ccs_before = the TLS 1.3 CCS records before it (tls13 only: they take no
+ * sequence number).  Returns the stop and the record count (group-uniform). */
+template <typename F>
+__device__ HdrStop group_walk(const uint8_t *base, uint32_t len, int lane, bool tls13, uint32_t *count, F f)
+{
+    const int q = lane & (RG - 1);
+    uint32_t p = 0, k = 0, nccs = 0;
+    HdrStop st = { 0, 0 };
+    while (len - p >= 5) {
+        const uint32_t dlen0 = ((uint32_t) base[p + 3] << 8) | base[p + 4];
+        const uint64_t at = (uint64_t) p + (uint64_t) q * (5 + dlen0);
+        int32_t err;
+        const RxHdr h = rx_header(base, len, at, dlen0, &err);
+        const uint32_t okm = group_ballot(h.ok, lane);
+        const uint32_t m = (uint32_t) __builtin_ctz(~okm);                 /* leading records */
+        if (m == 0) {                                                      /* the header at p itself */
+            st.status = __shfl(err, lane & ~(RG - 1));
+            break;
+        }
+        const uint32_t ccsm = group_ballot(h.ok && tls13 && h.type == 20, lane) & ((1u << m) - 1u);
+        if ((uint32_t) q < m) f(k + q, h, nccs + (uint32_t) __builtin_popcount(ccsm & ((1u << q) - 1u)));
+        nccs += (uint32_t) __builtin_popcount(ccsm);
+        k += m;
+        p += m * (5 + dlen0);
+    }
+    st.pos = p;
+    *count = k;
+    return st;
+}
+
+__global__ __launch_bounds__(RX_THREADS) void in_count_group_kernel(const tlsrec_stream_in *s, uint32_t n,
+                                                                    const uint8_t *arena, uint32_t *counts,
+                                                                    HdrStop *stops, unsigned long long *bytes)
+{
+    const int tid = threadIdx.x, lane = tid & 63, q = tid & (RG - 1);
+    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
+    unsigned long long b = 0;
+    if (i < n) {
+        const tlsrec_stream_in si = s[i];
+        uint32_t cnt = 0;
+        const HdrStop st = group_walk(arena + si.off, si.len, lane, false, &cnt,
+                                      [&](uint32_t, const RxHdr &h, uint32_t) { b += h.dlen; });
+        if (q == 0) {
+            counts[i] = cnt;
+            stops[i] = st;
+        }
+    } else if (i == n && q == 0) {      /* scan sentinel: offs[n] = total */
+        counts[n] = 0;
+    }
+    wave_add_bytes(bytes, b);
+}
+
+__global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_stream_in *s, uint32_t n,
+                                                                   const uint8_t *arena, const uint32_t *offs,
+                                                                   const SlotState *slots, uint32_t cap,
+                                                                   tlsrec_batch_rec *recs)
+{
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
+    if (i >= n) return;
+    const tlsrec_stream_in si = s[i];
+    const bool tls13 = slot_minor(slots, cap, si.slot) == 4;
+    const uint64_t seq0 = be64(si.in_ctr);
+    tlsrec_batch_rec *out = recs + offs[i];
+    uint32_t cnt;
+    group_walk(arena + si.off, si.len, lane, tls13, &cnt, [&](uint32_t k, const RxHdr &h, uint32_t ccs_before) {
+        tlsrec_batch_rec d;
+        memset(&d, 0, sizeof(d));
+        d.buf_off = si.off + h.pos;                     /* rec->buf = header (:3715-3716) */
+        d.buf_len = 5 + h.dlen;
+        d.data_offset = 5;
+        d.data_len = h.dlen;
+        const bool ccs = tls13 && h.type == 20;         /* TLS 1.3 CCS: not decrypted, no in_ctr step */
+        d.slot = ccs ? NO_SLOT : si.slot;
+        put_be64(d.ctr, seq0 + (k - ccs_before));       /* in_ctr + the records before that took a number */
+        d.type = (uint8_t) h.type;
+        d.ver[0] = h.v0;
+        d.ver[1] = h.v1;
+        out[k] = d;
+    });
 }
 
 /* ---------------- send ------------------------------------------------- */
@@ -589,14 +754,27 @@ __device__ __forceinline__ void dtls_unreach_wipe(uint8_t *arena, const tlsrec_b
     for (uint32_t x = res[kk].data_offset; x < end; x++) b[x] = 0;
 }
 
-__global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
-                                   uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
-                                   const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
-                                   const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
+/* ssl_get_next_record over connection i's datagrams in arrival order, on
+ * the decrypt results (one lane). */
+__device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsrec_dgram *dg, uint32_t ndg,
+                                uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
+                                const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
+                                const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
     const tlsrec_dtls_in ci = c[i];
+    /* (r06) touch what the in-order walk below reads -- the datagram
+     * descriptors and first header bytes, the records' descriptors and
+     * results -- with independent loads first, so the walk's chain of
+     * dependent loads finds them in the cache */
+    if (dtls_conn_ok(ci, ndg, slots, cap)) {
+        uint32_t acc = 0;
+        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++) {
+            const tlsrec_dgram x = dg[d];
+            if (x.len) acc += arena[x.off];
+        }
+        for (uint32_t kk = offs[i]; kk < offs[i] + counts[i]; kk++) acc += recs[kk].slot ^ (uint32_t) res[kk].status;
+        asm volatile("" ::"v"(acc));
+    }
     ReplayWindow w = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
     const bool ignore_cid = (ci.flags & TLSREC_DTLS_IGNORE_UNEXPECTED_CID) != 0;
     uint32_t nbz = ci.nb_zero, bms = ci.badmac_seen, nacc = 0, done = 0, inval = 0;
@@ -677,6 +855,102 @@ __global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tl
     o.badmac_seen = bms;
     o.nb_zero = (uint8_t) nbz;
     cres[i] = o;
+}
+
+__global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
+                                   uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
+                                   const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
+                                   const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dtls_finish_one(i, c, dg, ndg, arena, offs, counts, slots, cap, recs, res, disp, cres);
+}
+
+/* ---- DTLS receive, lane-group framing (r06) -----------------------------
+ * dtls_count / dtls_emit with a group of RG lanes per connection: lane j
+ * walks datagrams j, j + RG, ... of the connection (each datagram's records
+ * are found from its own first byte, so the datagrams walk in parallel), and
+ * a 16-lane scan of the per-datagram record counts places each datagram's
+ * records. */
+__device__ __forceinline__ uint32_t group_incl_scan(uint32_t v, int q)
+{
+#pragma unroll
+    for (int d = 1; d < RG; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d, RG);
+        if (q >= d) v += u;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(RX_THREADS) void dtls_count_group_kernel(const tlsrec_dtls_in *c, uint32_t n,
+                                                                      const tlsrec_dgram *dg, uint32_t ndg,
+                                                                      const uint8_t *arena, const SlotState *slots,
+                                                                      uint32_t cap, uint32_t *counts,
+                                                                      unsigned long long *bytes)
+{
+    const int tid = threadIdx.x, q = tid & (RG - 1);
+    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
+    unsigned long long b = 0;
+    uint32_t cnt = 0;
+    if (i < n) {
+        const tlsrec_dtls_in ci = c[i];
+        if (dtls_conn_ok(ci, ndg, slots, cap))
+            for (uint32_t d = ci.first_dgram + (uint32_t) q; d < ci.first_dgram + ci.ndgram; d += RG)
+                dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &h, const uint8_t *) {
+                    cnt++;
+                    b += h.data_len;
+                });
+    }
+    cnt = group_incl_scan(cnt, q);                       /* the group's total in its last lane */
+    if (i < n && q == RG - 1) counts[i] = cnt;
+    else if (i == n && q == 0) counts[n] = 0;          /* scan sentinel */
+    wave_add_bytes(bytes, b);
+}
+
+/* One descriptor per record.  A record is decrypted when its epoch matches
+ * and the window the connection arrived with does not reject it (as
+ * dtls_emit_kernel). */
+__global__ __launch_bounds__(RX_THREADS) void dtls_emit_group_kernel(const tlsrec_dtls_in *c, uint32_t n,
+                                                                     const tlsrec_dgram *dg, uint32_t ndg,
+                                                                     const uint8_t *arena, const uint32_t *offs,
+                                                                     const SlotState *slots, uint32_t cap,
+                                                                     tlsrec_batch_rec *recs)
+{
+    const int tid = threadIdx.x, q = tid & (RG - 1);
+    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
+    if (i >= n) return;
+    const tlsrec_dtls_in ci = c[i];
+    if (!dtls_conn_ok(ci, ndg, slots, cap)) return;
+    const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
+    uint32_t k0 = offs[i];
+    for (uint32_t base = 0; base < ci.ndgram; base += RG) {
+        const uint32_t d = ci.first_dgram + base + (uint32_t) q;
+        const bool mine = base + (uint32_t) q < ci.ndgram;
+        uint32_t c1 = 0;
+        if (mine) dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &, const uint8_t *) { c1++; });
+        const uint32_t incl = group_incl_scan(c1, q);
+        uint32_t k = k0 + incl - c1;
+        k0 += __shfl(incl, (tid & 63) | (RG - 1));     /* the round's records */
+        if (!mine) continue;
+        const uint64_t dbase = dg[d].off;
+        dtls_walk(arena + dbase, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &h, const uint8_t *p) {
+            tlsrec_batch_rec r;
+            memset(&r, 0, sizeof(r));
+            r.buf_off = dbase + h.pos;                 /* rec->buf = the header (:3715-3716) */
+            r.buf_len = h.data_offset + h.data_len;
+            r.data_offset = h.data_offset;
+            r.data_len = h.data_len;
+            memcpy(r.ctr, p + 3, 8);                   /* explicit epoch + sequence number (:3683-3687) */
+            r.type = p[0];
+            r.ver[0] = p[1];
+            r.ver[1] = p[2];
+            r.cid_len = (uint8_t) h.cid_len;
+            r.cid_off[0] = 11;
+            const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
+            r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
+            recs[k++] = r;
+        });
+    }
 }
 
 /* send: one record per datagram */
@@ -861,28 +1135,40 @@ static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
 {
     sc.scan_bytes = tlsrec__scan_scratch_bytes(n + 1);
     const size_t a = 256, sz4 = (((size_t) n + 1) * 4 + a - 1) / a * a, szs = ((size_t) n * sizeof(HdrStop) + a) / a * a;
-    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + a + sc.scan_bytes + a, &sc.lease);
+    constexpr size_t szb = BYTES_SPREAD * BYTES_STRIDE * 8;     /* the spread byte counters */
+    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + szb + sc.scan_bytes + a, &sc.lease);
     if (lr) return lr;
     uint8_t *m = (uint8_t *) sc.lease.mem;
     sc.counts = (uint32_t *) m;
     sc.offs = (uint32_t *) (m + sz4);
     sc.stops = (HdrStop *) (m + 2 * sz4);
     sc.bytes = (unsigned long long *) (m + 2 * sz4 + szs);
-    sc.scan_tmp = m + 2 * sz4 + szs + a;
-    return hipMemsetAsync(sc.bytes, 0, sizeof(unsigned long long), st) == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    sc.scan_tmp = m + 2 * sz4 + szs + szb;
+    return hipMemsetAsync(sc.bytes, 0, szb, st) == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+}
+
+/* TLSREC_RX_GROUPWALK=0: the r05 receive framing (one lane per connection
+ * in the count and emit kernels), kept for A/B runs and as the tests' second
+ * path */
+static bool groupwalk_env(void)
+{
+    const char *e = getenv("TLSREC_RX_GROUPWALK");
+    return !(e && atoi(e) == 0);
 }
 
 /* exclusive scan of counts[0..n] -> offs; returns offs[n] (the total) on the
  * host, and the mean record size of the batch (0 if unknown) */
 static int scan_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total, uint32_t *avg_bytes = nullptr)
 {
-    unsigned long long bytes = 0;
+    unsigned long long spread[BYTES_SPREAD * BYTES_STRIDE];
     if (tlsrec__exclusive_scan(sc.counts, sc.offs, n + 1, (uint32_t *) sc.scan_tmp, st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&bytes, sc.bytes, sizeof(bytes), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(spread, sc.bytes, sizeof(spread), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    unsigned long long bytes = 0;
+    for (int k = 0; k < BYTES_SPREAD; k++) bytes += spread[k * BYTES_STRIDE];
     if (avg_bytes) *avg_bytes = *total ? (uint32_t) (bytes / *total) : 0u;
     return 0;
 }
@@ -903,17 +1189,26 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
     Scratch sc;
     int r = scratch_alloc(sc, nstreams, st);
     uint32_t total = 0, avg = 0;
+    const bool gw = groupwalk_env();
     if (r == 0) {
-        hipLaunchKernelGGL(in_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
-                           (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
+        if (gw)
+            hipLaunchKernelGGL(in_count_group_kernel, dim3(blocks(nstreams + 1, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                               streams, nstreams, (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
+        else
+            hipLaunchKernelGGL(in_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
+                               (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
         r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
-                           (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        if (gw)
+            hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                               streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        else
+            hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
+                               (const uint8_t *) arena, sc.offs, slots, cap, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }
@@ -1027,17 +1322,26 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     Scratch sc;
     int r = scratch_alloc(sc, nconns, st);
     uint32_t total = 0, avg = 0;
+    const bool gw = groupwalk_env();
     if (r == 0) {
-        hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                           ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
+        if (gw)
+            hipLaunchKernelGGL(dtls_count_group_kernel, dim3(blocks(nconns + 1, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                               conns, nconns, dgrams, ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
+        else
+            hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns,
+                               dgrams, ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
         r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                           ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        if (gw)
+            hipLaunchKernelGGL(dtls_emit_group_kernel, dim3(blocks(nconns, RX_CONNS)), dim3(RX_THREADS), 0, st, conns,
+                               nconns, dgrams, ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        else
+            hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }

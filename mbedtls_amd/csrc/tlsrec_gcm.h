@@ -24,6 +24,14 @@
 #define TLSREC_GCM_LINE_GROUPS 1
 #endif
 
+/* Ablation builds (tools/build_variant.sh, never the product library): what
+ * a per-round piece of the paired small-record passes costs, by leaving it
+ * out -- bit 0 the lane-power multiply (tags wrong), bit 1 the per-key H^L
+ * table build (the previous key's table is used: tags wrong).  0 = off. */
+#ifndef TLSREC_ABLATE
+#define TLSREC_ABLATE 0
+#endif
+
 namespace tlsrec {
 
 /* ======================================================================
@@ -309,7 +317,9 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 pair_sync(pcnt, phase, lane);
                 s = __builtin_amdgcn_readfirstlane(min(pmin[0], pmin[1]));
                 if (s == 0xffffffffu) break;
-                if (a.tm & 16u) {
+                if ((TLSREC_ABLATE & 2) != 0) {
+                    /* ablation: no table build */
+                } else if (a.tm & 16u) {
                     /* built from H^L itself (tm bit 4, r05): one 16-byte read of
                      * the key's powers instead of 8 KiB of table per key pass */
                     gtab4_build_half(const_cast<uint8_t *>(hor), a.ghtab + (size_t) s * KEY_TABLE_WORDS + KEY_HPOW_OFF + (L - 1),
@@ -673,7 +683,10 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                     if (__ballot(lenx && q == 0))
                         if (lenx && q == 0)
                             Y = xor4(gmul<HPI>(hor, Y), make_uint4(0, bswap32(jb.aad_len * 8), 0, bswap32(jb.aead_len * 8)));
-                    Y = group_xor4<L>(gf_mul_v(Y, hq));                  /* GHASH, in every lane of the record */
+                    if constexpr ((TLSREC_ABLATE & 1) != 0)
+                        Y = group_xor4<L>(xor4(Y, hq));                  /* ablation: no multiply */
+                    else
+                        Y = group_xor4<L>(gf_mul_v(Y, hq));              /* GHASH, in every lane of the record */
                 } else if constexpr (WP && L >= 2 && L <= 32) {
                     if (a.tm & (L == 16 ? 1u : 2u)) {
                         const SlotState &ss = a.slots[s];

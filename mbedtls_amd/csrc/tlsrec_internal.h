@@ -36,10 +36,16 @@ constexpr int KEY_TABLE_WORDS = KEY_TABLES * 512 + KEY_G5_WORDS + KEY_HPOW_N;   
 
 constexpr int GCM_WAVES = 16;                       /* default waves per workgroup (one WG per CU) */
 /* The bucket pass counts ChaCha20-Poly1305 records (one class for every key:
- * the kernel takes each record's key itself) on CP_SPREAD counters, a wave's
- * records on counter (wave index mod CP_SPREAD): on one counter, 2 M records
- * round-robin over keys were 65 K same-address atomics, 0.75 ms of a c4s step. */
-constexpr uint32_t CP_SPREAD = 64;
+ * the kernel takes each record's key itself) on CP_COUNTERS counters, a wave's
+ * records on counter (wave index mod CP_COUNTERS): on one counter, 2 M records
+ * round-robin over keys were 65 K same-address atomics, 0.75 ms of a c4s step.
+ * (r06) The counters sit CP_STRIDE entries apart, one per 128-byte line: all
+ * 64 in two lines still serialized the ChaCha half's 65 K atomics on two L2
+ * channels (a c4s count kernel of 328 us); the class block spans CP_SPREAD
+ * entries, the unused ones count nothing. */
+constexpr uint32_t CP_COUNTERS = 64;
+constexpr uint32_t CP_STRIDE = 32;
+constexpr uint32_t CP_SPREAD = CP_COUNTERS * CP_STRIDE;
 constexpr int CP_THREADS = 256;
 constexpr int ARIA_GCM_WAVES = 16;   /* waves per ARIA-GCM workgroup (kernels.hip launch_gcm_aria) */
 constexpr int CP_WAVES = CP_THREADS / 64;

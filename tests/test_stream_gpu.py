@@ -154,6 +154,59 @@ def test_encrypt_then_decrypt_many_connections():
     c.close()
 
 
+@pytest.mark.parametrize("r06", ["1", "0"], ids=["groupwalk", "r05-framing"])
+def test_irregular_record_lengths_match_oracle(r06, monkeypatch):
+    """Streams whose records change length mid-stream (runs of one length,
+    single odd records, CCS records between, 1..40 records, a trailing
+    partial record or a bad header after a run): the lane-group walk (a
+    run of equal lengths checked 16 headers at a time)
+    must frame exactly what the serial walk does -- records, sequence
+    numbers, stop status and position -- under both framing paths."""
+    monkeypatch.setenv("TLSREC_RX_GROUPWALK", r06)      # the r06 lane-group walks and the r05 one-lane walks,
+    monkeypatch.setenv("TLSREC_GROUPED", r06)           # with and without the bucket pass
+    slots = _slots(53)
+    c = Conns(slots)
+    rng = np.random.default_rng(29)
+    conns = []
+    for i in range(120):
+        slot = i % 20
+        t = c.ot[slot]
+        ctr0 = int(rng.integers(0, 1 << 40))
+        ctr, data = ctr0, b""
+        for seg in range(int(rng.integers(1, 6))):
+            if t.tls_version == O.TLS1_3 and rng.random() < 0.2:
+                data += bytes([20, 3, 3, 0, 1, 1])                       # CCS: passes, no counter step
+            frag = int(rng.choice([1, 16, 100, 1400, 4096]))
+            n = int(rng.integers(1, 18)) * frag - int(rng.integers(0, frag))
+            st, w, nrec, c2 = O.stream_encrypt(t, prng_bytes(7000 + 10 * i + seg, max(n, 1)), 23,
+                                               ctr.to_bytes(8, "big"), frag)
+            assert st == 0
+            data += w
+            ctr = int.from_bytes(c2, "big")
+        tail = int(rng.integers(0, 4))
+        if tail == 1:
+            data += data[:3]                                             # partial header
+        elif tail == 2:
+            data += bytes([23, 3, 3, 0, 40]) + bytes(10)                 # partial record
+        elif tail == 3:
+            data += bytes([25, 3, 3, 0, 40]) + bytes(45)                 # bad type
+        conns.append((slot, data, ctr0, 0))
+    a, recs, res, sres, offs = c.decrypt(conns)
+    for i, (slot, data, ctr, nbz) in enumerate(conns):
+        want, wrecs, wbuf = O.stream_decrypt(c.ot[slot], data, ctr.to_bytes(8, "big"), nbz)
+        g = sres[i]
+        assert (int(g["status"]), int(g["nrec"]), int(g["consumed"]), bytes(g["in_ctr"]), int(g["nb_zero"])) == \
+            (want["status"], want["nrec"], want["consumed"], want["in_ctr"], want["nb_zero"]), (i, want)
+        f = int(g["first"])
+        for k, (off, doff, dlen, typ) in enumerate(wrecs):
+            rr = res[f + k]
+            assert (int(rr["data_offset"]), int(rr["data_len"]), int(rr["type"])) == (doff, dlen, typ), (i, k)
+            assert int(recs[f + k]["buf_off"]) == offs[i] + off
+            s0 = offs[i] + off + doff
+            assert a[s0:s0 + dlen].tobytes() == wbuf[off + doff:off + doff + dlen], (i, k)
+    c.close()
+
+
 def _empty_record(t, ctr):
     buf = bytearray(64)
     head = 8 if (t.tls_version == O.TLS1_2 and t.cipher != O.CHACHA20_POLY1305) else 0
