@@ -404,9 +404,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void t
  * (their atomics no longer queue on one line); the tail past the last full
  * block keeps its order.  A permutation of the block: only the order of the
  * keys' runs in perm changes, never a record's key. */
+#ifndef TLSREC_BUCKET_TRANSPOSE
+#define TLSREC_BUCKET_TRANSPOSE 1      /* 0: r05's slot order (A/B builds) */
+#endif
 __device__ __forceinline__ uint32_t slot_ctr(uint32_t slot, uint32_t cap)
 {
-    if (slot >= (cap & ~1023u)) return slot;
+    if (!TLSREC_BUCKET_TRANSPOSE || slot >= (cap & ~1023u)) return slot;
     return (slot & ~1023u) | ((slot & 31u) << 5) | ((slot >> 5) & 31u);
 }
 

@@ -77,15 +77,12 @@
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <pthread.h>
-#include <linux/futex.h>
 #include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/syscall.h>
 #include <time.h>
-#include <unistd.h>
 
 #include "tlsrec.h"
 #include "tlsrec_clmul.h"
@@ -946,33 +943,12 @@ uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr
          g_tr_b1 = 0;
 double g_tick_ns = 10.0;
 uint64_t g_submit_ns = 0, g_life_ticks = 0, g_idle_ticks = 0;
-/* a waiting host thread spins this long before it parks (below;
- * TLSREC_SERVER_SPIN_US, < 0: spin only, the r05 behaviour) */
-int64_t g_spin_ns = 20000;
-/* (r06) Waiting without a CPU: a thread whose request is not back after its
- * spin parks on a futex (its slot's wait word = the sequence number it waits
- * for), and one poller thread -- started with the first parked waiter --
- * watches the parked slots' done words and wakes their threads.  With more
- * calling threads than CPUs the spinners themselves were the contention
- * (r05 / r06: 32 threads on the box's 16 CPUs 133-264 K round trips/s, 16
- * threads 240-420 K).  While fewer threads wait than the process has CPUs,
- * waiters spin for g_spin_ns first (a parked call costs a futex wake);
- * beyond that they park after ~1 us. */
-struct alignas(64) SrvWait {
-    std::atomic<uint32_t> word{0};
-};
-SrvWait g_wait[2][SRV_SLOTS];
-std::atomic<uint32_t> g_parked{0};        /* threads parked */
-std::atomic<uint32_t> g_waiting{0};       /* threads waiting for a reply (spinning or parked) */
-std::atomic<uint32_t> g_poller_word{0};   /* the poller sleeps here while nothing is parked */
-std::atomic<int> g_poller_run{0};         /* 1 running, 2 asked to stop */
-pthread_t g_poller;
-int g_ncpu = 1;
-
-long futex_op(std::atomic<uint32_t> *w, int op, uint32_t v, const timespec *ts)
-{
-    return syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), op, v, ts, nullptr, 0);
-}
+/* a waiting host thread spins; with TLSREC_SERVER_SPIN_US >= 0 it yields its
+ * CPU between polls after that long.  (r06, same box, 16 / 32 calling
+ * threads on the box's 16 CPUs: yielding after 20 us, or parking on a futex
+ * behind a poller thread, served fewer round trips than spinning -- a
+ * parked call waits for its wake-up; spinning is the default) */
+int64_t g_spin_ns = -1;
 /* batch work (tlsrec__server_yield / _note_batch): no grid while any is
  * queued or pending.  Batches may run on several streams at once: each
  * records its own event in a small ring, and the batches between their yield
@@ -1004,36 +980,8 @@ uint64_t now_ns()
     return (uint64_t) t.tv_sec * 1000000000ull + (uint64_t) t.tv_nsec;
 }
 
-void *srv_poller(void *)
-{
-    while (g_poller_run.load(std::memory_order_acquire) == 1) {
-        if (g_parked.load(std::memory_order_acquire) == 0) {
-            const timespec ts = { 0, 2000000 };
-            futex_op(&g_poller_word, FUTEX_WAIT_PRIVATE, 0, &ts);
-            continue;
-        }
-        for (int si = 0; si < 2; si++) {
-            SrvReq *h = g_set[si].h;
-            if (!h) continue;
-            for (int k = 0; k < SRV_SLOTS; k++) {
-                const uint32_t want = g_wait[si][k].word.load(std::memory_order_acquire);
-                if (want && __atomic_load_n(&h[k].done, __ATOMIC_ACQUIRE) == want) {
-                    g_wait[si][k].word.store(0, std::memory_order_release);
-                    futex_op(&g_wait[si][k].word, FUTEX_WAKE_PRIVATE, 1, nullptr);
-                }
-            }
-        }
-        __builtin_ia32_pause();
-    }
-    return nullptr;
-}
-
 void srv_shutdown()
 {
-    if (g_poller_run.exchange(2) == 1) {
-        futex_op(&g_poller_word, FUTEX_WAKE_PRIVATE, 1, nullptr);
-        pthread_join(g_poller, nullptr);
-    }
     pthread_mutex_lock(&g_mu);
     for (auto &S : g_set) {
         if (S.launched) {
@@ -1090,11 +1038,6 @@ int srv_setup_locked()
     g_idle_ticks = (uint64_t) (idle_ms * khz);
     if (const char *y = getenv("TLSREC_SERVER_YIELD")) g_yield = strcmp(y, "0") != 0;
     if (const char *sp = getenv("TLSREC_SERVER_SPIN_US")) g_spin_ns = (int64_t) (atof(sp) * 1e3);
-    {
-        cpu_set_t cs;
-        g_ncpu = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : 1;
-        if (g_ncpu < 1) g_ncpu = 1;
-    }
 #ifdef TLSREC_TEST_HOOKS
     if (const char *d = getenv("TLSREC_TEST_SERVER_POST_DELAY_US")) g_test_post_delay_ns = (uint64_t) (atof(d) * 1e3);
 #endif
@@ -1278,35 +1221,13 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
     __atomic_fetch_add(&S->ctl_h->settled, 1u, __ATOMIC_SEQ_CST);
 
     int rc = 0;
-    const uint64_t t_post = now_ns();
-    const uint32_t waiting = g_waiting.fetch_add(1, std::memory_order_relaxed) + 1;
-    /* spin while the waiters fit the CPUs, else park almost at once */
-    const uint64_t spin_ns = g_spin_ns < 0 ? ~0ull : (waiting < (uint32_t) g_ncpu ? (uint64_t) g_spin_ns : 1000u);
-    SrvWait &w = g_wait[S - g_set][i];
-    bool parked = false;
+    const uint64_t t_post = g_spin_ns >= 0 ? now_ns() : 0;
     for (uint32_t spins = 1;; spins++) {
         if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
-        if (!parked && (spins & 63) == 0 && now_ns() - t_post > spin_ns) {
-            /* park: the poller wakes this thread when done reaches seq */
-            parked = true;
-            w.word.store(seq, std::memory_order_release);
-            g_parked.fetch_add(1, std::memory_order_acq_rel);
-            int expect = 0;
-            if (g_poller_run.load(std::memory_order_acquire) == 0 && g_poller_run.compare_exchange_strong(expect, 1)) {
-                if (pthread_create(&g_poller, nullptr, srv_poller, nullptr) != 0) g_poller_run.store(0);
-            }
-            futex_op(&g_poller_word, FUTEX_WAKE_PRIVATE, 1, nullptr);
-        }
-        if (parked) {
-            if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
-            /* bounded sleeps: the grid-ended check below still runs */
-            const timespec ts = { 0, g_poller_run.load(std::memory_order_relaxed) == 1 ? 200000 : 20000 };
-            futex_op(&w.word, FUTEX_WAIT_PRIVATE, seq, &ts);
-        } else {
-            __builtin_ia32_pause();
-        }
+        __builtin_ia32_pause();
+        if (g_spin_ns >= 0 && (spins & 63) == 0 && now_ns() - t_post > (uint64_t) g_spin_ns) sched_yield();
         hipError_t eq;
-        if ((parked || (spins & 4095) == 0) && (eq = hipEventQuery(S->ev)) != hipErrorNotReady) {
+        if ((spins & 4095) == 0 && (eq = hipEventQuery(S->ev)) != hipErrorNotReady) {
             /* the grid has ended: served just before, or never taken */
             if (g_debug) fprintf(stderr, "tlsrec server: grid ended (%s) before seq %u\n", hipGetErrorString(eq), seq);
             if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
@@ -1316,11 +1237,6 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
             break;
         }
     }
-    if (parked) {
-        w.word.store(0, std::memory_order_release);
-        g_parked.fetch_sub(1, std::memory_order_acq_rel);
-    }
-    g_waiting.fetch_sub(1, std::memory_order_relaxed);
     if (rc == 0) {
         *out = rq->res;
         /* a request the server refused comes back untouched (fail closed) */

@@ -432,17 +432,14 @@ __global__ void __launch_bounds__(256) out_map_kernel(uint32_t n, const uint32_t
  * of a copy and an in-place pass.  With nothing to copy, a record needs one
  * thread, not a wave (LPR = 1: 64 records per wave; as one wave per record
  * this kernel took 0.36-0.43 ms of a 2 ms send of 1 M records). */
+/* record k (= j - offs[i]) of connection i: header, descriptor, and the
+ * content (srcoff: its offset for the AEAD to read in place; else copied
+ * into the record's slot by the LPR lanes) */
 template <int LPR>
-__global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs,
-                                                        uint32_t total, const SlotState *slots, uint32_t cap,
-                                                        const uint8_t *in, uint8_t *out, tlsrec_batch_rec *recs,
-                                                        uint64_t *srcoff)
+__device__ __forceinline__ void out_frame_one(const tlsrec_stream_out &si, uint32_t k, uint32_t j, uint32_t lane,
+                                              const SlotState *slots, uint32_t cap, const uint8_t *in, uint8_t *out,
+                                              tlsrec_batch_rec *recs, uint64_t *srcoff)
 {
-    const uint32_t j = blockIdx.x * (256 / LPR) + threadIdx.x / LPR, lane = threadIdx.x % LPR;
-    if (j >= total) return;
-    const uint32_t i = recs[j].slot;              /* connection of record j (out_map_kernel) */
-    const tlsrec_stream_out si = s[i];
-    const uint32_t k = j - offs[i];
     const uint32_t f = frag_of(si);
     const OutShape sh = out_shape(slots, cap, si.slot);
     const uint64_t src_off = (uint64_t) k * f;
@@ -496,6 +493,18 @@ __global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out 
         d.ver[1] = 3;
         recs[j] = d;
     }
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(256) out_frame_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs,
+                                                        uint32_t total, const SlotState *slots, uint32_t cap,
+                                                        const uint8_t *in, uint8_t *out, tlsrec_batch_rec *recs,
+                                                        uint64_t *srcoff)
+{
+    const uint32_t j = blockIdx.x * (256 / LPR) + threadIdx.x / LPR, lane = threadIdx.x % LPR;
+    if (j >= total) return;
+    const uint32_t i = recs[j].slot;              /* connection of record j (out_map_kernel) */
+    out_frame_one<LPR>(s[i], j - offs[i], j, lane, slots, cap, in, out, recs, srcoff);
 }
 
 __global__ void out_finish_kernel(const tlsrec_stream_out *s, uint32_t n, const uint32_t *offs, const uint32_t *counts,
@@ -762,19 +771,6 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
                                 const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
 {
     const tlsrec_dtls_in ci = c[i];
-    /* (r06) touch what the in-order walk below reads -- the datagram
-     * descriptors and first header bytes, the records' descriptors and
-     * results -- with independent loads first, so the walk's chain of
-     * dependent loads finds them in the cache */
-    if (dtls_conn_ok(ci, ndg, slots, cap)) {
-        uint32_t acc = 0;
-        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++) {
-            const tlsrec_dgram x = dg[d];
-            if (x.len) acc += arena[x.off];
-        }
-        for (uint32_t kk = offs[i]; kk < offs[i] + counts[i]; kk++) acc += recs[kk].slot ^ (uint32_t) res[kk].status;
-        asm volatile("" ::"v"(acc));
-    }
     ReplayWindow w = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
     const bool ignore_cid = (ci.flags & TLSREC_DTLS_IGNORE_UNEXPECTED_CID) != 0;
     uint32_t nbz = ci.nb_zero, bms = ci.badmac_seen, nacc = 0, done = 0, inval = 0;
@@ -866,93 +862,6 @@ __global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tl
     if (i < n) dtls_finish_one(i, c, dg, ndg, arena, offs, counts, slots, cap, recs, res, disp, cres);
 }
 
-/* ---- DTLS receive, lane-group framing (r06) -----------------------------
- * dtls_count / dtls_emit with a group of RG lanes per connection: lane j
- * walks datagrams j, j + RG, ... of the connection (each datagram's records
- * are found from its own first byte, so the datagrams walk in parallel), and
- * a 16-lane scan of the per-datagram record counts places each datagram's
- * records. */
-__device__ __forceinline__ uint32_t group_incl_scan(uint32_t v, int q)
-{
-#pragma unroll
-    for (int d = 1; d < RG; d <<= 1) {
-        const uint32_t u = __shfl_up(v, d, RG);
-        if (q >= d) v += u;
-    }
-    return v;
-}
-
-__global__ __launch_bounds__(RX_THREADS) void dtls_count_group_kernel(const tlsrec_dtls_in *c, uint32_t n,
-                                                                      const tlsrec_dgram *dg, uint32_t ndg,
-                                                                      const uint8_t *arena, const SlotState *slots,
-                                                                      uint32_t cap, uint32_t *counts,
-                                                                      unsigned long long *bytes)
-{
-    const int tid = threadIdx.x, q = tid & (RG - 1);
-    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
-    unsigned long long b = 0;
-    uint32_t cnt = 0;
-    if (i < n) {
-        const tlsrec_dtls_in ci = c[i];
-        if (dtls_conn_ok(ci, ndg, slots, cap))
-            for (uint32_t d = ci.first_dgram + (uint32_t) q; d < ci.first_dgram + ci.ndgram; d += RG)
-                dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &h, const uint8_t *) {
-                    cnt++;
-                    b += h.data_len;
-                });
-    }
-    cnt = group_incl_scan(cnt, q);                       /* the group's total in its last lane */
-    if (i < n && q == RG - 1) counts[i] = cnt;
-    else if (i == n && q == 0) counts[n] = 0;          /* scan sentinel */
-    wave_add_bytes(bytes, b);
-}
-
-/* One descriptor per record.  A record is decrypted when its epoch matches
- * and the window the connection arrived with does not reject it (as
- * dtls_emit_kernel). */
-__global__ __launch_bounds__(RX_THREADS) void dtls_emit_group_kernel(const tlsrec_dtls_in *c, uint32_t n,
-                                                                     const tlsrec_dgram *dg, uint32_t ndg,
-                                                                     const uint8_t *arena, const uint32_t *offs,
-                                                                     const SlotState *slots, uint32_t cap,
-                                                                     tlsrec_batch_rec *recs)
-{
-    const int tid = threadIdx.x, q = tid & (RG - 1);
-    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
-    if (i >= n) return;
-    const tlsrec_dtls_in ci = c[i];
-    if (!dtls_conn_ok(ci, ndg, slots, cap)) return;
-    const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
-    uint32_t k0 = offs[i];
-    for (uint32_t base = 0; base < ci.ndgram; base += RG) {
-        const uint32_t d = ci.first_dgram + base + (uint32_t) q;
-        const bool mine = base + (uint32_t) q < ci.ndgram;
-        uint32_t c1 = 0;
-        if (mine) dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &, const uint8_t *) { c1++; });
-        const uint32_t incl = group_incl_scan(c1, q);
-        uint32_t k = k0 + incl - c1;
-        k0 += __shfl(incl, (tid & 63) | (RG - 1));     /* the round's records */
-        if (!mine) continue;
-        const uint64_t dbase = dg[d].off;
-        dtls_walk(arena + dbase, dgram_len(dg[d]), ci.cid_len, [&](const DtlsHdr &h, const uint8_t *p) {
-            tlsrec_batch_rec r;
-            memset(&r, 0, sizeof(r));
-            r.buf_off = dbase + h.pos;                 /* rec->buf = the header (:3715-3716) */
-            r.buf_len = h.data_offset + h.data_len;
-            r.data_offset = h.data_offset;
-            r.data_len = h.data_len;
-            memcpy(r.ctr, p + 3, 8);                   /* explicit epoch + sequence number (:3683-3687) */
-            r.type = p[0];
-            r.ver[0] = p[1];
-            r.ver[1] = p[2];
-            r.cid_len = (uint8_t) h.cid_len;
-            r.cid_off[0] = 11;
-            const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
-            r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
-            recs[k++] = r;
-        });
-    }
-}
-
 /* send: one record per datagram */
 __device__ __forceinline__ uint32_t dtls_cid_of(const SlotState *slots, uint32_t slot) { return slots[slot].cid_len; }
 
@@ -998,16 +907,10 @@ __device__ __forceinline__ void dtls_seq(uint8_t ctr[8], const uint8_t base[8], 
  * srcoff (nothing to copy), one thread per record (LPR = 1, as
  * out_frame_kernel). */
 template <int LPR>
-__global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream_out *s, uint32_t n,
-                                                             const uint32_t *offs, uint32_t total,
-                                                             const SlotState *slots, uint32_t cap, const uint8_t *in,
-                                                             uint8_t *out, tlsrec_batch_rec *recs, uint64_t *srcoff)
+__device__ __forceinline__ void dtls_out_frame_one(const tlsrec_stream_out &si, uint32_t k, uint32_t j, uint32_t lane,
+                                                   const SlotState *slots, uint32_t cap, const uint8_t *in,
+                                                   uint8_t *out, tlsrec_batch_rec *recs, uint64_t *srcoff)
 {
-    const uint32_t j = blockIdx.x * (256 / LPR) + threadIdx.x / LPR, lane = threadIdx.x % LPR;
-    if (j >= total) return;
-    const uint32_t i = recs[j].slot;              /* connection of record j (out_map_kernel) */
-    const tlsrec_stream_out si = s[i];
-    const uint32_t k = j - offs[i];
     const uint32_t f = frag_of(si);
     const OutShape sh = out_shape(slots, cap, si.slot);
     const uint32_t cid = dtls_cid_of(slots, si.slot), hdr = 13 + cid;
@@ -1061,6 +964,42 @@ __global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream
         d.ver[0] = 0xfe;
         d.ver[1] = 0xfd;
         recs[j] = d;
+    }
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(256) dtls_out_frame_kernel(const tlsrec_stream_out *s, uint32_t n,
+                                                             const uint32_t *offs, uint32_t total,
+                                                             const SlotState *slots, uint32_t cap, const uint8_t *in,
+                                                             uint8_t *out, tlsrec_batch_rec *recs, uint64_t *srcoff)
+{
+    const uint32_t j = blockIdx.x * (256 / LPR) + threadIdx.x / LPR, lane = threadIdx.x % LPR;
+    if (j >= total) return;
+    const uint32_t i = recs[j].slot;              /* connection of record j (out_map_kernel) */
+    dtls_out_frame_one<LPR>(s[i], j - offs[i], j, lane, slots, cap, in, out, recs, srcoff);
+}
+
+/* (r06) The in-place send frame (srcoff) with a group of RG lanes per
+ * connection: lane q frames records q, q + RG, ... of its connection, so no
+ * out_map pass has to tell each record its connection (a 4-byte write into
+ * every descriptor, 17-37 us of a 1 M-record send) and a connection's
+ * descriptor is read once per group, not once per record. */
+template <bool DTLS>
+__global__ void __launch_bounds__(RX_THREADS) out_frame_conn_kernel(const tlsrec_stream_out *s, uint32_t n,
+                                                                    const uint32_t *offs, const uint32_t *counts,
+                                                                    const SlotState *slots, uint32_t cap,
+                                                                    const uint8_t *in, uint8_t *out,
+                                                                    tlsrec_batch_rec *recs, uint64_t *srcoff)
+{
+    const uint32_t i = blockIdx.x * RX_CONNS + threadIdx.x / RG, q = threadIdx.x % RG;
+    if (i >= n) return;
+    const tlsrec_stream_out si = s[i];
+    const uint32_t first = offs[i], c = counts[i];
+    for (uint32_t k = q; k < c; k += RG) {
+        if constexpr (DTLS)
+            dtls_out_frame_one<1>(si, k, first + k, 0, slots, cap, in, out, recs, srcoff);
+        else
+            out_frame_one<1>(si, k, first + k, 0, slots, cap, in, out, recs, srcoff);
     }
 }
 
@@ -1265,8 +1204,6 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs, sc.counts,
-                           recs);
         /* AES-GCM / ChaCha20-Poly1305 tables: the AEAD reads the application
          * data in place (tlsrec__batch_src); other AEADs: copy, then in place */
         uint64_t *srcoff = nullptr;
@@ -1274,12 +1211,15 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
         if (tlsrec__keytab_src_ok(kt) && src_env() &&
             tlsrec__scratch_acquire(st, 3, (size_t) total * sizeof(uint64_t), &sl) == 0)
             srcoff = (uint64_t *) sl.mem;
-        if (srcoff)
-            hipLaunchKernelGGL(out_frame_kernel<1>, dim3(blocks(total, 256)), dim3(256), 0, st, streams, nstreams,
-                               sc.offs, total, slots, cap, in_arena, out_arena, recs, srcoff);
-        else
+        if (srcoff) {
+            hipLaunchKernelGGL(out_frame_conn_kernel<false>, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                               streams, nstreams, sc.offs, sc.counts, slots, cap, in_arena, out_arena, recs, srcoff);
+        } else {
+            hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs,
+                               sc.counts, recs);
             hipLaunchKernelGGL(out_frame_kernel<64>, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams,
                                sc.offs, total, slots, cap, in_arena, out_arena, recs, srcoff);
+        }
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0)
             r = srcoff ? tlsrec__batch_src(kt, recs, res, total, in_arena, out_arena, stream, avg, srcoff)
@@ -1322,26 +1262,17 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     Scratch sc;
     int r = scratch_alloc(sc, nconns, st);
     uint32_t total = 0, avg = 0;
-    const bool gw = groupwalk_env();
     if (r == 0) {
-        if (gw)
-            hipLaunchKernelGGL(dtls_count_group_kernel, dim3(blocks(nconns + 1, RX_CONNS)), dim3(RX_THREADS), 0, st,
-                               conns, nconns, dgrams, ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
-        else
-            hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns,
-                               dgrams, ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
+        hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                           ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
         r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        if (gw)
-            hipLaunchKernelGGL(dtls_emit_group_kernel, dim3(blocks(nconns, RX_CONNS)), dim3(RX_THREADS), 0, st, conns,
-                               nconns, dgrams, ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
-        else
-            hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+        hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                           ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }
@@ -1397,8 +1328,6 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs, sc.counts,
-                           recs);
         /* AES-GCM / ChaCha20-Poly1305 tables: the AEAD reads the application
          * data in place (tlsrec__batch_src); other AEADs: copy, then in place */
         uint64_t *srcoff = nullptr;
@@ -1406,12 +1335,15 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
         if (tlsrec__keytab_src_ok(kt) && src_env() &&
             tlsrec__scratch_acquire(st, 3, (size_t) total * sizeof(uint64_t), &sl) == 0)
             srcoff = (uint64_t *) sl.mem;
-        if (srcoff)
-            hipLaunchKernelGGL(dtls_out_frame_kernel<1>, dim3(blocks(total, 256)), dim3(256), 0, st, streams, nstreams,
-                               sc.offs, total, slots, cap, in_arena, out_arena, recs, srcoff);
-        else
+        if (srcoff) {
+            hipLaunchKernelGGL(out_frame_conn_kernel<true>, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                               streams, nstreams, sc.offs, sc.counts, slots, cap, in_arena, out_arena, recs, srcoff);
+        } else {
+            hipLaunchKernelGGL(out_map_kernel, dim3(blocks(nstreams, 4)), dim3(256), 0, st, nstreams, sc.offs,
+                               sc.counts, recs);
             hipLaunchKernelGGL(dtls_out_frame_kernel<64>, dim3(blocks(total, 4)), dim3(256), 0, st, streams, nstreams,
                                sc.offs, total, slots, cap, in_arena, out_arena, recs, srcoff);
+        }
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0)
             r = srcoff ? tlsrec__batch_src(kt, recs, res, total, in_arena, out_arena, stream, avg, srcoff)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Markdown table of one round's bench rows (the JSON lines tools/gpu_final.sh
+"""Markdown table of one round's bench rows (the JSON lines tools/gpu_r06.sh
 rows writes, copied to profiles/<round>/rows/):
     python profiles/rows_table.py profiles/r05/rows"""
 import glob
@@ -22,7 +22,7 @@ for f in sorted(glob.glob(os.path.join(root, "*.json"))):
             continue
         r = d.get("roofline") or {}
         cpu = d.get("cpu_baseline") or {}
-        legs = {lg.get("leg"): lg.get("value") for lg in cpu.get("legs", [])}
+        legs = {lg.get("leg"): lg.get("value") for lg in cpu.get("legs", [])} or {cpu.get("leg"): cpu.get("value")}
         label = name if len(lines) == 1 else f"{name} ({d['metric'].split(' throughput')[0].split()[-1]})"
         print(f"| {label} | {d['value']} {d.get('unit', '')} | {r.get('frac', '')} | {r.get('kernel_ms_avg', '')} | "
               f"{legs.get('evp', '-')} / {legs.get('port', '-')} | `{f}` |")

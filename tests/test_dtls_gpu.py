@@ -226,10 +226,9 @@ def test_reference_replay_vectors_through_records():
     tab.close()
 
 
-@pytest.mark.parametrize("r06", ["1", "0"], ids=["groupwalk", "r05-framing"])
+@pytest.mark.parametrize("r06", ["1", "0"], ids=["grouped", "bucket-pass"])
 def test_dispositions_match_oracle(r06, monkeypatch):
-    monkeypatch.setenv("TLSREC_RX_GROUPWALK", r06)      # the r06 lane-group walks and the r05 one-lane walks,
-    monkeypatch.setenv("TLSREC_GROUPED", r06)           # with and without the bucket pass
+    monkeypatch.setenv("TLSREC_GROUPED", r06)           # the batch without (r06) and with (r05) the bucket pass
     cid = b"\xaa\xbb\xcc"
     slots = [(M.CIPHER_AES_128_GCM, prng_bytes(3, 16), prng_bytes(4, 16), b""),
              (M.CIPHER_CHACHA20_POLY1305, prng_bytes(5, 32), prng_bytes(6, 16), cid),
@@ -287,15 +286,12 @@ def test_dispositions_match_oracle(r06, monkeypatch):
     tab.close()
 
 
-@pytest.mark.parametrize("r06", ["1", "0"], ids=["groupwalk", "r05-framing"])
+@pytest.mark.parametrize("r06", ["1", "0"], ids=["grouped", "bucket-pass"])
 def test_many_datagrams_per_connection(r06, monkeypatch):
-    """More datagrams per connection than the receive walks' lane group (16,
-    stream.hip RG): 37 and 50 datagrams of one to three records, a bad MAC
+    """Many datagrams per connection: 37 and 50 datagrams of one to three records, a bad MAC
     and a replay among them, and a connection with none -- record order and
-    dispositions against the oracle, under the lane-group walks and the r05
-    passes"""
-    monkeypatch.setenv("TLSREC_RX_GROUPWALK", r06)      # the r06 lane-group walks and the r05 one-lane walks,
-    monkeypatch.setenv("TLSREC_GROUPED", r06)           # with and without the bucket pass
+    dispositions against the oracle, with and without the bucket pass"""
+    monkeypatch.setenv("TLSREC_GROUPED", r06)           # the batch without (r06) and with (r05) the bucket pass
     slots = [(M.CIPHER_AES_128_GCM, prng_bytes(13, 16), prng_bytes(14, 16), b""),
              (M.CIPHER_CHACHA20_POLY1305, prng_bytes(15, 32), prng_bytes(16, 16), b"")]
     tab = Table(slots)

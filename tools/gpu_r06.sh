@@ -20,6 +20,11 @@ base)
   row stream16s 300 python3 tools/bench_stream.py --conns 65536 --recs 16 --content 1400 && cat $O/stream16s.json &&
   row dtls_small 300 python3 tools/bench_dtls.py && cat $O/dtls_small.json
   ;;
+tests)   # the stream / DTLS / server GPU tests
+  timeout -k 10 500 python -u -m pytest tests/test_stream_gpu.py tests/test_dtls_gpu.py tests/test_server_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/sds_tests.txt 2>&1 \
+      || { echo "tests failed"; tail -30 $O/sds_tests.txt; exit 1; }
+  tail -1 $O/sds_tests.txt
+  ;;
 srv)   # record server: GPU tests, then threads 1/16/32, spin-only (old) vs spin-then-yield (new), ABAB
   timeout -k 10 300 python -u -m pytest tests/test_server_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/srv_tests.txt 2>&1 \
       || { echo "server tests failed"; tail -20 $O/srv_tests.txt; exit 1; }
@@ -65,7 +70,7 @@ rowab)   # same-box A/B of libraries on the stream / DTLS rows: LIBS (env, space
   : > $O/rowab.jsonl
   for rep in 1 2; do for lib in $LIBS; do
     tag=$(basename $lib .so)
-    for row in "stream16s tools/bench_stream.py --conns 65536 --recs 16 --content 1400" "dtls_small tools/bench_dtls.py"; do
+    for row in "stream16s tools/bench_stream.py --conns 65536 --recs 16 --content 1400" "dtls_small tools/bench_dtls.py" "stream_cp tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3" "dtls_cp tools/bench_dtls.py --cipher 3"; do
       set -- $row; name=$1; shift
       TLSREC_LIBRARY=$R/$lib timeout -k 10 200 python3 "$@" --no-cpu > $O/t.json 2> $O/t.err || { echo "FAIL $name $tag"; tail -3 $O/t.err; exit 1; }
       python3 -c "import json; [print(json.dumps(dict(json.loads(l), lib='$tag', rep=$rep, row='$name'))) for l in open('$O/t.json')]" >> $O/rowab.jsonl
@@ -95,5 +100,41 @@ for l in open('$O/rxab.jsonl'):
   cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_rx_stream -o run --output-format csv -- python3 $R/tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3 --no-cpu --steps 3 > $R/$O/prof_rx_stream.json 2>&1 && \
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_rx_dtls -o run --output-format csv -- python3 $R/tools/bench_dtls.py --no-cpu --steps 3 > $R/$O/prof_rx_dtls.json 2>&1 && cd $R
   ;;
-*) echo "usage: tools/gpu_r06.sh base|srv|frame|libab|rowab|rxab"; exit 2;;
+rows)   # the round's one full sweep on the final build: -m gpu suite, smoke, every bench row
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.txt 2>&1 \
+      || { echo "gpu tests failed"; tail -20 $O/gpu_tests.txt; exit 1; }
+  tail -1 $O/gpu_tests.txt
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.txt; exit 1; }
+  tail -1 $O/smoke.txt
+  row c2 400 python3 bench.py && summ c2 &&
+  for c in c3 c4 c4s k4 c1 c2s c3d chacha16k gcm192 ccm ccm8 aria256 camellia128; do
+    row $c 400 python3 bench.py --config $c --no-e2e && summ $c || exit 1
+  done &&
+  row count_gpus 60 python3 -c "import bench, json; print(json.dumps({'count_gpus': bench.count_gpus()}))" && cat $O/count_gpus.json &&
+  row dist1 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --dist && summ dist1 &&
+  row stream16 300 python3 tools/bench_stream.py --conns 65536 --recs 16 &&
+  row stream4 300 python3 tools/bench_stream.py --conns 65536 --recs 4 &&
+  row stream16s 300 python3 tools/bench_stream.py --conns 65536 --recs 16 --content 1400 &&
+  row stream_cp 300 python3 tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3 &&
+  row dtls_small 300 python3 tools/bench_dtls.py &&
+  row dtls_cp 300 python3 tools/bench_dtls.py --cipher 3 &&
+  row dtls16k 300 python3 tools/bench_dtls.py --content 16384 --recs 4 --cipher 2 &&
+  row keysched 300 python3 tools/bench_keysched.py &&
+  make -s -C tests/c abi_host &&
+  : > $O/latency.jsonl &&
+  for a in "2 1.3 16383" "2 1.3 1400" "3 1.3 1400" "1 1.2 1400" "2 1.3 100"; do
+    timeout -k 10 120 ./tests/c/abi_host latency $a 2000 >> $O/latency.jsonl || exit 1
+  done && for t in 1 16 32; do timeout -k 10 120 ./tests/c/abi_host threads $t 2000 gcm_chacha >> $O/latency.jsonl || exit 1; done &&
+  python3 profiles/rows_table.py $O
+  ;;
+prof)   # rocprofv3 kernel stats + PMC passes on the final build
+  export PROFILE_RDREQ=1
+  PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2 > $O/prof_c2.log 2>&1 || { echo "c2 failed"; tail -5 $O/prof_c2.log; exit 1; }
+  PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2s --config c2s > $O/prof_c2s.log 2>&1 || { echo "c2s failed"; tail -5 $O/prof_c2s.log; exit 1; }
+  PMC_RECORDS=4194304 profiles/run_profile.sh ${T}_c4s --config c4s > $O/prof_c4s.log 2>&1 || { echo "c4s failed"; tail -5 $O/prof_c4s.log; exit 1; }
+  profiles/run_profile.sh ${T}_dtls_small --cmd tools/bench_dtls.py --steps 3 --no-cpu > $O/prof_dtls.log 2>&1 || { echo "dtls failed"; tail -5 $O/prof_dtls.log; exit 1; }
+  profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 --no-cpu > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
+  echo prof done
+  ;;
+*) echo "usage: tools/gpu_r06.sh base|srv|frame|libab|rowab|rxab|tests|rows|prof"; exit 2;;
 esac
