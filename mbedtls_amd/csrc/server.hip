@@ -943,12 +943,20 @@ uint64_t g_tr_n = 0, g_tr_sum[3] = { 0, 0, 0 }, g_tr_aes = 0, g_tr_mul = 0, g_tr
          g_tr_b1 = 0;
 double g_tick_ns = 10.0;
 uint64_t g_submit_ns = 0, g_life_ticks = 0, g_idle_ticks = 0;
-/* a waiting host thread spins; with TLSREC_SERVER_SPIN_US >= 0 it yields its
- * CPU between polls after that long.  (r06, same box, 16 / 32 calling
- * threads on the box's 16 CPUs: yielding after 20 us, or parking on a futex
- * behind a poller thread, served fewer round trips than spinning -- a
- * parked call waits for its wake-up; spinning is the default) */
-int64_t g_spin_ns = -1;
+/* A waiting host thread spins while the waiting threads fit the process's
+ * CPUs and yields its CPU between polls once they do not (r06): with 32
+ * calling threads on the box's 16 CPUs pure spinning kept descheduled
+ * threads -- whose requests were done, or not yet posted -- off the CPUs
+ * for milliseconds, and 7-9 of 128 K calls went to the launch path (a set
+ * switch waiting on an unanswered slot, a grid ending before a late post);
+ * yielding had none.  At 16 threads spinning stays ahead (same box, 3 reps,
+ * profiles/r06/ab/threads_*.jsonl).  TLSREC_SERVER_SPIN_US: < 0 spin
+ * always, >= 0 yield after that long always.  Parking on a futex behind a
+ * poller thread measured slower than both (a parked call waits for its
+ * wake-up). */
+int64_t g_spin_ns = -2;                   /* -2: adaptive (above) */
+std::atomic<uint32_t> g_waiting{0};
+uint32_t g_ncpu = 1;
 /* batch work (tlsrec__server_yield / _note_batch): no grid while any is
  * queued or pending.  Batches may run on several streams at once: each
  * records its own event in a small ring, and the batches between their yield
@@ -1038,6 +1046,22 @@ int srv_setup_locked()
     g_idle_ticks = (uint64_t) (idle_ms * khz);
     if (const char *y = getenv("TLSREC_SERVER_YIELD")) g_yield = strcmp(y, "0") != 0;
     if (const char *sp = getenv("TLSREC_SERVER_SPIN_US")) g_spin_ns = (int64_t) (atof(sp) * 1e3);
+    {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        const int nc = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : 1;
+        g_ncpu = nc > 0 ? (uint32_t) nc : 1u;
+        /* a cgroup CPU quota caps it (a container sees every CPU of the host) */
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = { 0 };
+            unsigned long long per = 0;
+            if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+                const unsigned long long c = (strtoull(q, nullptr, 10) + per - 1) / per;
+                if (c > 0 && c < g_ncpu) g_ncpu = (uint32_t) c;
+            }
+            fclose(f);
+        }
+    }
 #ifdef TLSREC_TEST_HOOKS
     if (const char *d = getenv("TLSREC_TEST_SERVER_POST_DELAY_US")) g_test_post_delay_ns = (uint64_t) (atof(d) * 1e3);
 #endif
@@ -1222,10 +1246,15 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
 
     int rc = 0;
     const uint64_t t_post = g_spin_ns >= 0 ? now_ns() : 0;
+    g_waiting.fetch_add(1, std::memory_order_relaxed);
     for (uint32_t spins = 1;; spins++) {
         if (__atomic_load_n(&rq->done, __ATOMIC_ACQUIRE) == seq) break;
         __builtin_ia32_pause();
-        if (g_spin_ns >= 0 && (spins & 63) == 0 && now_ns() - t_post > (uint64_t) g_spin_ns) sched_yield();
+        if ((spins & 63) == 0) {
+            const bool yield = g_spin_ns == -2 ? g_waiting.load(std::memory_order_relaxed) > g_ncpu
+                                               : (g_spin_ns >= 0 && now_ns() - t_post > (uint64_t) g_spin_ns);
+            if (yield) sched_yield();
+        }
         hipError_t eq;
         if ((spins & 4095) == 0 && (eq = hipEventQuery(S->ev)) != hipErrorNotReady) {
             /* the grid has ended: served just before, or never taken */
@@ -1237,6 +1266,7 @@ extern "C" int tlsrec__server_run(int dec, uint32_t cipher, uint32_t nr, const t
             break;
         }
     }
+    g_waiting.fetch_sub(1, std::memory_order_relaxed);
     if (rc == 0) {
         *out = rq->res;
         /* a request the server refused comes back untouched (fail closed) */

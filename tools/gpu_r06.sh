@@ -30,7 +30,7 @@ srv)   # record server: GPU tests, then threads 1/16/32, spin-only (old) vs spin
       || { echo "server tests failed"; tail -20 $O/srv_tests.txt; exit 1; }
   tail -1 $O/srv_tests.txt
   : > $O/threads.jsonl
-  for rep in 1 2 3; do for spin in -1 20; do for t in 16 32; do
+  for rep in 1 2 3; do for spin in ${SPINS:--1 20}; do for t in 16 32; do
     TLSREC_SERVER_SPIN_US=$spin timeout -k 10 120 ./tests/c/abi_host threads $t 2000 gcm_chacha > $O/t.json || exit 1
     python3 -c "import json,sys; d=json.loads(open('$O/t.json').read()); d['spin_us']=$spin; d['rep']=$rep; print(json.dumps(d))" >> $O/threads.jsonl
   done; done; done
