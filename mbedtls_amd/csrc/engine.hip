@@ -814,7 +814,10 @@ static int batch(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_b
         /* (r05: small records up to 255 per key, L by the round-fill model of
          * tlsrec__gcm_pair_small_l) */
         bool pair = false;
-        if (auto_l && !kt->has_cid && keyrun && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0) {
+        /* (r06) the paired kernels hold lane powers only (tlsrec_gcm.h): a
+         * coalesced call or a TREEMUL mode without bit 3 takes the 8-wave passes */
+        if (auto_l && !kt->has_cid && keyrun && nr != 12 && wpe != 0 && gcm_pair_env() && avg_bytes != 0 &&
+            !opt.coalesced && (gcm_tm(true, true) & 8u)) {
             int Lp = 0;
             const bool small_pair = avg_bytes <= 4096 && rpk >= gcm_pair_small_min() && rpk < gcm_pair_small_max();
             if (small_pair) Lp = (int) tlsrec__gcm_pair_small_l(rpk);

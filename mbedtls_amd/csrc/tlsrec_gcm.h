@@ -167,13 +167,14 @@ __device__ __noinline__ uint4 gcm_cid_aad_fold(const uint8_t *gp, uint4 a0, cons
 /* Out of line (r05): inlined, its ~600 instructions shifted the register
  * allocation and schedule of the record loop around it (a faster multiply
  * cost k4 1.2 % through a 5-instruction longer step loop, same box). */
-__device__ __noinline__ uint4 gf_mul_v(uint4 x, uint4 p)
+__device__ __forceinline__ uint4 gf_mul_i(uint4 x, uint4 p)
 {
     const uint32_t a[4] = { x.x, x.y, x.z, x.w }, b[4] = { p.x, p.y, p.z, p.w };
     uint32_t r[4];
     tlsrec_gf128_mul(a, b, r);
     return make_uint4(r[0], r[1], r[2], r[3]);
 }
+__device__ __noinline__ uint4 gf_mul_v(uint4 x, uint4 p) { return gf_mul_i(x, p); }
 
 template <int SH>
 __device__ __forceinline__ uint4 gtree_v(const uint4 (&P)[5], uint4 Y, int lane, int q)
@@ -457,7 +458,12 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                  * kernels it cost c2 5 % with the flag off (the hot loop carries
                  * the LEN position test and its registers; same box, r04p/q:
                  * 737 -> 700 GiB/s), and on it was no faster (r04e) */
-                const bool lp = WP && !CID && (a.tm & 8u);
+                /* the paired passes are compiled for lane powers only (r06): with
+                 * the fold and the two final multiplies by H as a value in them too,
+                 * their out-of-line calls cost 28 spilled VGPRs whose stores ran in
+                 * every round (engine.hip picks the 8-wave passes for the other
+                 * TREEMUL modes) */
+                const bool lp = PAIR || (WP && !CID && (a.tm & 8u));
                 const bool lenx = lp && m % BL == 0;
                 const uint32_t z = lp ? 0u : (BL - mm % BL) % BL;           /* front padding: position of C_1 */
                 const uint32_t J = jb.run ? (lp ? (lenx ? m / BL : (m + BL) / BL) : (mm + z) / BL) : 0;
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                     if constexpr ((TLSREC_ABLATE & 1) != 0)
                         Y = group_xor4<L>(xor4(Y, hq));                  /* ablation: no multiply */
                     else
-                        Y = group_xor4<L>(gf_mul_v(Y, hq));              /* GHASH, in every lane of the record */
+                        Y = group_xor4<L>(PAIR ? gf_mul_i(Y, hq) : gf_mul_v(Y, hq));   /* GHASH, in every lane of the record */
                 } else if constexpr (WP && L >= 2 && L <= 32) {
                     if (a.tm & (L == 16 ? 1u : 2u)) {
                         const SlotState &ss = a.slots[s];

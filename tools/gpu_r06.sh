@@ -25,6 +25,11 @@ tests)   # the stream / DTLS / server GPU tests
       || { echo "tests failed"; tail -30 $O/sds_tests.txt; exit 1; }
   tail -1 $O/sds_tests.txt
   ;;
+suite)   # the whole -m gpu suite
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.txt 2>&1 \
+      || { echo "gpu tests failed"; tail -30 $O/gpu_tests.txt; exit 1; }
+  tail -1 $O/gpu_tests.txt
+  ;;
 srv)   # record server: GPU tests, then threads 1/16/32, spin-only (old) vs spin-then-yield (new), ABAB
   timeout -k 10 300 python -u -m pytest tests/test_server_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/srv_tests.txt 2>&1 \
       || { echo "server tests failed"; tail -20 $O/srv_tests.txt; exit 1; }
@@ -136,5 +141,5 @@ prof)   # rocprofv3 kernel stats + PMC passes on the final build
   profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 --no-cpu > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
   echo prof done
   ;;
-*) echo "usage: tools/gpu_r06.sh base|srv|frame|libab|rowab|rxab|tests|rows|prof"; exit 2;;
+*) echo "usage: tools/gpu_r06.sh base|suite|srv|frame|libab|rowab|rxab|tests|rows|prof"; exit 2;;
 esac
