@@ -398,27 +398,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void t
  * Atomics are wave-aggregated when the wave's records share one key (a
  * batch already grouped by key costs one atomic per wave).
  * ==================================================================== */
-/* (r06) a slot's counter within its class block: slots of an aligned
- * 1 024-slot block transposed as 32 x 32, so that the 32 consecutive slots a
- * wave of round-robin records names fall on 32 different 128-byte lines
- * (their atomics no longer queue on one line); the tail past the last full
- * block keeps its order.  A permutation of the block: only the order of the
- * keys' runs in perm changes, never a record's key. */
-#ifndef TLSREC_BUCKET_TRANSPOSE
-#define TLSREC_BUCKET_TRANSPOSE 1      /* 0: r05's slot order (A/B builds) */
-#endif
-__device__ __forceinline__ uint32_t slot_ctr(uint32_t slot, uint32_t cap)
-{
-    if (!TLSREC_BUCKET_TRANSPOSE || slot >= (cap & ~1023u)) return slot;
-    return (slot & ~1023u) | ((slot & 31u) << 5) | ((slot >> 5) & 31u);
-}
-
+/* (r06: the per-slot counters transposed 32 x 32 within aligned 1 024-slot
+ * blocks, so that a wave's 32 consecutive slots fall on 32 lines, measured
+ * neutral on c4s -- 881 / 881 GiB/s same box, profiles/r06/ab -- and left) */
 __device__ __forceinline__ uint32_t bucket_key(const BucketArgs &a, const tlsrec_batch_rec &d, uint32_t i)
 {
     if (d.slot >= a.capacity) return 0xffffffffu;
     const int c = a.cipher_of[d.slot];
     constexpr uint32_t S = CP_SPREAD;
-    const uint32_t slot = slot_ctr(d.slot, a.capacity);
+    const uint32_t slot = d.slot;
     switch (c) {
         case TLSREC_CIPHER_AES_128_GCM: return slot;
         case TLSREC_CIPHER_AES_256_GCM: return a.capacity + slot;
