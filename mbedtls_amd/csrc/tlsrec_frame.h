@@ -229,7 +229,11 @@ TLSREC_HD void tlsrec_plan_encrypt(tlsrec_plan *p, const tlsrec_plan_key *k,
     }
     if (k->tls13 || cid) {
         uint32_t g = granularity ? granularity : 16;
-        uint64_t pad = (g - (data_len + 1) % g) % g;                   /* :431-435 */
+        /* data_len <= 16384 here: 32-bit, and a mask for a power-of-two
+         * granularity (the 64-bit remainder cost the GCM encrypt kernels
+         * registers in every round) */
+        const uint32_t dl1 = (uint32_t) data_len + 1;
+        const uint64_t pad = (g & (g - 1)) == 0 ? (0u - dl1) & (g - 1) : (g - dl1 % g) % g;   /* :431-435 */
         if (post_avail == 0) {                                         /* :473-475 */
             p->status = TLSREC_E_BUFFER_TOO_SMALL;
             return;

@@ -38,7 +38,7 @@ if "--ceiling" in args:
     del args[k:k + 2]
 root, kern, records = args[0], args[1], int(args[2])
 out = {}
-for p in ("pmc_sq1", "pmc_sq2", "pmc_sq3", "pmc_fetch", "pmc_write", "pmc_rdreq"):
+for p in ("pmc_sq1", "pmc_sq2", "pmc_sq3", "pmc_fetch", "pmc_write", "pmc_rdreq", "pmc_tcp", "pmc_tcc"):
     if os.path.isdir(os.path.join(root, p)):
         out[p] = summarize(os.path.join(root, p), kern)
 sq1, sq2 = out["pmc_sq1"], out["pmc_sq2"]
@@ -69,6 +69,22 @@ if "pmc_rdreq" in out and "hbm_read_bytes_sized" in out["pmc_rdreq"] and "pmc_wr
     d["hbm_read_bytes_per_record_sized"] = out["pmc_rdreq"]["hbm_read_bytes_sized"] / records
     d["hbm_bytes_per_record_sized"] = (out["pmc_rdreq"]["hbm_read_bytes_sized"] +
                                        out["pmc_write"]["hbm_write_bytes"]) / records
+if "pmc_tcp" in out:
+    # vector L1 (TCP): accesses, the reads it sends to L2, and its address
+    # translation (UTCL1) hits / misses
+    t = out["pmc_tcp"]
+    acc = t.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0)
+    d["tcp_accesses_per_record"] = acc / records
+    d["tcp_l2_reads_per_record"] = t.get("TCP_TCC_READ_REQ_sum", 0.0) / records
+    tr = t.get("TCP_UTCL1_TRANSLATION_HIT_sum", 0.0) + t.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0)
+    d["utcl1_miss_frac"] = t.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0) / max(1.0, tr)
+    d["utcl1_misses_per_record"] = t.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0) / records
+if "pmc_tcc" in out:
+    t = out["pmc_tcc"]
+    h, m = t.get("TCC_HIT_sum", 0.0), t.get("TCC_MISS_sum", 0.0)
+    d["l2_hit_frac"] = h / max(1.0, h + m)
+    d["l2_requests_per_record"] = (h + m) / records
+    d["l2_dram_reads_per_record"] = t.get("TCC_EA0_RDREQ_DRAM_sum", 0.0) / records
 out["derived"] = d
 print(json.dumps(out, indent=1))
 if ceil_path:

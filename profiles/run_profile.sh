@@ -4,7 +4,8 @@
 #   profiles/run_profile.sh <tag> --cmd <python script> [args...]   (any workload, e.g. tools/bench_dtls.py)
 # 1) rocprofv3 --kernel-trace --stats on the workload
 # 2) separate --pmc passes (SQ instruction mix / LDS, FETCH_SIZE, WRITE_SIZE,
-#    and the L2->fabric read requests by size, TCC_EA0_RDREQ_{32B,64B,128B})
+#    and the L2->fabric read requests by size, TCC_EA0_RDREQ_{32B,64B,128B};
+#    PROFILE_CACHE=1 adds vector-L1 / UTCL1 and L2 hit passes)
 #    on a PMC_RECORDS-record run of the same bench config (default 262144;
 #    multi-key configs pass their full record count so the launch path is the
 #    same), or on the same --cmd workload.
@@ -39,5 +40,9 @@ pass pmc_fetch FETCH_SIZE
 pass pmc_write WRITE_SIZE
 if [ "${PROFILE_RDREQ:-1}" = 1 ]; then
   pass pmc_rdreq TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum
+fi
+if [ "${PROFILE_CACHE:-0}" = 1 ]; then
+  pass pmc_tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum
+  pass pmc_tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum
 fi
 echo "profile done: $OUT"

@@ -141,5 +141,12 @@ prof)   # rocprofv3 kernel stats + PMC passes on the final build
   profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 --no-cpu > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
   echo prof done
   ;;
-*) echo "usage: tools/gpu_r06.sh base|suite|srv|frame|libab|rowab|rxab|tests|rows|prof"; exit 2;;
+profsmall)   # the paired-pass rows only: c4s, DTLS and stream 16 x 1.4 KiB (+ cache / UTCL1 passes)
+  export PROFILE_RDREQ=1 PROFILE_CACHE=1
+  PMC_RECORDS=4194304 profiles/run_profile.sh ${T}_c4s --config c4s > $O/prof_c4s.log 2>&1 || { echo "c4s failed"; tail -5 $O/prof_c4s.log; exit 1; }
+  profiles/run_profile.sh ${T}_dtls_small --cmd tools/bench_dtls.py --steps 3 --no-cpu > $O/prof_dtls.log 2>&1 || { echo "dtls failed"; tail -5 $O/prof_dtls.log; exit 1; }
+  profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 --no-cpu > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
+  echo profsmall done
+  ;;
+*) echo "usage: tools/gpu_r06.sh base|suite|srv|profsmall|frame|libab|rowab|rxab|tests|rows|prof"; exit 2;;
 esac
