@@ -93,15 +93,28 @@ typedef const __attribute__((address_space(4))) uint32_t kconst_u32;
  * in every step. */
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4 glob_u32x4;
+/* TLSREC_NT_DATA (A/B builds): bit 0 loads, bit 1 stores of record payload
+ * with the non-temporal hint */
+#ifndef TLSREC_NT_DATA
+#define TLSREC_NT_DATA 0
+#endif
 __device__ __forceinline__ uint4 gload16(const uint8_t *p)
 {
+#if TLSREC_NT_DATA & 1
+    const u32x4 v = __builtin_nontemporal_load((const glob_u32x4 *) (uintptr_t) p);
+#else
     const u32x4 v = *(const glob_u32x4 *) (uintptr_t) p;
+#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void gstore16(uint8_t *p, uint4 v)
 {
     u32x4 w = { v.x, v.y, v.z, v.w };
+#if TLSREC_NT_DATA & 2
+    __builtin_nontemporal_store(w, (glob_u32x4 *) (uintptr_t) p);
+#else
     *(glob_u32x4 *) (uintptr_t) p = w;
+#endif
 }
 
 #define TLSREC_PSEL(k) (0x0C0C0000u | ((4u + (k)) << 8))

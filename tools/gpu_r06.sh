@@ -71,6 +71,27 @@ libab)   # same-box A/B of two libraries on bench.py configs: LIBA LIBB CONFIGS 
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], d['value'], d['roofline']['kernel_ms_avg'], d['check']['bad_records'])" $O/t.json $c $tag | tee -a $O/libab.txt
   done; done
   ;;
+multiab)   # same-box A/B of several libraries (LIBS) on bench configs (CONFIGS) and rows (ROWS: stream16s dtls_small stream_cp dtls_cp), alternating, REPS reps
+  : > $O/multiab.jsonl
+  for rep in $(seq ${REPS:-2}); do for lib in $LIBS; do
+    tag=$(basename $lib .so)
+    for c in $CONFIGS; do
+      TLSREC_LIBRARY=$R/$lib timeout -k 10 300 python3 bench.py --config $c --no-cpu --no-e2e --verify 16 > $O/t.json 2> $O/t.err || { echo "FAIL $c $tag"; tail -3 $O/t.err; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(json.dumps(dict(row=sys.argv[2], lib=sys.argv[3], rep=$rep, value=d['value'], kernel_ms=d['roofline']['kernel_ms_avg'], bad=d['check']['bad_records'])))" $O/t.json $c $tag >> $O/multiab.jsonl
+    done
+    for name in $ROWS; do
+      case $name in
+        stream16s) set -- tools/bench_stream.py --conns 65536 --recs 16 --content 1400;;
+        stream_cp) set -- tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3;;
+        dtls_small) set -- tools/bench_dtls.py;;
+        dtls_cp) set -- tools/bench_dtls.py --cipher 3;;
+      esac
+      TLSREC_LIBRARY=$R/$lib timeout -k 10 200 python3 "$@" --no-cpu > $O/t.json 2> $O/t.err || { echo "FAIL $name $tag"; tail -3 $O/t.err; exit 1; }
+      python3 -c "import json; [print(json.dumps(dict(row='$name'+('_enc' if 'encrypt' in d['metric'] else '_dec'), lib='$tag', rep=$rep, value=d['value'], kernel_ms=(d.get('roofline') or {}).get('kernel_ms_avg'), check=d.get('check')))) for d in map(json.loads, open('$O/t.json'))]" >> $O/multiab.jsonl
+    done
+  done; done
+  python3 tools/ab_summary.py $O/multiab.jsonl
+  ;;
 rowab)   # same-box A/B of libraries on the stream / DTLS rows: LIBS (env, space separated)
   : > $O/rowab.jsonl
   for rep in 1 2; do for lib in $LIBS; do
