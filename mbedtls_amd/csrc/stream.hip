@@ -58,6 +58,16 @@ __device__ __forceinline__ void put_be64(uint8_t c[8], uint64_t v)
     }
 }
 
+/* 16 bytes at any byte address through the global address space (gfx950
+ * runs unaligned-access mode; generic pointers would load through flat) */
+typedef unsigned int st_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) st_u32x4 st_glob_u32x4;
+__device__ __forceinline__ uint4 load16(const uint8_t *p)
+{
+    const st_u32x4 v = *(const st_glob_u32x4 *) (uintptr_t) p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 /* TLS minor version of a loaded slot (3 or 4), 0 if the slot is unusable */
 __device__ __forceinline__ uint32_t slot_minor(const SlotState *slots, uint32_t cap, uint32_t slot)
 {
@@ -362,6 +372,177 @@ __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_
     });
 }
 
+/* ---------------- receive, one framing pass (r06, second form) ----------
+ * count -> scan -> emit as one kernel: a workgroup takes the next tile of
+ * connections (an atomic tile counter, so every tile it waits on is already
+ * running), counts their records, publishes the tile's aggregate, finds its
+ * exclusive prefix by a decoupled look-back, publishes the inclusive prefix
+ * and walks its connections' headers again -- now L2-hot -- to write the
+ * descriptors.  The look-back runs on a whole wave: lane j reads the status
+ * of the tile j + 1 places back, so one round covers 64 predecessors; a tile
+ * adds the aggregates up to the nearest inclusive prefix.  (The first single-
+ * pass form, r06, looked back with one thread, one predecessor at a time, and
+ * measured 7 ms: DESIGN §10.)  Tile status word: bits 62-63 the flag, bits
+ * 0-31 the value. */
+constexpr uint64_t TS_AGG = 1ull << 62, TS_INC = 2ull << 62;
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+/* workgroup-wide (every thread calls it, NT threads): publish the tile's
+ * aggregate agg, return the sum of every earlier tile's records (the tile's
+ * exclusive prefix).  Thread j reads the status of the tile j + 1 places back,
+ * so one round covers NT predecessors: with all tiles of a generation done
+ * counting at about the same time, the front of inclusive prefixes moves NT
+ * tiles per round trip (64 per round, one wave, measured 234 us for 16 K
+ * tiles of a 1 M-record stream batch). */
+template <int NT>
+__device__ uint32_t tile_lookback(unsigned long long *status, uint32_t tile, uint32_t agg)
+{
+    __shared__ uint32_t sh_fp[NT / 64], sh_sum[NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0)
+        __hip_atomic_store(status + tile, (tile == 0 ? TS_INC : TS_AGG) | agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (tile == 0) return 0;
+    uint32_t excl = 0;
+    int64_t base = (int64_t) tile - 1;
+    for (;;) {
+        const int64_t t = base - tid;
+        const unsigned long long v = t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : TS_INC;   /* before tile 0: an inclusive prefix of 0 */
+        const uint32_t flag = (uint32_t) (v >> 62);
+        const uint64_t pm = __ballot(flag == 2);
+        if (lane == 0) sh_fp[wave] = pm ? (uint32_t) (wave * 64) + (uint32_t) __builtin_ctzll(pm) : (uint32_t) NT;
+        __syncthreads();
+        uint32_t fp = sh_fp[0];                          /* nearest inclusive prefix */
+#pragma unroll
+        for (int w = 1; w < NT / 64; w++) fp = min(fp, sh_fp[w]);
+        if (__syncthreads_or(flag == 0 && (uint32_t) tid <= fp)) {   /* a predecessor still counting */
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const uint32_t ws = wave_sum_u32((uint32_t) tid <= fp ? (uint32_t) v : 0u);
+        if (lane == 0) sh_sum[wave] = ws;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < NT / 64; w++) excl += sh_sum[w];
+        __syncthreads();                                 /* sh_fp / sh_sum reused next round */
+        if (fp < (uint32_t) NT) break;
+        base -= NT;
+    }
+    if (tid == 0)
+        __hip_atomic_store(status + tile, TS_INC | (uint32_t) (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+/* the workgroup's tile id (first thread claims it) */
+__device__ __forceinline__ uint32_t claim_tile(uint32_t *ctr, uint32_t *sh)
+{
+    if (threadIdx.x == 0) *sh = atomicAdd(ctr, 1u);
+    __syncthreads();
+    return *sh;
+}
+
+/* Stream receive framing in one pass: RG lanes per connection as
+ * in_count_group_kernel / in_emit_group_kernel; a tile is RX_CH chunks of
+ * RX_CONNS connections (chunk c's group g takes connection c RX_CONNS + g of
+ * the tile), so 1 M records of 4-record streams make 2 K tiles, not 16 K.
+ * Writes counts, stops, offs (offs[n] = the batch's record count) and the
+ * descriptors (at most max_records of them). */
+#ifndef TLSREC_RX_CH
+#define TLSREC_RX_CH 8
+#endif
+constexpr int RX_CH = TLSREC_RX_CH;
+constexpr int RX_TILE = RX_CH * RX_CONNS;
+__global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_stream_in *s, uint32_t n,
+                                                              const uint8_t *arena, const SlotState *slots,
+                                                              uint32_t cap, uint32_t *counts, uint32_t *offs,
+                                                              HdrStop *stops, unsigned long long *bytes,
+                                                              unsigned long long *tstat, uint32_t *tctr,
+                                                              tlsrec_batch_rec *recs, uint32_t max_records)
+{
+    __shared__ uint32_t sh_tile, sh_cnt[RX_TILE], sh_off[RX_TILE];
+    const int tid = threadIdx.x, lane = tid & 63, q = tid & (RG - 1), g = tid / RG;
+    const uint32_t tile = claim_tile(tctr, &sh_tile);
+    const uint32_t i0 = tile * RX_TILE;
+    unsigned long long b = 0;
+    for (int c = 0; c < RX_CH; c++) {
+        const uint32_t i = i0 + (uint32_t) (c * RX_CONNS + g);
+        uint32_t cnt = 0;
+        if (i < n) {
+            const tlsrec_stream_in si = s[i];
+            const HdrStop st = group_walk(arena + si.off, si.len, lane, false, &cnt,
+                                          [&](uint32_t, const RxHdr &h, uint32_t) { b += h.dlen; });
+            if (q == 0) {
+                counts[i] = cnt;
+                stops[i] = st;
+            }
+        }
+        if (q == 0) sh_cnt[c * RX_CONNS + g] = cnt;
+    }
+    wave_add_bytes(bytes, b);
+    __syncthreads();
+    /* the tile's exclusive scan over its RX_TILE connections (threads < RX_TILE, RX_TW waves) */
+    constexpr int RX_TW = (RX_TILE + 63) / 64;
+    uint32_t incl = 0, agg = 0;
+    if (tid < RX_TW * 64) {
+        incl = tid < RX_TILE ? sh_cnt[tid] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+    }
+    __syncthreads();                                      /* sh_cnt read: sh_off may take the wave totals */
+    if (tid < RX_TW * 64 && lane == 63) sh_off[tid >> 6] = incl;   /* wave totals (sh_off reused below) */
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < RX_TW; w++) agg += sh_off[w];
+    uint32_t wpre = 0;
+    for (int w = 0; w < (tid >> 6) && w < RX_TW; w++) wpre += sh_off[w];
+    const uint32_t excl = tile_lookback<RX_THREADS>(tstat, tile, agg);
+    __syncthreads();                                      /* every thread has read the wave totals */
+    if (tid < RX_TILE) sh_off[tid] = excl + wpre + incl - sh_cnt[tid];
+    __syncthreads();
+    if (tid < RX_TILE) {
+        const uint32_t i = i0 + (uint32_t) tid;
+        if (i < n) offs[i] = sh_off[tid];
+        if (i + 1 == n) offs[n] = sh_off[tid] + sh_cnt[tid];     /* the scan's sentinel: the batch total */
+    }
+    if (!recs) return;
+    for (int c = 0; c < RX_CH; c++) {
+        const uint32_t i = i0 + (uint32_t) (c * RX_CONNS + g);
+        const uint32_t cnt = sh_cnt[c * RX_CONNS + g], off = sh_off[c * RX_CONNS + g];
+        if (i >= n || !cnt) continue;                     /* group-uniform */
+        const tlsrec_stream_in si = s[i];
+        const bool tls13 = slot_minor(slots, cap, si.slot) == 4;
+        const uint64_t seq0 = be64(si.in_ctr);
+        tlsrec_batch_rec *out = recs + off;
+        uint32_t c2;
+        group_walk(arena + si.off, si.len, lane, tls13, &c2, [&](uint32_t k, const RxHdr &h, uint32_t ccs_before) {
+            if (off + k >= max_records) return;
+            tlsrec_batch_rec d;
+            memset(&d, 0, sizeof(d));
+            d.buf_off = si.off + h.pos;                     /* rec->buf = header (:3715-3716) */
+            d.buf_len = 5 + h.dlen;
+            d.data_offset = 5;
+            d.data_len = h.dlen;
+            const bool ccs = tls13 && h.type == 20;         /* TLS 1.3 CCS: not decrypted, no in_ctr step */
+            d.slot = ccs ? NO_SLOT : si.slot;
+            put_be64(d.ctr, seq0 + (k - ccs_before));
+            d.type = (uint8_t) h.type;
+            d.ver[0] = h.v0;
+            d.ver[1] = h.v1;
+            out[k] = d;
+        });
+    }
+}
+
 /* ---------------- send ------------------------------------------------- */
 struct OutShape {
     uint32_t ok;              /* slot usable */
@@ -619,7 +800,7 @@ __device__ __forceinline__ uint32_t dgram_len(const tlsrec_dgram &d)
  * <= TLS 1.2, data_len != 0, the datagram holds the record); f(h, header) per
  * record. */
 template <typename F>
-__device__ int32_t dtls_walk(const uint8_t *b, uint32_t len, uint32_t cid_conf, F f)
+__device__ __forceinline__ int32_t dtls_walk(const uint8_t *b, uint32_t len, uint32_t cid_conf, F f)
 {
     if (len == 0) return DG_EOF;
     uint32_t pos = 0;
@@ -647,6 +828,70 @@ __device__ int32_t dtls_walk(const uint8_t *b, uint32_t len, uint32_t cid_conf, 
     return DG_END;
 }
 
+/* dtls_walk with the datagram's first 16 bytes already loaded (have16):
+ * a datagram that is exactly one plain record -- the common case -- is
+ * decided from registers, f gets a pointer to the loaded bytes; anything
+ * else (several records, a CID header, an error) walks from memory as
+ * dtls_walk does, f not having been called yet.  Same records, same stop. */
+template <typename F>
+__device__ __forceinline__ int32_t dtls_walk_pre(const uint8_t *b, uint32_t len, uint4 h16, bool have16,
+                                                 uint32_t cid_conf, F f)
+{
+    if (have16) {
+        uint8_t h[16];
+        __builtin_memcpy(h, &h16, 16);
+        const uint32_t type = h[0], dlen = ((uint32_t) h[11] << 8) | h[12];
+        if (!(cid_conf != 0 && type == TLSREC_MSG_CID) && type >= 20 && type <= 23 &&
+            read_version_dtls(h[1], h[2]) <= 0x0303u && dlen != 0 && len == 13 + dlen) {
+            const DtlsHdr d = { 0, 13, dlen, 0 };
+            f(d, (const uint8_t *) h);
+            return DG_END;
+        }
+    }
+    return dtls_walk(b, len, cid_conf, f);
+}
+
+/* A connection's datagrams d0 .. d1 - 1 in arrival order, U at a time: their
+ * descriptors, then their first 16 bytes, are loaded before any is walked, so
+ * one lane's walk waits on memory once per U datagrams rather than twice per
+ * datagram (r06: with 16 datagrams per connection, one lane each, the count /
+ * emit / finish kernels were chains of 32 dependent loads).  fr(off, hdr, p)
+ * per record, fd(stop) per datagram. */
+template <int U, typename FR, typename FD, typename FC>
+__device__ __forceinline__ void dtls_conn_walk(uint32_t d0, uint32_t d1, const tlsrec_dgram *dg, const uint8_t *arena,
+                                               uint32_t cid_conf, FR fr, FD fd, FC fc)
+{
+    for (uint32_t d = d0; d < d1; d += U) {
+        fc();                                   /* the caller's own loads for the next U datagrams */
+        uint64_t off[U];
+        uint32_t len[U];
+        uint4 h[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            off[u] = 0;
+            len[u] = 0;
+            if (d + u < d1) {
+                const tlsrec_dgram g = dg[d + u];
+                off[u] = g.off;
+                len[u] = dgram_len(g);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = len[u] >= 16 ? load16(arena + off[u]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (d + u >= d1) break;
+            const uint64_t o = off[u];
+            fd(dtls_walk_pre(arena + o, len[u], h[u], len[u] >= 16, cid_conf,
+                             [&](const DtlsHdr &hd, const uint8_t *p) { fr(o, hd, p); }));
+        }
+    }
+}
+#ifndef TLSREC_DG_U
+#define TLSREC_DG_U 4
+#endif
+constexpr int DG_U = TLSREC_DG_U;
+
 /* the anti-replay window (mbedtls_ssl_dtls_replay_check / _update, ssl_msg.c:3248-3306) */
 struct ReplayWindow {
     uint64_t top, bits;
@@ -659,17 +904,17 @@ struct ReplayWindow {
         for (int k = 2; k < 8; k++) v = (v << 8) | ctr[k];
         return v;
     }
-    __device__ __forceinline__ bool fresh(const uint8_t *ctr) const
+    __device__ __forceinline__ bool fresh(const uint8_t *ctr) const { return fresh_s(seq48(ctr)); }
+    __device__ __forceinline__ void update(const uint8_t *ctr) { update_s(seq48(ctr)); }
+    __device__ __forceinline__ bool fresh_s(uint64_t s) const
     {
-        const uint64_t s = seq48(ctr);
         if (!on || s > top) return true;
         const uint64_t bit = top - s;
         return bit < 64 && !((bits >> bit) & 1);
     }
-    __device__ __forceinline__ void update(const uint8_t *ctr)
+    __device__ __forceinline__ void update_s(uint64_t s)
     {
         if (!on) return;
-        const uint64_t s = seq48(ctr);
         if (s > top) {
             const uint64_t shift = s - top;
             bits = shift >= 64 ? 1 : ((bits << shift) | 1);
@@ -745,6 +990,82 @@ __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsr
     }
 }
 
+/* dtls_count_kernel + scan + dtls_emit_kernel in one pass (in_frame_kernel's
+ * tile look-back), one lane per connection, DG_THREADS connections per tile,
+ * datagrams walked DG_U at a time; the emit walk reads the headers the count
+ * walk has just brought into L2.  Descriptors beyond max_records are not
+ * written. */
+constexpr int DG_THREADS = 256;
+__global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtls_in *c, uint32_t n,
+                                                                const tlsrec_dgram *dg, uint32_t ndg,
+                                                                const uint8_t *arena, const SlotState *slots,
+                                                                uint32_t cap, uint32_t *counts, uint32_t *offs,
+                                                                unsigned long long *bytes, unsigned long long *tstat,
+                                                                uint32_t *tctr, tlsrec_batch_rec *recs,
+                                                                uint32_t max_records)
+{
+    __shared__ uint32_t sh_tile, sh_wsum[DG_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tile = claim_tile(tctr, &sh_tile);
+    const uint32_t i = tile * DG_THREADS + (uint32_t) tid;
+    unsigned long long b = 0;
+    uint32_t cnt = 0;
+    tlsrec_dtls_in ci;
+    bool ok = false;
+    if (i < n) {
+        ci = c[i];
+        ok = dtls_conn_ok(ci, ndg, slots, cap);
+        if (ok)
+            dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
+                                 [&](uint64_t, const DtlsHdr &h, const uint8_t *) {
+                                     cnt++;
+                                     b += h.data_len;
+                                 },
+                                 [](int32_t) {}, [] {});
+        counts[i] = cnt;
+    }
+    wave_add_bytes(bytes, b);
+    /* the tile's exclusive scan: within waves by shuffles, across waves in LDS */
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) sh_wsum[wave] = incl;
+    __syncthreads();
+    const uint32_t excl = tile_lookback<DG_THREADS>(tstat, tile, sh_wsum[0] + sh_wsum[1] + sh_wsum[2] + sh_wsum[3]);
+    uint32_t off = excl + incl - cnt;
+    for (int w = 0; w < wave; w++) off += sh_wsum[w];
+    if (i < n) offs[i] = off;
+    if (i + 1 == n) offs[n] = off + cnt;                  /* the scan's sentinel: the batch total */
+    if (!ok || !cnt || !recs) return;
+    const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
+    uint32_t k = off;
+    dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
+                         [&](uint64_t base, const DtlsHdr &h, const uint8_t *p) {
+                             if (k < max_records) {
+                                 tlsrec_batch_rec r;
+                                 memset(&r, 0, sizeof(r));
+                                 r.buf_off = base + h.pos;                  /* rec->buf = the header (:3715-3716) */
+                                 r.buf_len = h.data_offset + h.data_len;
+                                 r.data_offset = h.data_offset;
+                                 r.data_len = h.data_len;
+                                 memcpy(r.ctr, p + 3, 8);                   /* explicit epoch + sequence number (:3683-3687) */
+                                 r.type = p[0];
+                                 r.ver[0] = p[1];
+                                 r.ver[1] = p[2];
+                                 r.cid_len = (uint8_t) h.cid_len;
+                                 r.cid_off[0] = 11;                         /* the CID follows the sequence number */
+                                 const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
+                                 r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
+                                 recs[k] = r;
+                             }
+                             k++;
+                         },
+                         [](int32_t) {}, [] {});
+}
+
 /* ssl_get_next_record over each connection's datagrams in arrival order, on
  * the decrypt results (one lane per connection). */
 /* A record the speculative pass decrypted but the in-order pass does not
@@ -764,7 +1085,10 @@ __device__ __forceinline__ void dtls_unreach_wipe(uint8_t *arena, const tlsrec_b
 }
 
 /* ssl_get_next_record over connection i's datagrams in arrival order, on
- * the decrypt results (one lane). */
+ * the decrypt results (one lane).  PRE: the datagrams DG_U at a time
+ * (dtls_conn_walk), the records' results and descriptor slots loaded with
+ * them. */
+template <bool PRE>
 __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsrec_dgram *dg, uint32_t ndg,
                                 uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
                                 const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
@@ -774,69 +1098,122 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
     ReplayWindow w = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
     const bool ignore_cid = (ci.flags & TLSREC_DTLS_IGNORE_UNEXPECTED_CID) != 0;
     uint32_t nbz = ci.nb_zero, bms = ci.badmac_seen, nacc = 0, done = 0, inval = 0;
-    const uint32_t first = offs[i];
+    const uint32_t first = offs[i], nrec = counts[i];
     uint32_t k = first;
     int32_t st = 0;
+    bool dropped = false;
+    /* PRE: the next DG_U records' results and slots (record kb + u) */
+    uint32_t kb = 0;
+    tlsrec_batch_res pr[DG_U];
+    uint32_t ps[DG_U];
+    auto prefetch = [&]() __attribute__((always_inline)) {
+        kb = k;
+#pragma unroll
+        for (int u = 0; u < DG_U; u++) {
+            if (k + u < first + nrec) {
+                pr[u] = res[k + u];
+                ps[u] = recs[k + u].slot;
+            }
+        }
+    };
+    auto onrec = [&](uint32_t epoch, uint64_t seq) __attribute__((always_inline)) {
+        const uint32_t kk = k++;
+        /* PRE: records come in order, so the prefetched ones leave from the
+         * head of a register queue -- shifted for every record, never indexed
+         * (an indexed array would live in scratch memory) */
+        bool have = false;
+        uint32_t qslot = 0;
+        tlsrec_batch_res qr;
+        if constexpr (PRE) {
+            if (kk - kb < (uint32_t) DG_U) {
+                have = true;
+                qslot = ps[0];
+                qr = pr[0];
+#pragma unroll
+                for (int u = 0; u + 1 < DG_U; u++) {
+                    ps[u] = ps[u + 1];
+                    pr[u] = pr[u + 1];
+                }
+            }
+        }
+        if (st) { disp[kk] = TLSREC_DTLS_NOT_REACHED; dtls_unreach_wipe(arena, recs, res, slots, kk); return; }
+        if (dropped) { disp[kk] = TLSREC_DTLS_DROPPED; dtls_unreach_wipe(arena, recs, res, slots, kk); return; }
+        if (epoch != ci.in_epoch) {            /* :3755-3768, skipped after the handshake (:4727-4800) */
+            disp[kk] = epoch == (uint32_t) ci.in_epoch + 1 ? TLSREC_ERR_SSL_EARLY_MESSAGE
+                                                           : TLSREC_ERR_SSL_UNEXPECTED_RECORD;
+            return;
+        }
+        if (!w.fresh_s(seq)) {                 /* :3769-3776 */
+            disp[kk] = TLSREC_ERR_SSL_UNEXPECTED_RECORD;
+            dtls_unreach_wipe(arena, recs, res, slots, kk);
+            return;
+        }
+        uint32_t rslot;
+        tlsrec_batch_res r;
+        if constexpr (PRE) {
+            if (have) {
+                rslot = qslot;
+                r = qr;
+            } else {                            /* a datagram of several records ran past the prefetch */
+                rslot = recs[kk].slot;
+                r = res[kk];
+            }
+        } else {
+            rslot = recs[kk].slot;
+            r = res[kk];
+        }
+        if (rslot == NO_SLOT) {                /* not decrypted: impossible, the window only grows */
+            st = TLSREC_ERR_SSL_INTERNAL_ERROR;
+            disp[kk] = st;
+            return;
+        }
+        int32_t e = r.status;                  /* ssl_prepare_record_content (:3810-4017) */
+        if (e == TLSREC_ERR_SSL_UNEXPECTED_CID && ignore_cid) { disp[kk] = e; return; }   /* :3872-3879 */
+        if (e == 0) {
+            if (r.type < 20 || r.type > 23) {  /* :3914-3917 */
+                e = TLSREC_ERR_SSL_INVALID_RECORD;
+            } else if (r.data_len == 0) {      /* :3920-3941 */
+                if (r.type != TLSREC_MSG_APPLICATION_DATA) e = TLSREC_ERR_SSL_INVALID_RECORD;
+                else if (++nbz > 3) e = TLSREC_ERR_SSL_INVALID_MAC;
+            } else {
+                nbz = 0;
+            }
+        }
+        if (e == 0) {
+            w.update_s(seq);                   /* mbedtls_ssl_dtls_replay_update (:4003-4007) */
+            if (r.data_len > 16384) e = TLSREC_ERR_SSL_INVALID_RECORD;   /* :4011-4014 */
+        }
+        disp[kk] = e;
+        if (e == TLSREC_ERR_SSL_INVALID_MAC) { /* :4837-4873 */
+            if (ci.badmac_limit != 0 && ++bms >= ci.badmac_limit) st = e;
+            else dropped = true;
+        } else if (e) {
+            st = e;
+        } else {
+            nacc++;
+        }
+    };
+    /* the header's epoch and 48-bit sequence number (:3683-3687) */
+    auto hdr_rec = [&](const uint8_t *p) __attribute__((always_inline)) { onrec(((uint32_t) p[3] << 8) | p[4], ReplayWindow::seq48(p + 3)); };
+    /* after each datagram */
+    auto ondgram = [&](int32_t stop) __attribute__((always_inline)) {
+        if (!st && !dropped) {
+            if (stop == DG_INVALID) inval++;
+            else if (stop == DG_TRAILING) st = TLSREC_ERR_SSL_INTERNAL_ERROR;
+            else if (stop == DG_EOF) st = TLSREC_ERR_SSL_CONN_EOF;
+        }
+        if (!st) done++;
+        dropped = false;
+    };
     if (!dtls_conn_ok(ci, ndg, slots, cap)) {
         st = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    } else if constexpr (PRE) {
+        dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
+                             [&](uint64_t, const DtlsHdr &, const uint8_t *p) { hdr_rec(p); }, ondgram, prefetch);
     } else {
-        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++) {
-            bool dropped = false;
-            const int32_t stop = dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len,
-                                           [&](const DtlsHdr &, const uint8_t *p) {
-                const uint32_t kk = k++;
-                if (st) { disp[kk] = TLSREC_DTLS_NOT_REACHED; dtls_unreach_wipe(arena, recs, res, slots, kk); return; }
-                if (dropped) { disp[kk] = TLSREC_DTLS_DROPPED; dtls_unreach_wipe(arena, recs, res, slots, kk); return; }
-                const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
-                if (epoch != ci.in_epoch) {            /* :3755-3768, skipped after the handshake (:4727-4800) */
-                    disp[kk] = epoch == (uint32_t) ci.in_epoch + 1 ? TLSREC_ERR_SSL_EARLY_MESSAGE
-                                                                   : TLSREC_ERR_SSL_UNEXPECTED_RECORD;
-                    return;
-                }
-                if (!w.fresh(p + 3)) {                 /* :3769-3776 */
-                    disp[kk] = TLSREC_ERR_SSL_UNEXPECTED_RECORD;
-                    dtls_unreach_wipe(arena, recs, res, slots, kk);
-                    return;
-                }
-                if (recs[kk].slot == NO_SLOT) {        /* not decrypted: impossible, the window only grows */
-                    st = TLSREC_ERR_SSL_INTERNAL_ERROR;
-                    disp[kk] = st;
-                    return;
-                }
-                const tlsrec_batch_res r = res[kk];
-                int32_t e = r.status;                  /* ssl_prepare_record_content (:3810-4017) */
-                if (e == TLSREC_ERR_SSL_UNEXPECTED_CID && ignore_cid) { disp[kk] = e; return; }   /* :3872-3879 */
-                if (e == 0) {
-                    if (r.type < 20 || r.type > 23) {  /* :3914-3917 */
-                        e = TLSREC_ERR_SSL_INVALID_RECORD;
-                    } else if (r.data_len == 0) {      /* :3920-3941 */
-                        if (r.type != TLSREC_MSG_APPLICATION_DATA) e = TLSREC_ERR_SSL_INVALID_RECORD;
-                        else if (++nbz > 3) e = TLSREC_ERR_SSL_INVALID_MAC;
-                    } else {
-                        nbz = 0;
-                    }
-                }
-                if (e == 0) {
-                    w.update(p + 3);                   /* mbedtls_ssl_dtls_replay_update (:4003-4007) */
-                    if (r.data_len > 16384) e = TLSREC_ERR_SSL_INVALID_RECORD;   /* :4011-4014 */
-                }
-                disp[kk] = e;
-                if (e == TLSREC_ERR_SSL_INVALID_MAC) { /* :4837-4873 */
-                    if (ci.badmac_limit != 0 && ++bms >= ci.badmac_limit) st = e;
-                    else dropped = true;
-                } else if (e) {
-                    st = e;
-                } else {
-                    nacc++;
-                }
-            });
-            if (!st && !dropped) {
-                if (stop == DG_INVALID) inval++;
-                else if (stop == DG_TRAILING) st = TLSREC_ERR_SSL_INTERNAL_ERROR;
-                else if (stop == DG_EOF) st = TLSREC_ERR_SSL_CONN_EOF;
-            }
-            if (!st) done++;
-        }
+        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++)
+            ondgram(dtls_walk(arena + dg[d].off, dgram_len(dg[d]), ci.cid_len,
+                              [&](const DtlsHdr &, const uint8_t *p) { hdr_rec(p); }));
     }
     tlsrec_dtls_in_res o;
     memset(&o, 0, sizeof(o));
@@ -844,7 +1221,7 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
     o.window = w.bits;
     o.status = st;
     o.first = first;
-    o.nrec = counts[i];
+    o.nrec = nrec;
     o.naccepted = nacc;
     o.dgrams_done = done;
     o.invalid_dgrams = inval;
@@ -853,13 +1230,14 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
     cres[i] = o;
 }
 
+template <bool PRE>
 __global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
                                    uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
                                    const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
                                    const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dtls_finish_one(i, c, dg, ndg, arena, offs, counts, slots, cap, recs, res, disp, cres);
+    if (i < n) dtls_finish_one<PRE>(i, c, dg, ndg, arena, offs, counts, slots, cap, recs, res, disp, cres);
 }
 
 /* send: one record per datagram */
@@ -1057,9 +1435,26 @@ struct Scratch {
     uint32_t *counts = nullptr, *offs = nullptr;
     HdrStop *stops = nullptr;
     unsigned long long *bytes = nullptr;   /* record bytes of the batch (its mean size steers the GCM launch) */
+    unsigned long long *tstat = nullptr;   /* one-pass framing: tile status words (zeroed with bytes) */
+    uint32_t *tctr = nullptr;              /* one-pass framing: tile counter */
     void *scan_tmp = nullptr;
     size_t scan_bytes = 0;
 };
+}
+
+/* TLSREC_RX_FUSED=0: the DTLS receive framing as count, scan and emit
+ * kernels (r05 / early r06), kept for A/B runs and as the tests' second path;
+ * TLSREC_RX_FUSED_STREAM=1: the stream receive framing in one pass (measured
+ * slower than its three kernels) */
+static bool fused_env(void)
+{
+    const char *e = getenv("TLSREC_RX_FUSED");
+    return !(e && atoi(e) == 0);
+}
+static bool fused_stream_env(void)
+{
+    const char *e = getenv("TLSREC_RX_FUSED_STREAM");
+    return e && atoi(e) != 0;
 }
 
 /* the send paths read the application data in place (r05; TLSREC_STREAM_SRC=0
@@ -1070,20 +1465,41 @@ static bool src_env(void)
     return !(e && atoi(e) == 0);
 }
 
-static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st)
+/* tiles: the one-pass framing kernels' tile status words (0 = none) */
+static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st, uint32_t tiles = 0)
 {
     sc.scan_bytes = tlsrec__scan_scratch_bytes(n + 1);
     const size_t a = 256, sz4 = (((size_t) n + 1) * 4 + a - 1) / a * a, szs = ((size_t) n * sizeof(HdrStop) + a) / a * a;
     constexpr size_t szb = BYTES_SPREAD * BYTES_STRIDE * 8;     /* the spread byte counters */
-    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + szb + sc.scan_bytes + a, &sc.lease);
+    const size_t szt = tiles ? ((size_t) tiles * 8 + a) / a * a + a : 0;   /* status words + the counter's line */
+    const int lr = tlsrec__scratch_acquire(st, 1, 2 * sz4 + szs + szb + szt + sc.scan_bytes + a, &sc.lease);
     if (lr) return lr;
     uint8_t *m = (uint8_t *) sc.lease.mem;
     sc.counts = (uint32_t *) m;
     sc.offs = (uint32_t *) (m + sz4);
     sc.stops = (HdrStop *) (m + 2 * sz4);
     sc.bytes = (unsigned long long *) (m + 2 * sz4 + szs);
-    sc.scan_tmp = m + 2 * sz4 + szs + szb;
-    return hipMemsetAsync(sc.bytes, 0, szb, st) == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    if (tiles) {
+        sc.tstat = (unsigned long long *) (m + 2 * sz4 + szs + szb);
+        sc.tctr = (uint32_t *) (m + 2 * sz4 + szs + szb + szt - a);
+    }
+    sc.scan_tmp = m + 2 * sz4 + szs + szb + szt;
+    return hipMemsetAsync(sc.bytes, 0, szb + szt, st) == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+}
+
+/* after a one-pass framing kernel: offs[n] (the total) and the mean record
+ * size to the host */
+static int fetch_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total, uint32_t *avg_bytes)
+{
+    unsigned long long spread[BYTES_SPREAD * BYTES_STRIDE];
+    if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(spread, sc.bytes, sizeof(spread), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    unsigned long long bytes = 0;
+    for (int k = 0; k < BYTES_SPREAD; k++) bytes += spread[k * BYTES_STRIDE];
+    *avg_bytes = *total ? (uint32_t) (bytes / *total) : 0u;
+    return 0;
 }
 
 /* TLSREC_RX_GROUPWALK=0: the r05 receive framing (one lane per connection
@@ -1126,10 +1542,19 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
     const SlotState *slots = tlsrec__keytab_slots(kt);
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
-    int r = scratch_alloc(sc, nstreams, st);
+    const bool fused = fused_stream_env() && groupwalk_env();
+    const uint32_t tiles = blocks(nstreams, RX_TILE);
+    int r = scratch_alloc(sc, nstreams, st, fused ? tiles : 0u);
     uint32_t total = 0, avg = 0;
     const bool gw = groupwalk_env();
-    if (r == 0) {
+    if (r == 0 && fused) {
+        /* count, scan and emit in one pass (descriptors up to max_records) */
+        hipLaunchKernelGGL(in_frame_kernel, dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
+                           (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
+                           sc.tctr, recs, recs ? max_records : 0u);
+        r = hipGetLastError() == hipSuccess ? fetch_total(sc, nstreams, st, &total, &avg)
+                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    } else if (r == 0) {
         if (gw)
             hipLaunchKernelGGL(in_count_group_kernel, dim3(blocks(nstreams + 1, RX_CONNS)), dim3(RX_THREADS), 0, st,
                                streams, nstreams, (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
@@ -1142,13 +1567,15 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        if (gw)
-            hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
-                               streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
-        else
-            hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
-                               (const uint8_t *) arena, sc.offs, slots, cap, recs);
-        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (!fused) {
+            if (gw)
+                hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                                   streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+            else
+                hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
+                                   (const uint8_t *) arena, sc.offs, slots, cap, recs);
+            if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
         if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }
     if (r == 0) {
@@ -1260,9 +1687,18 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     const SlotState *slots = tlsrec__keytab_slots(kt);
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
-    int r = scratch_alloc(sc, nconns, st);
+    const bool fused = fused_env();
+    const uint32_t tiles = blocks(nconns, DG_THREADS);
+    int r = scratch_alloc(sc, nconns, st, fused ? tiles : 0u);
     uint32_t total = 0, avg = 0;
-    if (r == 0) {
+    if (r == 0 && fused) {
+        /* count, scan and emit in one pass (descriptors up to max_records) */
+        hipLaunchKernelGGL(dtls_frame_kernel, dim3(tiles), dim3(DG_THREADS), 0, st, conns, nconns, dgrams, ndgrams,
+                           (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.bytes, sc.tstat, sc.tctr,
+                           recs, recs ? max_records : 0u);
+        r = hipGetLastError() == hipSuccess ? fetch_total(sc, nconns, st, &total, &avg)
+                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    } else if (r == 0) {
         hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
                            ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
         r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total, &avg)
@@ -1271,14 +1707,20 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     if (r == 0 && total) {
-        hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                           ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
-        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (!fused) {
+            hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
+            if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
         if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     }
     if (r == 0) {
-        hipLaunchKernelGGL(dtls_finish_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                           ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
+        if (fused)
+            hipLaunchKernelGGL(dtls_finish_kernel<true>, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns,
+                               dgrams, ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
+        else
+            hipLaunchKernelGGL(dtls_finish_kernel<false>, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns,
+                               dgrams, ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
     tlsrec__scratch_release(&sc.lease);

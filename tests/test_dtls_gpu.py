@@ -226,9 +226,19 @@ def test_reference_replay_vectors_through_records():
     tab.close()
 
 
-@pytest.mark.parametrize("r06", ["1", "0"], ids=["grouped", "bucket-pass"])
-def test_dispositions_match_oracle(r06, monkeypatch):
-    monkeypatch.setenv("TLSREC_GROUPED", r06)           # the batch without (r06) and with (r05) the bucket pass
+FRAMINGS = [("1", "1"), ("1", "0"), ("0", "0")]
+FRAMING_IDS = ["one-pass", "grouped-3-kernels", "bucket-pass-3-kernels"]
+
+
+def _framing(monkeypatch, fr):
+    grouped, fused = fr
+    monkeypatch.setenv("TLSREC_GROUPED", grouped)       # the batch without (r06) and with (r05) the bucket pass,
+    monkeypatch.setenv("TLSREC_RX_FUSED", fused)        # count / scan / emit as one pass (look-back) or three kernels
+
+
+@pytest.mark.parametrize("fr", FRAMINGS, ids=FRAMING_IDS)
+def test_dispositions_match_oracle(fr, monkeypatch):
+    _framing(monkeypatch, fr)
     cid = b"\xaa\xbb\xcc"
     slots = [(M.CIPHER_AES_128_GCM, prng_bytes(3, 16), prng_bytes(4, 16), b""),
              (M.CIPHER_CHACHA20_POLY1305, prng_bytes(5, 32), prng_bytes(6, 16), cid),
@@ -286,12 +296,12 @@ def test_dispositions_match_oracle(r06, monkeypatch):
     tab.close()
 
 
-@pytest.mark.parametrize("r06", ["1", "0"], ids=["grouped", "bucket-pass"])
-def test_many_datagrams_per_connection(r06, monkeypatch):
+@pytest.mark.parametrize("fr", FRAMINGS, ids=FRAMING_IDS)
+def test_many_datagrams_per_connection(fr, monkeypatch):
     """Many datagrams per connection: 37 and 50 datagrams of one to three records, a bad MAC
     and a replay among them, and a connection with none -- record order and
-    dispositions against the oracle, with and without the bucket pass"""
-    monkeypatch.setenv("TLSREC_GROUPED", r06)           # the batch without (r06) and with (r05) the bucket pass
+    dispositions against the oracle, under every framing path"""
+    _framing(monkeypatch, fr)
     slots = [(M.CIPHER_AES_128_GCM, prng_bytes(13, 16), prng_bytes(14, 16), b""),
              (M.CIPHER_CHACHA20_POLY1305, prng_bytes(15, 32), prng_bytes(16, 16), b"")]
     tab = Table(slots)
@@ -314,6 +324,50 @@ def test_many_datagrams_per_connection(r06, monkeypatch):
     grams0.append(grams0[5])                       # a replayed datagram
     grams1 = [rec(1, k, 100 + k) for k in range(50)]
     conns = [(0, {"in_epoch": 1}, grams0), (1, {"in_epoch": 1}, []), (1, {"in_epoch": 1}, grams1)]
+    check_vs_oracle(tab, conns, tab.decrypt(conns))
+    tab.close()
+
+
+@pytest.mark.parametrize("fr", FRAMINGS[:2], ids=FRAMING_IDS[:2])
+def test_many_connections_match_oracle(fr, monkeypatch):
+    """17 000 connections (67 tiles of the one-pass framing kernel's look-back)
+    of 0..3 datagrams, each of one or two records (the register fast path and
+    the walk from memory), with replays, other epochs, a bad MAC and a
+    trailing byte among them: against the oracle, connection by connection."""
+    _framing(monkeypatch, fr)
+    slots = [(M.CIPHER_AES_128_GCM, prng_bytes(21, 16), prng_bytes(22, 16), b""),
+             (M.CIPHER_CHACHA20_POLY1305, prng_bytes(23, 32), prng_bytes(24, 16), b""),
+             (M.CIPHER_AES_256_GCM, prng_bytes(25, 32), prng_bytes(26, 16), b"")]
+    tab = Table(slots)
+    rng = np.random.default_rng(41)
+
+    def rec(slot, seq, n, epoch=1):
+        st, w, _, _ = O.dtls_encrypt(tab.ot[slot], prng_bytes(seq * 7 + slot, n), 23, ctr(epoch, seq), 16384)
+        assert st == 0
+        return w
+
+    conns = []
+    for i in range(17000):
+        slot = i % 3
+        seq = int(rng.integers(1, 1000))
+        grams = []
+        for _ in range(int(rng.integers(0, 4))):
+            g = rec(slot, seq, int(rng.integers(1, 90)))
+            seq += 1
+            u = rng.random()
+            if u < 0.15:
+                g += rec(slot, seq, int(rng.integers(1, 40)))             # two records in one datagram
+                seq += 1
+            elif u < 0.18:
+                g = g[:20] + bytes([g[20] ^ 1]) + g[21:]                   # bad MAC
+            elif u < 0.20:
+                g += b"\x17"                                             # one trailing byte
+            elif u < 0.23:
+                g = rec(slot, seq - 1, 30, epoch=2)                        # the next epoch
+            grams.append(g)
+        if grams and rng.random() < 0.05:
+            grams.append(grams[0])                                         # a replay
+        conns.append((slot, {"in_epoch": 1}, grams))
     check_vs_oracle(tab, conns, tab.decrypt(conns))
     tab.close()
 

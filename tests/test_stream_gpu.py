@@ -154,21 +154,32 @@ def test_encrypt_then_decrypt_many_connections():
     c.close()
 
 
-@pytest.mark.parametrize("r06", ["1", "0"], ids=["groupwalk", "r05-framing"])
-def test_irregular_record_lengths_match_oracle(r06, monkeypatch):
+FRAMINGS = [("1", "1", "1"), ("1", "1", "0"), ("0", "0", "0")]
+FRAMING_IDS = ["one-pass", "groupwalk-3-kernels", "r05-framing"]
+
+
+def _framing(monkeypatch, fr):
+    gw, grouped, fused = fr
+    monkeypatch.setenv("TLSREC_RX_GROUPWALK", gw)       # the r06 lane-group walks or the r05 one-lane walks,
+    monkeypatch.setenv("TLSREC_GROUPED", grouped)       # with and without the bucket pass,
+    monkeypatch.setenv("TLSREC_RX_FUSED_STREAM", fused) # count / scan / emit as one pass (look-back) or three kernels
+
+
+@pytest.mark.parametrize("fr", FRAMINGS, ids=FRAMING_IDS)
+def test_irregular_record_lengths_match_oracle(fr, monkeypatch):
     """Streams whose records change length mid-stream (runs of one length,
     single odd records, CCS records between, 1..40 records, a trailing
     partial record or a bad header after a run): the lane-group walk (a
     run of equal lengths checked 16 headers at a time)
     must frame exactly what the serial walk does -- records, sequence
-    numbers, stop status and position -- under both framing paths."""
-    monkeypatch.setenv("TLSREC_RX_GROUPWALK", r06)      # the r06 lane-group walks and the r05 one-lane walks,
-    monkeypatch.setenv("TLSREC_GROUPED", r06)           # with and without the bucket pass
+    numbers, stop status and position -- under every framing path (1 200
+    connections: 75 tiles of the one-pass kernel's look-back)."""
+    _framing(monkeypatch, fr)
     slots = _slots(53)
     c = Conns(slots)
     rng = np.random.default_rng(29)
     conns = []
-    for i in range(120):
+    for i in range(1200):
         slot = i % 20
         t = c.ot[slot]
         ctr0 = int(rng.integers(0, 1 << 40))

@@ -2,7 +2,6 @@
 # Round-6 profiling probes (one box per call; each GPU step under its own
 # timeout, chained).
 #   tools/gpu_pcs.sh frame   -- kernel trace of the 1 M-record receive calls (stream / DTLS, ChaCha and AES)
-#   tools/gpu_pcs.sh pcs     -- PC sampling (host trap) of the DTLS 16 x 1.4 KiB AES-128-GCM rows
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -16,9 +15,5 @@ frame)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/dtls_cp -o run --output-format csv -- python3 $R/tools/bench_dtls.py --cipher 3 --no-cpu --steps 3 > $O/dtls_cp.json 2>&1 &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/dtls_small -o run --output-format csv -- python3 $R/tools/bench_dtls.py --no-cpu --steps 3 > $O/dtls_small.json 2>&1 &&
   echo frame done
-  ;;
-pcs)
-  timeout -s KILL 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval 1 -d $O/pcs_dtls -o run --output-format csv -- python3 $R/tools/bench_dtls.py --no-cpu --steps 3 > $O/pcs_dtls.log 2>&1
-  rc=$?; echo "pcs rc=$rc"; tail -5 $O/pcs_dtls.log; find $O/pcs_dtls -type f | head
   ;;
 esac

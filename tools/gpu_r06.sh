@@ -73,10 +73,11 @@ libab)   # same-box A/B of two libraries on bench.py configs: LIBA LIBB CONFIGS 
   ;;
 multiab)   # same-box A/B of several libraries (LIBS) on bench configs (CONFIGS) and rows (ROWS: stream16s dtls_small stream_cp dtls_cp), alternating, REPS reps
   : > $O/multiab.jsonl
-  for rep in $(seq ${REPS:-2}); do for lib in $LIBS; do
-    tag=$(basename $lib .so)
+  for rep in $(seq ${REPS:-2}); do for ent in $LIBS; do
+    lib=${ent%%:*}; envs=""; [ "$ent" != "$lib" ] && envs=$(echo "${ent#*:}" | tr ',' ' ')
+    tag=$(basename $lib .so)${envs:+:$envs}
     for c in $CONFIGS; do
-      TLSREC_LIBRARY=$R/$lib timeout -k 10 300 python3 bench.py --config $c --no-cpu --no-e2e --verify 16 > $O/t.json 2> $O/t.err || { echo "FAIL $c $tag"; tail -3 $O/t.err; exit 1; }
+      env $envs TLSREC_LIBRARY=$R/$lib timeout -k 10 300 python3 bench.py --config $c --no-cpu --no-e2e --verify 16 > $O/t.json 2> $O/t.err || { echo "FAIL $c $tag"; tail -3 $O/t.err; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(json.dumps(dict(row=sys.argv[2], lib=sys.argv[3], rep=$rep, value=d['value'], kernel_ms=d['roofline']['kernel_ms_avg'], bad=d['check']['bad_records'])))" $O/t.json $c $tag >> $O/multiab.jsonl
     done
     for name in $ROWS; do
@@ -86,11 +87,27 @@ multiab)   # same-box A/B of several libraries (LIBS) on bench configs (CONFIGS)
         dtls_small) set -- tools/bench_dtls.py;;
         dtls_cp) set -- tools/bench_dtls.py --cipher 3;;
       esac
-      TLSREC_LIBRARY=$R/$lib timeout -k 10 200 python3 "$@" --no-cpu > $O/t.json 2> $O/t.err || { echo "FAIL $name $tag"; tail -3 $O/t.err; exit 1; }
+      env $envs TLSREC_LIBRARY=$R/$lib timeout -k 10 200 python3 "$@" --no-cpu > $O/t.json 2> $O/t.err || { echo "FAIL $name $tag"; tail -3 $O/t.err; exit 1; }
       python3 -c "import json; [print(json.dumps(dict(row='$name'+('_enc' if 'encrypt' in d['metric'] else '_dec'), lib='$tag', rep=$rep, value=d['value'], kernel_ms=(d.get('roofline') or {}).get('kernel_ms_avg'), check=d.get('check')))) for d in map(json.loads, open('$O/t.json'))]" >> $O/multiab.jsonl
     done
   done; done
   python3 tools/ab_summary.py $O/multiab.jsonl
+  ;;
+fusedab)   # one-pass receive framing: stream / DTLS GPU tests, A/B (TLSREC_RX_FUSED 0 / 1) on the receive rows, kernel trace
+  timeout -k 10 500 python -u -m pytest tests/test_stream_gpu.py tests/test_dtls_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/stream_tests.txt 2>&1 \
+      || { echo "stream tests failed"; tail -30 $O/stream_tests.txt; exit 1; }
+  tail -1 $O/stream_tests.txt
+  : > $O/fusedab.jsonl
+  for rep in 1 2; do for f in 0 1; do
+    for row in "stream_cp tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3" "stream16s tools/bench_stream.py --conns 65536 --recs 16 --content 1400" "dtls_cp tools/bench_dtls.py --cipher 3" "dtls_small tools/bench_dtls.py"; do
+      set -- $row; name=$1; shift
+      TLSREC_RX_FUSED=$f timeout -k 10 200 python3 "$@" --no-cpu > $O/t.json 2> $O/t.err || { echo "FAIL $name"; tail -3 $O/t.err; exit 1; }
+      python3 -c "import json; [print(json.dumps(dict(row='$name'+('_enc' if 'encrypt' in d['metric'] else '_dec'), lib='fused$f', rep=$rep, value=d['value'], kernel_ms=(d.get('roofline') or {}).get('kernel_ms_avg'), check=d.get('check')))) for d in map(json.loads, open('$O/t.json'))]" >> $O/fusedab.jsonl
+    done
+  done; done
+  python3 tools/ab_summary.py $O/fusedab.jsonl
+  cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_stream_cp -o run --output-format csv -- python3 $R/tools/bench_stream.py --conns 262144 --recs 4 --content 1400 --cipher 3 --no-cpu --steps 3 > $R/$O/prof_stream_cp.json 2>&1 && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_dtls_cp -o run --output-format csv -- python3 $R/tools/bench_dtls.py --cipher 3 --no-cpu --steps 3 > $R/$O/prof_dtls_cp.json 2>&1 && cd $R && echo prof done
   ;;
 rowab)   # same-box A/B of libraries on the stream / DTLS rows: LIBS (env, space separated)
   : > $O/rowab.jsonl
