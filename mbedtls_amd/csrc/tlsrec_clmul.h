@@ -187,4 +187,39 @@ TLSREC_CLMUL_FN void tlsrec_gtab4_base(const uint32_t p[4], uint32_t k, uint64_t
     tlsrec_gf128_shr(bh, bl, sh - s1);
 }
 
+/* V * X (V >> 1 as the big-endian number, the bit falling off X^127 folded
+ * back as X^128 = X^7 + X^2 + X + 1, i.e. 0xE1 at the top) -- a masked
+ * constant instead of tlsrec_gf128_shr's general fold */
+TLSREC_CLMUL_FN void tlsrec_gf128_mulx(uint64_t *hi, uint64_t *lo)
+{
+    const uint64_t m = 0 - (*lo & 1u);
+    *lo = (*lo >> 1) | (*hi << 63);
+    *hi = (*hi >> 1) ^ (m & 0xE100000000000000ull);
+}
+
+/* Entries 4q .. 4q + 3 of window k of P's 4-bit position table (the layout
+ * of tlsrec_gtab4_entry), as the paired GCM passes build it (r06): one lane
+ * per (window, quarter), B_k = P X^(4k) and its multiples by X, X^2, X^3
+ * once, the quarter's two high bits selecting its base, the four entries
+ * the base plus the 0 / X^3 / X^2 / X^2 + X^3 multiples (with tlsrec_gtab4_entry
+ * per entry, 16 general shifts a lane).  out: 4 entries in the kernels' word
+ * layout. */
+TLSREC_CLMUL_FN void tlsrec_gtab4_quad(const uint32_t p[4], uint32_t k, uint32_t q, uint32_t out[4][4])
+{
+    uint64_t h0, l0;
+    tlsrec_gtab4_base(p, k, &h0, &l0);                 /* B X^0: n bit 3 */
+    uint64_t h1 = h0, l1 = l0;
+    tlsrec_gf128_mulx(&h1, &l1);                       /* B X^1: n bit 2 */
+    uint64_t h2 = h1, l2 = l1;
+    tlsrec_gf128_mulx(&h2, &l2);                       /* B X^2: n bit 1 */
+    uint64_t h3 = h2, l3 = l2;
+    tlsrec_gf128_mulx(&h3, &l3);                       /* B X^3: n bit 0 */
+    const uint64_t m3 = 0 - (uint64_t) ((q >> 1) & 1u), m2 = 0 - (uint64_t) (q & 1u);   /* masks: P is secret */
+    const uint64_t bh = (h0 & m3) ^ (h1 & m2), bl = (l0 & m3) ^ (l1 & m2);
+    tlsrec_g_to_words(bh, bl, out[0]);
+    tlsrec_g_to_words(bh ^ h3, bl ^ l3, out[1]);
+    tlsrec_g_to_words(bh ^ h2, bl ^ l2, out[2]);
+    tlsrec_g_to_words(bh ^ h2 ^ h3, bl ^ l2 ^ l3, out[3]);
+}
+
 #endif /* TLSREC_CLMUL_H */

@@ -31,6 +31,11 @@
 #ifndef TLSREC_ABLATE
 #define TLSREC_ABLATE 0
 #endif
+/* paired passes: the tag stage's plan fields kept in LDS from the setup
+ * (r06; bit 0 decrypt, bit 1 encrypt) */
+#ifndef TLSREC_PLAN_STASH
+#define TLSREC_PLAN_STASH 0      /* measured: no gain, the spills move */
+#endif
 
 namespace tlsrec {
 
@@ -86,14 +91,27 @@ __device__ __forceinline__ void pair_sync(uint32_t *cnt, uint32_t &phase, int la
 }
 
 /* Half ph of the pair builds windows 16 ph .. 16 ph + 15 of the 4-bit
- * position table of P (tlsrec_clmul.h tlsrec_gtab4_*) at tab: lane (k0, n)
- * makes entry n of windows k0, k0 + 4, k0 + 8, k0 + 12.  Out of line: the
- * record kernel's registers are full, and inlined the build moved its spills
- * into the per-record code. */
+ * position table of P (tlsrec_clmul.h) at tab: lane (k, q) makes entries
+ * 4q .. 4q + 3 of window 16 ph + k (tlsrec_gtab4_quad: the window's base and
+ * its three multiples by X, then XORs -- r06; r05's lane (k0, n) made one
+ * entry of four windows, each entry from four general shifts, ~4x the VALU
+ * work).  Out of line: the record kernel's registers are full, and inlined
+ * the build moved its spills into the per-record code. */
+#ifndef TLSREC_GTAB_QUAD
+#define TLSREC_GTAB_QUAD 1
+#endif
 __device__ __noinline__ void gtab4_build_half(uint8_t *tab, const uint4 *pp, int lane, int ph)
 {
     const uint4 pv = *pp;
     const uint32_t pw[4] = { pv.x, pv.y, pv.z, pv.w };
+#if TLSREC_GTAB_QUAD
+    const uint32_t k = 16u * (uint32_t) ph + ((uint32_t) lane >> 2), q = (uint32_t) lane & 3u;
+    uint32_t w[4][4];
+    tlsrec_gtab4_quad(pw, k, q, w);
+    uint4 *dst = reinterpret_cast<uint4 *>(tab + k * 256 + q * 64);
+#pragma unroll
+    for (int t = 0; t < 4; t++) dst[t] = make_uint4(w[t][0], w[t][1], w[t][2], w[t][3]);
+#else
     const uint32_t n = (uint32_t) lane & 15u, k0 = 16u * (uint32_t) ph + ((uint32_t) lane >> 4);
     uint64_t bh, bl;
     tlsrec_gtab4_base(pw, k0, &bh, &bl);
@@ -107,6 +125,7 @@ __device__ __noinline__ void gtab4_build_half(uint8_t *tab, const uint4 *pp, int
         dst[t * 64] = make_uint4(w[0], w[1], w[2], w[3]);    /* window k0 + 4 t */
         if (t < 3) tlsrec_gf128_shr(&bh, &bl, 16);
     }
+#endif
 }
 
 /* Per-record state that the AEAD loop reads (kept small: it lives in
@@ -429,6 +448,23 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                         if (q == 0) finish_early(p, d, a.out, &a.res[ridx]);
                     } else {
                         jb.setup<DEC>(p, d, km, a.in, a.out);
+                        if constexpr (PAIR && (TLSREC_PLAN_STASH & (DEC ? 1 : 2)) != 0) {
+                            /* (r06) what the tag stage needs of the plan, in the
+                             * record's fold slot (unused with lane powers): the
+                             * stage no longer reloads the descriptor and re-derives
+                             * the plan (only a failed tag does, for the wipe) */
+                            if (q == 0)
+                                reinterpret_cast<uint4 *>(lds + LY::FOLD)[wave * LY::FOLDN + g] =
+                                    make_uint4(p.data_offset, p.data_len, (uint32_t) p.post_status,
+                                               (uint32_t) p.type | ((uint32_t) d.type << 8));
+                            if constexpr (!DEC)
+                                if (q == 0 && p.explicit_iv && p.post_status == 0) {
+                                    /* the explicit nonce now, not after the AEAD: the
+                                     * AEAD never reads these 8 bytes of head room */
+                                    uint8_t *e = a.out + d.buf_off + p.data_offset;
+                                    for (int i = 0; i < 8; i++) e[i] = d.ctr[i];
+                                }
+                        }
                         if constexpr (!DEC)
                             if (a.src_off) {           /* the content in the caller's buffer (stream send) */
                                 jb.src = a.in + a.src_off[ridx];
@@ -600,7 +636,8 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                          * and written back part-used.  Load G steps' blocks
                          * together and store them together: each line is touched
                          * once per direction. */
-                        if constexpr (PAIR && L <= 4 && B == 1 && TLSREC_GCM_LINE_GROUPS) {
+                        if constexpr ((PAIR || (TLSREC_GCM_LINE_GROUPS & 2)) && L <= 4 && B == 1 &&
+                                      (TLSREC_GCM_LINE_GROUPS & 1)) {
                             constexpr int G = 128 / (16 * L);
                             /* single steps up to a group boundary: groups then
                              * start on a line for records without front padding
@@ -723,6 +760,49 @@ __global__ __launch_bounds__(W * 64) void tlsrec_gcm_kernel(GcmArgs a)
                 if (!jb.run) continue;
                 const uint4 ej0 = reinterpret_cast<const uint4 *>(lds + LY::EJ0)[wave * 64 + (slot_in_chunk & 63)];
                 const uint4 tag = xor4(Y, ej0);
+                if constexpr (PAIR && (TLSREC_PLAN_STASH & (DEC ? 1 : 2)) != 0) {
+                    const uint4 ps = reinterpret_cast<const uint4 *>(lds + LY::FOLD)[wave * LY::FOLDN + g];
+                    tlsrec_batch_res r;
+                    r.data_offset = ps.x;
+                    r.data_len = ps.y;
+                    r.cid_len = 0;
+                    r.reserved[0] = r.reserved[1] = 0;
+                    if (!DEC) {
+                        if (q == 0) {
+                            store_block(jb.dst, jb.aead_len, jb.aead_len + 16, tag, false);
+                            r.status = (int32_t) ps.z;
+                            r.type = (uint8_t) ps.w;
+                            a.res[ridx] = r;
+                        }
+                    } else {
+                        uint4 want = load_block(jb.src, jb.aead_len, jb.aead_len + 16, jb.aead_len + 16, 0, false);
+                        uint32_t diff = (want.x ^ tag.x) | (want.y ^ tag.y) | (want.z ^ tag.z) | (want.w ^ tag.w);
+                        diff = group_or<L>(q == 0 ? diff : 0u);               /* the group leader's verdict, to all */
+                        uint32_t key = group_max<L>(nzkey);
+                        r.type = (uint8_t) (ps.w >> 8);                       /* d.type */
+                        if (diff != 0) {
+                            /* PSA wipes the whole output buffer on a bad tag (the
+                             * plan's AEAD position from the descriptor again) */
+                            const tlsrec_batch_rec d = dsrc[didx];
+                            tlsrec_plan p;
+                            make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);
+                            zero_range(a.out + d.buf_off, p.aead_pos, d.buf_len, q, L);
+                            r.status = TLSREC_E_INVALID_MAC;
+                        } else if (jb.inner) {                               /* ssl_msg.c:1809-1829 */
+                            if (key == 0) {
+                                r.status = TLSREC_E_INVALID_RECORD;
+                            } else {
+                                r.status = 0;
+                                r.data_len = (key >> 8) - 1;
+                                r.type = (uint8_t) (key & 0xff);
+                            }
+                        } else {
+                            r.status = 0;
+                        }
+                        if (q == 0) a.res[ridx] = r;
+                    }
+                    continue;
+                }
                 const tlsrec_batch_rec d = dsrc[didx];
                 tlsrec_plan p;
                 make_plan<DEC, CID>(p, d, km, &a.slots[s], a.in);

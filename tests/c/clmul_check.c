@@ -36,3 +36,17 @@ void clmul_check_gtab4(const uint8_t p[16], uint8_t out[8192])
             }
         }
 }
+
+/* the same table from tlsrec_gtab4_quad, the r06 build of the paired GCM
+ * passes: lane (window k, quarter q) makes entries 4q .. 4q + 3 */
+void clmul_check_gtab4_quad(const uint8_t p[16], uint8_t out[8192])
+{
+    uint32_t a[4];
+    memcpy(a, p, 16);
+    for (uint32_t k = 0; k < 32; k++)
+        for (uint32_t q = 0; q < 4; q++) {
+            uint32_t w[4][4];
+            tlsrec_gtab4_quad(a, k, q, w);
+            memcpy(out + k * 256 + q * 64, w, 64);
+        }
+}

@@ -60,16 +60,18 @@ def _xpow_string(bits):
     return bytes(v)
 
 
-def test_gtab4_table_vs_oracle(libs):
+@pytest.mark.parametrize("fn", ["clmul_check_gtab4", "clmul_check_gtab4_quad"], ids=["entry", "quad"])
+def test_gtab4_table_vs_oracle(libs, fn):
     """the 4-bit position table built from P alone (tlsrec_gtab4_*, what the
     paired GCM passes build in LDS from H^L): entry n of window k = P * sum of
     X^(4k+i) over the set bits 3-i of n, against the oracle's multiply --
-    every window and entry, for H-like and edge values of P"""
+    every window and entry, for H-like and edge values of P; built entry by
+    entry (r05) and a quarter window per lane (r06, tlsrec_gtab4_quad)"""
     c, o = libs
     vals = [b"\x80" + bytes(15), bytes(15) + b"\x01", b"\xff" * 16] + [prng_bytes(9800 + i, 16) for i in range(12)]
     out = ctypes.create_string_buffer(8192)
     for p in vals:
-        c.clmul_check_gtab4(p, out)
+        getattr(c, fn)(p, out)
         for k in range(32):
             for n in range(16):
                 want = _mul(o, "orc_gf128_mul", p, _xpow_string([4 * k + i for i in range(4) if (n >> (3 - i)) & 1]))
