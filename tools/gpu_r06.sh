@@ -152,7 +152,10 @@ rows)   # the round's one full sweep on the final build: -m gpu suite, smoke, ev
   row c2 400 python3 bench.py && summ c2 &&
   for c in c3 c4 c4s k4 c1 c2s c3d chacha16k gcm192 ccm ccm8 aria256 camellia128; do
     row $c 400 python3 bench.py --config $c --no-e2e && summ $c || exit 1
-  done &&
+  done
+  [ "${ROWS_SPLIT:-0}" = 1 ] && { echo "rows part 1 done"; exit 0; }
+  ;&
+rows2)   # the second half of rows (ROWS_SPLIT=1 rows, then rows2: each call under gpurun's 20-minute limit)
   row count_gpus 60 python3 -c "import bench, json; print(json.dumps({'count_gpus': bench.count_gpus()}))" && cat $O/count_gpus.json &&
   row dist1 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --dist && summ dist1 &&
   row stream16 300 python3 tools/bench_stream.py --conns 65536 --recs 16 &&
