@@ -476,6 +476,32 @@ __device__ __forceinline__ void gmul_word(const uint8_t *lds, uint32_t wd, int d
     }
 }
 
+/* gmul_word with the table at LDS offset base (a multiple of 256) of the
+ * kernel's LDS array lds: the entry address as base | (nibble x 16) --
+ * one v_and_or per read where lds-relative pointer arithmetic took a shift,
+ * a mask and an add (r06; the paired passes' tables sit at a per-pair base) */
+#ifndef TLSREC_GH_OR
+#define TLSREC_GH_OR 1
+#endif
+template <int PI, int NE = 4>
+__device__ __forceinline__ void gmul_word_or(const uint8_t *lds, uint32_t base, uint32_t wd, int d, uint4 &acc,
+                                             int e0 = 0)
+{
+#pragma unroll
+    for (int i = 0; i < NE; i++) {
+        const int e = e0 + i;
+        const int b = 4 * d + e;
+        const uint32_t ahi = base | ((e == 0) ? (wd & 0xf0u) : ((wd >> (8 * e)) & 0xf0u));
+        const uint32_t alo = base | ((e == 0) ? ((wd << 4) & 0xf0u) : ((wd >> (8 * e - 4)) & 0xf0u));
+        uint4 th = *reinterpret_cast<const uint4 *>(lds + ahi + PI * 8192 + (2 * b) * 256);
+        uint4 tl = *reinterpret_cast<const uint4 *>(lds + alo + PI * 8192 + (2 * b + 1) * 256);
+        acc.x = xor3(acc.x, th.x, tl.x);
+        acc.y = xor3(acc.y, th.y, tl.y);
+        acc.z = xor3(acc.z, th.z, tl.z);
+        acc.w = xor3(acc.w, th.w, tl.w);
+    }
+}
+
 /* ---------------- GHASH with 5-bit position tables (G5) ------------------ *
  * ds_read_b64 serves 32 lanes per LDS cycle over all 64 banks, so a 256-byte
  * image of 32 eight-byte entries is conflict-free for any index: a 5-bit
@@ -687,7 +713,10 @@ __device__ __forceinline__ void aes_ghash(const uint8_t *lds, const uint8_t *gh,
                 else if (g < 6) asm volatile("" : "+v"(w[2]), "+v"(w[3]));
                 else asm volatile("" : "+v"(w[3]));
             } else {
-                gmul_word<PI, 2>(gh, w[g >> 1], g >> 1, acc, 2 * (g & 1));
+                if constexpr (TLSREC_GH_OR)
+                    gmul_word_or<PI, 2>(lds, (uint32_t) (gh - lds), w[g >> 1], g >> 1, acc, 2 * (g & 1));
+                else
+                    gmul_word<PI, 2>(gh, w[g >> 1], g >> 1, acc, 2 * (g & 1));
                 asm volatile("" : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(acc.x), "+v"(acc.y), "+v"(acc.z),
                              "+v"(acc.w));
                 /* the words still to be read enter the next phase through the barrier */
