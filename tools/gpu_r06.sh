@@ -182,6 +182,19 @@ prof)   # rocprofv3 kernel stats + PMC passes on the final build
   profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 --no-cpu > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
   echo prof done
   ;;
+profa)   # final-build profiles, part 1: c2 (headline), c2s, c4s (kernel stats + PMC passes, cache passes for c4s)
+  export PROFILE_RDREQ=1
+  PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2 > $O/prof_c2.log 2>&1 || { echo "c2 failed"; tail -5 $O/prof_c2.log; exit 1; }
+  PMC_RECORDS=262144 profiles/run_profile.sh ${T}_c2s --config c2s > $O/prof_c2s.log 2>&1 || { echo "c2s failed"; tail -5 $O/prof_c2s.log; exit 1; }
+  PROFILE_CACHE=1 PMC_RECORDS=4194304 profiles/run_profile.sh ${T}_c4s --config c4s > $O/prof_c4s.log 2>&1 || { echo "c4s failed"; tail -5 $O/prof_c4s.log; exit 1; }
+  echo profa done
+  ;;
+profb)   # final-build profiles, part 2: DTLS and stream 16 x 1.4 KiB AES rows (+ cache passes)
+  export PROFILE_RDREQ=1 PROFILE_CACHE=1
+  profiles/run_profile.sh ${T}_dtls_small --cmd tools/bench_dtls.py --steps 3 --no-cpu > $O/prof_dtls.log 2>&1 || { echo "dtls failed"; tail -5 $O/prof_dtls.log; exit 1; }
+  profiles/run_profile.sh ${T}_stream16s --cmd tools/bench_stream.py --conns 65536 --recs 16 --content 1400 --steps 3 --no-cpu > $O/prof_stream.log 2>&1 || { echo "stream failed"; tail -5 $O/prof_stream.log; exit 1; }
+  echo profb done
+  ;;
 profsmall)   # the paired-pass rows only: c4s, DTLS and stream 16 x 1.4 KiB (+ cache / UTCL1 passes)
   export PROFILE_RDREQ=1 PROFILE_CACHE=1
   PMC_RECORDS=4194304 profiles/run_profile.sh ${T}_c4s --config c4s > $O/prof_c4s.log 2>&1 || { echo "c4s failed"; tail -5 $O/prof_c4s.log; exit 1; }
