@@ -178,7 +178,10 @@ __global__ void in_finish_kernel(const tlsrec_stream_in *s, uint32_t n, const ui
     /* records in chunks of FK: the chunk's descriptors and results are loaded
      * before the in-order rules run over them (r06: one record's loads at a
      * time left the lane waiting on memory once per record) */
-    constexpr uint32_t FK = 4;
+#ifndef TLSREC_STREAM_FK
+#define TLSREC_STREAM_FK 4
+#endif
+    constexpr uint32_t FK = TLSREC_STREAM_FK;
     bool broke = false;
     for (uint32_t k0 = 0; k0 < cnt && !broke; k0 += FK) {
         tlsrec_batch_res rr[FK];
@@ -891,6 +894,10 @@ __device__ __forceinline__ void dtls_conn_walk(uint32_t d0, uint32_t d1, const t
 #define TLSREC_DG_U 4
 #endif
 constexpr int DG_U = TLSREC_DG_U;
+#ifndef TLSREC_DGF_U
+#define TLSREC_DGF_U TLSREC_DG_U
+#endif
+constexpr int DGF_U = TLSREC_DGF_U;      /* the in-order finish's datagrams per load batch */
 
 /* the anti-replay window (mbedtls_ssl_dtls_replay_check / _update, ssl_msg.c:3248-3306) */
 struct ReplayWindow {
@@ -1102,14 +1109,14 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
     uint32_t k = first;
     int32_t st = 0;
     bool dropped = false;
-    /* PRE: the next DG_U records' results and slots (record kb + u) */
+    /* PRE: the next DGF_U records' results and slots (record kb + u) */
     uint32_t kb = 0;
-    tlsrec_batch_res pr[DG_U];
-    uint32_t ps[DG_U];
+    tlsrec_batch_res pr[DGF_U];
+    uint32_t ps[DGF_U];
     auto prefetch = [&]() __attribute__((always_inline)) {
         kb = k;
 #pragma unroll
-        for (int u = 0; u < DG_U; u++) {
+        for (int u = 0; u < DGF_U; u++) {
             if (k + u < first + nrec) {
                 pr[u] = res[k + u];
                 ps[u] = recs[k + u].slot;
@@ -1125,12 +1132,12 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
         uint32_t qslot = 0;
         tlsrec_batch_res qr;
         if constexpr (PRE) {
-            if (kk - kb < (uint32_t) DG_U) {
+            if (kk - kb < (uint32_t) DGF_U) {
                 have = true;
                 qslot = ps[0];
                 qr = pr[0];
 #pragma unroll
-                for (int u = 0; u + 1 < DG_U; u++) {
+                for (int u = 0; u + 1 < DGF_U; u++) {
                     ps[u] = ps[u + 1];
                     pr[u] = pr[u + 1];
                 }
@@ -1208,7 +1215,7 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
     if (!dtls_conn_ok(ci, ndg, slots, cap)) {
         st = TLSREC_ERR_SSL_BAD_INPUT_DATA;
     } else if constexpr (PRE) {
-        dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
+        dtls_conn_walk<DGF_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
                              [&](uint64_t, const DtlsHdr &, const uint8_t *p) { hdr_rec(p); }, ondgram, prefetch);
     } else {
         for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++)
