@@ -137,7 +137,7 @@ __global__ void in_count_kernel(const tlsrec_stream_in *s, uint32_t n, const uin
 }
 
 __global__ void in_emit_kernel(const tlsrec_stream_in *s, uint32_t n, const uint8_t *arena, const uint32_t *offs,
-                               const SlotState *slots, uint32_t cap, tlsrec_batch_rec *recs)
+                               const SlotState *slots, uint32_t cap, tlsrec_batch_rec *recs, uint32_t max_records)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -159,7 +159,7 @@ __global__ void in_emit_kernel(const tlsrec_stream_in *s, uint32_t n, const uint
         d.ver[0] = v0;
         d.ver[1] = v1;
         if (!ccs) seq++;
-        out[k] = d;
+        if (offs[i] + k < max_records) out[k] = d;      /* (launched before the host has checked the total) */
     });
 }
 
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(RX_THREADS) void in_count_group_kernel(const tlsrec
 __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_stream_in *s, uint32_t n,
                                                                    const uint8_t *arena, const uint32_t *offs,
                                                                    const SlotState *slots, uint32_t cap,
-                                                                   tlsrec_batch_rec *recs)
+                                                                   tlsrec_batch_rec *recs, uint32_t max_records)
 {
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_
         d.type = (uint8_t) h.type;
         d.ver[0] = h.v0;
         d.ver[1] = h.v1;
-        out[k] = d;
+        if (offs[i] + k < max_records) out[k] = d;      /* (launched before the host has checked the total) */
     });
 }
 
@@ -967,7 +967,7 @@ __global__ void dtls_count_kernel(const tlsrec_dtls_in *c, uint32_t n, const tls
  * among them (replayed copies of a record that then fails its MAC included). */
 __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
                                  const uint8_t *arena, const uint32_t *offs, const SlotState *slots, uint32_t cap,
-                                 tlsrec_batch_rec *recs)
+                                 tlsrec_batch_rec *recs, uint32_t max_records)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -992,7 +992,8 @@ __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsr
             r.cid_off[0] = 11;                         /* the CID follows the sequence number */
             const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
             r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
-            recs[k++] = r;
+            if (k < max_records) recs[k] = r;          /* (launched before the host has checked the total) */
+            k++;
         });
     }
 }
@@ -1429,6 +1430,33 @@ __global__ void dtls_out_finish_kernel(const tlsrec_stream_out *s, uint32_t n, c
     sres[i] = o;
 }
 
+/* The batch's record count and byte total to the host (r06): one wave sums
+ * the spread byte counters and writes both into the calling thread's
+ * host-mapped mailbox, then the call's sequence number after a release
+ * fence.  Replaces two device-to-host copies and a stream synchronize: the
+ * host reads the totals while the kernels queued behind this one (the
+ * descriptor emit) still run.  (The copies cost 4 us each with a 20 us gap
+ * between them, and the launch after the synchronize another 30 us, per
+ * receive call; profiles/r06/ab/mailbox/.) */
+struct TotMbox {
+    uint64_t total, bytes, seq, pad;
+};
+
+__global__ void __launch_bounds__(64) totals_kernel(const uint32_t *total_p, const unsigned long long *spread,
+                                                    TotMbox *mb, uint64_t seq)
+{
+    const int lane = threadIdx.x;
+    unsigned long long v = lane < BYTES_SPREAD ? spread[lane * BYTES_STRIDE] : 0ull;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) {
+        mb->total = *total_p;
+        mb->bytes = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(&mb->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 } /* namespace tlsst */
 
 using namespace tlsst;
@@ -1494,19 +1522,86 @@ static int scratch_alloc(Scratch &sc, uint32_t n, hipStream_t st, uint32_t tiles
     return hipMemsetAsync(sc.bytes, 0, szb + szt, st) == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
 }
 
+/* The calling thread's host-mapped mailbox (allocated on first use, kept:
+ * a thread's calls are sequential, so one mailbox per thread serves them) */
+namespace {
+struct Mailbox {
+    TotMbox *h = nullptr, *d = nullptr;
+    uint64_t seq = 0;
+};
+thread_local Mailbox t_mbox;
+}
+
+/* TLSREC_RX_MAILBOX=0: the totals come back by two copies and a stream
+ * synchronize (before r06's second session), for A/B runs */
+static bool mailbox_env(void)
+{
+    const char *e = getenv("TLSREC_RX_MAILBOX");
+    return !(e && atoi(e) == 0);
+}
+
+/* queue the totals kernel: offs[n] and the byte counters to the mailbox;
+ * *seq = the value collect_totals waits for (0: the copy path, nothing queued) */
+static int publish_totals(Scratch &sc, uint32_t n, hipStream_t st, uint64_t *seq)
+{
+    *seq = 0;
+    if (!mailbox_env()) return 0;
+    Mailbox &m = t_mbox;
+    if (!m.h) {
+        void *h = nullptr, *d = nullptr;
+        if (hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        memset(h, 0, 256);
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            hipHostFree(h);
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
+        m.h = (TotMbox *) h;
+        m.d = (TotMbox *) d;
+    }
+    *seq = ++m.seq;
+    hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, st, sc.offs + n, sc.bytes, m.d, *seq);
+    return hipGetLastError() == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+}
+
+/* the totals publish_totals queued (seq != 0), or by copies and a stream
+ * synchronize (seq == 0); the mean record size into *avg_bytes */
+static int collect_totals(Scratch &sc, uint32_t n, hipStream_t st, uint64_t seq, uint32_t *total,
+                          uint32_t *avg_bytes)
+{
+    unsigned long long bytes = 0;
+    if (seq) {
+        TotMbox *h = t_mbox.h;
+        for (uint64_t it = 0;; it++) {
+            if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) == seq) break;
+            if ((it & 1023) == 1023) {      /* a stream that failed or drained without the totals: an error */
+                const hipError_t q = hipStreamQuery(st);
+                if (q != hipSuccess && q != hipErrorNotReady) return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                if (q == hipSuccess && __atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) != seq)
+                    return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+            }
+        }
+        *total = (uint32_t) __atomic_load_n(&h->total, __ATOMIC_RELAXED);
+        bytes = __atomic_load_n(&h->bytes, __ATOMIC_RELAXED);
+    } else {
+        unsigned long long spread[BYTES_SPREAD * BYTES_STRIDE];
+        if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(spread, sc.bytes, sizeof(spread), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        for (int k = 0; k < BYTES_SPREAD; k++) bytes += spread[k * BYTES_STRIDE];
+    }
+    if (avg_bytes) *avg_bytes = *total ? (uint32_t) (bytes / *total) : 0u;
+    return 0;
+}
+
 /* after a one-pass framing kernel: offs[n] (the total) and the mean record
  * size to the host */
 static int fetch_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total, uint32_t *avg_bytes)
 {
-    unsigned long long spread[BYTES_SPREAD * BYTES_STRIDE];
-    if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(spread, sc.bytes, sizeof(spread), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    unsigned long long bytes = 0;
-    for (int k = 0; k < BYTES_SPREAD; k++) bytes += spread[k * BYTES_STRIDE];
-    *avg_bytes = *total ? (uint32_t) (bytes / *total) : 0u;
-    return 0;
+    uint64_t seq;
+    const int r = publish_totals(sc, n, st, &seq);
+    return r ? r : collect_totals(sc, n, st, seq, total, avg_bytes);
 }
 
 /* TLSREC_RX_GROUPWALK=0: the r05 receive framing (one lane per connection
@@ -1518,21 +1613,22 @@ static bool groupwalk_env(void)
     return !(e && atoi(e) == 0);
 }
 
+/* exclusive scan of counts[0..n] -> offs, and the totals queued to the
+ * mailbox (*seq, see publish_totals): collect them with collect_totals */
+static int scan_publish(Scratch &sc, uint32_t n, hipStream_t st, uint64_t *seq)
+{
+    if (tlsrec__exclusive_scan(sc.counts, sc.offs, n + 1, (uint32_t *) sc.scan_tmp, st) != hipSuccess)
+        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+    return publish_totals(sc, n, st, seq);
+}
+
 /* exclusive scan of counts[0..n] -> offs; returns offs[n] (the total) on the
  * host, and the mean record size of the batch (0 if unknown) */
 static int scan_total(Scratch &sc, uint32_t n, hipStream_t st, uint32_t *total, uint32_t *avg_bytes = nullptr)
 {
-    unsigned long long spread[BYTES_SPREAD * BYTES_STRIDE];
-    if (tlsrec__exclusive_scan(sc.counts, sc.offs, n + 1, (uint32_t *) sc.scan_tmp, st) != hipSuccess)
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    if (hipMemcpyAsync(total, sc.offs + n, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(spread, sc.bytes, sizeof(spread), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-    unsigned long long bytes = 0;
-    for (int k = 0; k < BYTES_SPREAD; k++) bytes += spread[k * BYTES_STRIDE];
-    if (avg_bytes) *avg_bytes = *total ? (uint32_t) (bytes / *total) : 0u;
-    return 0;
+    uint64_t seq;
+    const int r = scan_publish(sc, n, st, &seq);
+    return r ? r : collect_totals(sc, n, st, seq, total, avg_bytes);
 }
 
 static inline uint32_t blocks(uint32_t n, uint32_t t) { return (n + t - 1) / t; }
@@ -1568,23 +1664,24 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
         else
             hipLaunchKernelGGL(in_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
                                (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
-        r = hipGetLastError() == hipSuccess ? scan_total(sc, nstreams, st, &total, &avg)
-                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        uint64_t seq = 0;
+        r = hipGetLastError() == hipSuccess ? scan_publish(sc, nstreams, st, &seq) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        /* the descriptors are emitted while the host collects the totals
+         * (r06; at most max_records of them: the check follows) */
+        if (r == 0 && recs) {
+            if (gw)
+                hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
+                                   streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records);
+            else
+                hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
+                                   (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records);
+            if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
+        if (r == 0) r = collect_totals(sc, nstreams, st, seq, &total, &avg);
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    if (r == 0 && total) {
-        if (!fused) {
-            if (gw)
-                hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
-                                   streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
-            else
-                hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
-                                   (const uint8_t *) arena, sc.offs, slots, cap, recs);
-            if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        }
-        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
-    }
+    if (r == 0 && total) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     if (r == 0) {
         hipLaunchKernelGGL(in_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams, sc.offs,
                            sc.counts, sc.stops, slots, cap, recs, res, sres);
@@ -1708,19 +1805,18 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     } else if (r == 0) {
         hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
                            ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
-        r = hipGetLastError() == hipSuccess ? scan_total(sc, nconns, st, &total, &avg)
-                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        uint64_t seq = 0;
+        r = hipGetLastError() == hipSuccess ? scan_publish(sc, nconns, st, &seq) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        if (r == 0 && recs) {       /* emitted while the host collects the totals (as the stream path) */
+            hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
+                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records);
+            if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        }
+        if (r == 0) r = collect_totals(sc, nconns, st, seq, &total, &avg);
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    if (r == 0 && total) {
-        if (!fused) {
-            hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs);
-            if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        }
-        if (r == 0) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
-    }
+    if (r == 0 && total) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
     if (r == 0) {
         if (fused)
             hipLaunchKernelGGL(dtls_finish_kernel<true>, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns,
