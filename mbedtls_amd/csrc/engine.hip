@@ -985,11 +985,12 @@ extern "C" int tlsrec__batch_src(const tlsrec_keytab *kt, const tlsrec_batch_rec
 
 extern "C" int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res,
                                    uint32_t n, const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec,
-                                   uint32_t avg_bytes)
+                                   uint32_t avg_bytes, int prefilled)
 {
     BatchOpt o;
     o.avg_bytes = avg_bytes;
     o.grouped = true;                    /* (the stream / DTLS layers' records, connection by connection) */
+    o.prefilled = prefilled != 0;
     return batch(kt, recs, res, n, in_arena, out_arena, 0, stream, dec, o);
 }
 

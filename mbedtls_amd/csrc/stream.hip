@@ -68,6 +68,17 @@ __device__ __forceinline__ uint4 load16(const uint8_t *p)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+/* the fail-closed result the receive emit kernels write beside each
+ * descriptor (the batch guard kernel's, ssl_msg.c:1260 / :1804): the batch
+ * then skips its guard launch */
+__device__ __forceinline__ void guard_result(tlsrec_batch_res *res)
+{
+    tlsrec_batch_res r;
+    memset(&r, 0, sizeof(r));
+    r.status = TLSREC_ERR_SSL_INTERNAL_ERROR;
+    *res = r;
+}
+
 /* TLS minor version of a loaded slot (3 or 4), 0 if the slot is unusable */
 __device__ __forceinline__ uint32_t slot_minor(const SlotState *slots, uint32_t cap, uint32_t slot)
 {
@@ -137,7 +148,8 @@ __global__ void in_count_kernel(const tlsrec_stream_in *s, uint32_t n, const uin
 }
 
 __global__ void in_emit_kernel(const tlsrec_stream_in *s, uint32_t n, const uint8_t *arena, const uint32_t *offs,
-                               const SlotState *slots, uint32_t cap, tlsrec_batch_rec *recs, uint32_t max_records)
+                               const SlotState *slots, uint32_t cap, tlsrec_batch_rec *recs, uint32_t max_records,
+                               tlsrec_batch_res *res)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -159,7 +171,10 @@ __global__ void in_emit_kernel(const tlsrec_stream_in *s, uint32_t n, const uint
         d.ver[0] = v0;
         d.ver[1] = v1;
         if (!ccs) seq++;
-        if (offs[i] + k < max_records) out[k] = d;      /* (launched before the host has checked the total) */
+        if (offs[i] + k < max_records) {                /* (launched before the host has checked the total) */
+            out[k] = d;
+            guard_result(&res[offs[i] + k]);
+        }
     });
 }
 
@@ -348,7 +363,8 @@ __global__ __launch_bounds__(RX_THREADS) void in_count_group_kernel(const tlsrec
 __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_stream_in *s, uint32_t n,
                                                                    const uint8_t *arena, const uint32_t *offs,
                                                                    const SlotState *slots, uint32_t cap,
-                                                                   tlsrec_batch_rec *recs, uint32_t max_records)
+                                                                   tlsrec_batch_rec *recs, uint32_t max_records,
+                                                                   tlsrec_batch_res *res)
 {
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
@@ -371,7 +387,10 @@ __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_
         d.type = (uint8_t) h.type;
         d.ver[0] = h.v0;
         d.ver[1] = h.v1;
-        if (offs[i] + k < max_records) out[k] = d;      /* (launched before the host has checked the total) */
+        if (offs[i] + k < max_records) {                /* (launched before the host has checked the total) */
+            out[k] = d;
+            guard_result(&res[offs[i] + k]);
+        }
     });
 }
 
@@ -467,7 +486,8 @@ __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_strea
                                                               uint32_t cap, uint32_t *counts, uint32_t *offs,
                                                               HdrStop *stops, unsigned long long *bytes,
                                                               unsigned long long *tstat, uint32_t *tctr,
-                                                              tlsrec_batch_rec *recs, uint32_t max_records)
+                                                              tlsrec_batch_rec *recs, uint32_t max_records,
+                                                              tlsrec_batch_res *res)
 {
     __shared__ uint32_t sh_tile, sh_cnt[RX_TILE], sh_off[RX_TILE];
     const int tid = threadIdx.x, lane = tid & 63, q = tid & (RG - 1), g = tid / RG;
@@ -542,6 +562,7 @@ __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_strea
             d.ver[0] = h.v0;
             d.ver[1] = h.v1;
             out[k] = d;
+            guard_result(&res[off + k]);
         });
     }
 }
@@ -967,7 +988,7 @@ __global__ void dtls_count_kernel(const tlsrec_dtls_in *c, uint32_t n, const tls
  * among them (replayed copies of a record that then fails its MAC included). */
 __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
                                  const uint8_t *arena, const uint32_t *offs, const SlotState *slots, uint32_t cap,
-                                 tlsrec_batch_rec *recs, uint32_t max_records)
+                                 tlsrec_batch_rec *recs, uint32_t max_records, tlsrec_batch_res *res)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -992,7 +1013,10 @@ __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsr
             r.cid_off[0] = 11;                         /* the CID follows the sequence number */
             const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
             r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
-            if (k < max_records) recs[k] = r;          /* (launched before the host has checked the total) */
+            if (k < max_records) {                     /* (launched before the host has checked the total) */
+                recs[k] = r;
+                guard_result(&res[k]);
+            }
             k++;
         });
     }
@@ -1010,7 +1034,7 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                                                                 uint32_t cap, uint32_t *counts, uint32_t *offs,
                                                                 unsigned long long *bytes, unsigned long long *tstat,
                                                                 uint32_t *tctr, tlsrec_batch_rec *recs,
-                                                                uint32_t max_records)
+                                                                uint32_t max_records, tlsrec_batch_res *res)
 {
     __shared__ uint32_t sh_tile, sh_wsum[DG_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1068,6 +1092,7 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                                  const uint32_t epoch = ((uint32_t) p[3] << 8) | p[4];
                                  r.slot = (epoch == ci.in_epoch && w0.fresh(p + 3)) ? ci.slot : NO_SLOT;
                                  recs[k] = r;
+                                 guard_result(&res[k]);
                              }
                              k++;
                          },
@@ -1486,6 +1511,13 @@ static bool fused_env(void)
     const char *e = getenv("TLSREC_RX_FUSED");
     return !(e && atoi(e) == 0);
 }
+/* TLSREC_RX_PREFILL=0: the receive batch runs its guard kernel although the
+ * emit kernels wrote the guard results (A/B runs) */
+static int prefill_env(void)
+{
+    const char *e = getenv("TLSREC_RX_PREFILL");
+    return (e && atoi(e) == 0) ? 0 : 1;
+}
 static bool fused_stream_env(void)
 {
     const char *e = getenv("TLSREC_RX_FUSED_STREAM");
@@ -1654,7 +1686,7 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
         /* count, scan and emit in one pass (descriptors up to max_records) */
         hipLaunchKernelGGL(in_frame_kernel, dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
                            (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
-                           sc.tctr, recs, recs ? max_records : 0u);
+                           sc.tctr, recs, (recs && res) ? max_records : 0u, res);
         r = hipGetLastError() == hipSuccess ? fetch_total(sc, nstreams, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else if (r == 0) {
@@ -1668,20 +1700,21 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
         r = hipGetLastError() == hipSuccess ? scan_publish(sc, nstreams, st, &seq) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         /* the descriptors are emitted while the host collects the totals
          * (r06; at most max_records of them: the check follows) */
-        if (r == 0 && recs) {
+        if (r == 0 && recs && res) {
             if (gw)
                 hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
-                                   streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records);
+                                   streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records,
+                                   res);
             else
                 hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
-                                   (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records);
+                                   (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records, res);
             if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         }
         if (r == 0) r = collect_totals(sc, nstreams, st, seq, &total, &avg);
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    if (r == 0 && total) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
+    if (r == 0 && total) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg, prefill_env());
     if (r == 0) {
         hipLaunchKernelGGL(in_finish_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams, sc.offs,
                            sc.counts, sc.stops, slots, cap, recs, res, sres);
@@ -1754,7 +1787,7 @@ extern "C" int tlsrec_stream_encrypt(const tlsrec_keytab *kt, const tlsrec_strea
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0)
             r = srcoff ? tlsrec__batch_src(kt, recs, res, total, in_arena, out_arena, stream, avg, srcoff)
-                       : tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
+                       : tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg, 0);
         if (srcoff) tlsrec__scratch_release(&sl);
     }
     if (r == 0) {
@@ -1799,7 +1832,7 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
         /* count, scan and emit in one pass (descriptors up to max_records) */
         hipLaunchKernelGGL(dtls_frame_kernel, dim3(tiles), dim3(DG_THREADS), 0, st, conns, nconns, dgrams, ndgrams,
                            (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.bytes, sc.tstat, sc.tctr,
-                           recs, recs ? max_records : 0u);
+                           recs, (recs && res) ? max_records : 0u, res);
         r = hipGetLastError() == hipSuccess ? fetch_total(sc, nconns, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else if (r == 0) {
@@ -1807,16 +1840,16 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
                            ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
         uint64_t seq = 0;
         r = hipGetLastError() == hipSuccess ? scan_publish(sc, nconns, st, &seq) : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
-        if (r == 0 && recs) {       /* emitted while the host collects the totals (as the stream path) */
+        if (r == 0 && recs && res) {   /* emitted while the host collects the totals (as the stream path) */
             hipLaunchKernelGGL(dtls_emit_kernel, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns, dgrams,
-                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records);
+                               ndgrams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records, res);
             if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         }
         if (r == 0) r = collect_totals(sc, nconns, st, seq, &total, &avg);
     }
     if (r == 0 && total > max_records) r = TLSREC_ERR_SSL_BUFFER_TOO_SMALL;
     if (r == 0 && total && (!recs || !res || !disp)) r = TLSREC_ERR_SSL_BAD_INPUT_DATA;
-    if (r == 0 && total) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg);
+    if (r == 0 && total) r = tlsrec__batch_sized(kt, recs, res, total, arena, arena, stream, 1, avg, prefill_env());
     if (r == 0) {
         if (fused)
             hipLaunchKernelGGL(dtls_finish_kernel<true>, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns,
@@ -1892,7 +1925,7 @@ extern "C" int tlsrec_dtls_encrypt(const tlsrec_keytab *kt, const tlsrec_stream_
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         if (r == 0)
             r = srcoff ? tlsrec__batch_src(kt, recs, res, total, in_arena, out_arena, stream, avg, srcoff)
-                       : tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg);
+                       : tlsrec__batch_sized(kt, recs, res, total, out_arena, out_arena, stream, 0, avg, 0);
         if (srcoff) tlsrec__scratch_release(&sl);
     }
     if (r == 0) {

@@ -184,9 +184,12 @@ typedef struct tlsrec_scratch_lease {
 int tlsrec__scratch_acquire(hipStream_t st, int kind, size_t bytes, tlsrec_scratch_lease *lease);
 void tlsrec__scratch_release(tlsrec_scratch_lease *lease);
 /* tlsrec_batch_encrypt (dec = 0) / _decrypt (dec = 1) with auto lanes, for a
- * caller that knows the batch's mean record size (the stream / DTLS layers) */
+ * caller that knows the batch's mean record size (the stream / DTLS layers);
+ * prefilled: the caller's kernels already wrote INTERNAL_ERROR into every
+ * result (the receive emit kernels, r06), so no guard kernel runs */
 int tlsrec__batch_sized(const tlsrec_keytab *kt, const tlsrec_batch_rec *recs, tlsrec_batch_res *res, uint32_t n,
-                        const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec, uint32_t avg_bytes);
+                        const uint8_t *in_arena, uint8_t *out_arena, void *stream, int dec, uint32_t avg_bytes,
+                        int prefilled);
 /* encrypt with each record's content read from in_arena + src_off[i] (GcmArgs::
  * src_off) and the records written to out_arena at buf_off: the stream / DTLS
  * send path without a copy of the application data.  Only for key tables of
