@@ -274,10 +274,11 @@ constexpr int RG = 16;                         /* lanes per connection */
 constexpr int RX_THREADS = 256;
 constexpr int RX_CONNS = RX_THREADS / RG;      /* connections per workgroup */
 
-/* the group's 16 bits of a wave ballot (group-uniform control flow) */
+/* the group's G bits of a wave ballot (group-uniform control flow) */
+template <int G = RG>
 __device__ __forceinline__ uint32_t group_ballot(bool b, int lane)
 {
-    return (uint32_t) (__ballot(b) >> (lane & ~(RG - 1))) & 0xffffu;
+    return (uint32_t) (__ballot(b) >> (lane & ~(G - 1))) & (uint32_t) ((1ull << G) - 1ull);
 }
 
 struct RxHdr {
@@ -310,10 +311,10 @@ __device__ __forceinline__ RxHdr rx_header(const uint8_t *base, uint32_t len, ui
 /* walk_in with the group: f(k, h, ccs_before) on the lane holding record k,
  * ccs_before = the TLS 1.3 CCS records before it (tls13 only: they take no
  * sequence number).  Returns the stop and the record count (group-uniform). */
-template <typename F>
+template <int G = RG, typename F>
 __device__ HdrStop group_walk(const uint8_t *base, uint32_t len, int lane, bool tls13, uint32_t *count, F f)
 {
-    const int q = lane & (RG - 1);
+    const int q = lane & (G - 1);
     uint32_t p = 0, k = 0, nccs = 0;
     HdrStop st = { 0, 0 };
     while (len - p >= 5) {
@@ -321,13 +322,13 @@ __device__ HdrStop group_walk(const uint8_t *base, uint32_t len, int lane, bool 
         const uint64_t at = (uint64_t) p + (uint64_t) q * (5 + dlen0);
         int32_t err;
         const RxHdr h = rx_header(base, len, at, dlen0, &err);
-        const uint32_t okm = group_ballot(h.ok, lane);
+        const uint32_t okm = group_ballot<G>(h.ok, lane);
         const uint32_t m = (uint32_t) __builtin_ctz(~okm);                 /* leading records */
         if (m == 0) {                                                      /* the header at p itself */
-            st.status = __shfl(err, lane & ~(RG - 1));
+            st.status = __shfl(err, lane & ~(G - 1));
             break;
         }
-        const uint32_t ccsm = group_ballot(h.ok && tls13 && h.type == 20, lane) & ((1u << m) - 1u);
+        const uint32_t ccsm = group_ballot<G>(h.ok && tls13 && h.type == 20, lane) & ((1u << m) - 1u);
         if ((uint32_t) q < m) f(k + q, h, nccs + (uint32_t) __builtin_popcount(ccsm & ((1u << q) - 1u)));
         nccs += (uint32_t) __builtin_popcount(ccsm);
         k += m;
@@ -338,17 +339,21 @@ __device__ HdrStop group_walk(const uint8_t *base, uint32_t len, int lane, bool 
     return st;
 }
 
+/* G lanes per connection: 16, or 4 / 8 when the caller's max_records says
+ * connections hold that few records (r06: a 4-record stream left 12 of 16
+ * lanes idle, four times the waves the walk needed) */
+template <int G>
 __global__ __launch_bounds__(RX_THREADS) void in_count_group_kernel(const tlsrec_stream_in *s, uint32_t n,
                                                                     const uint8_t *arena, uint32_t *counts,
                                                                     HdrStop *stops, unsigned long long *bytes)
 {
-    const int tid = threadIdx.x, lane = tid & 63, q = tid & (RG - 1);
-    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
+    const int tid = threadIdx.x, lane = tid & 63, q = tid & (G - 1);
+    const uint32_t i = blockIdx.x * (RX_THREADS / G) + (uint32_t) (tid / G);
     unsigned long long b = 0;
     if (i < n) {
         const tlsrec_stream_in si = s[i];
         uint32_t cnt = 0;
-        const HdrStop st = group_walk(arena + si.off, si.len, lane, false, &cnt,
+        const HdrStop st = group_walk<G>(arena + si.off, si.len, lane, false, &cnt,
                                       [&](uint32_t, const RxHdr &h, uint32_t) { b += h.dlen; });
         if (q == 0) {
             counts[i] = cnt;
@@ -360,6 +365,7 @@ __global__ __launch_bounds__(RX_THREADS) void in_count_group_kernel(const tlsrec
     wave_add_bytes(bytes, b);
 }
 
+template <int G>
 __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_stream_in *s, uint32_t n,
                                                                    const uint8_t *arena, const uint32_t *offs,
                                                                    const SlotState *slots, uint32_t cap,
@@ -367,14 +373,14 @@ __global__ __launch_bounds__(RX_THREADS) void in_emit_group_kernel(const tlsrec_
                                                                    tlsrec_batch_res *res)
 {
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t i = blockIdx.x * RX_CONNS + (uint32_t) (tid / RG);
+    const uint32_t i = blockIdx.x * (RX_THREADS / G) + (uint32_t) (tid / G);
     if (i >= n) return;
     const tlsrec_stream_in si = s[i];
     const bool tls13 = slot_minor(slots, cap, si.slot) == 4;
     const uint64_t seq0 = be64(si.in_ctr);
     tlsrec_batch_rec *out = recs + offs[i];
     uint32_t cnt;
-    group_walk(arena + si.off, si.len, lane, tls13, &cnt, [&](uint32_t k, const RxHdr &h, uint32_t ccs_before) {
+    group_walk<G>(arena + si.off, si.len, lane, tls13, &cnt, [&](uint32_t k, const RxHdr &h, uint32_t ccs_before) {
         tlsrec_batch_rec d;
         memset(&d, 0, sizeof(d));
         d.buf_off = si.off + h.pos;                     /* rec->buf = header (:3715-3716) */
@@ -476,11 +482,8 @@ __device__ __forceinline__ uint32_t claim_tile(uint32_t *ctr, uint32_t *sh)
  * the tile), so 1 M records of 4-record streams make 2 K tiles, not 16 K.
  * Writes counts, stops, offs (offs[n] = the batch's record count) and the
  * descriptors (at most max_records of them). */
-#ifndef TLSREC_RX_CH
-#define TLSREC_RX_CH 8
-#endif
-constexpr int RX_CH = TLSREC_RX_CH;
-constexpr int RX_TILE = RX_CH * RX_CONNS;
+/* G lanes per connection (as in_count_group_kernel), CH chunks per tile */
+template <int G, int CH>
 __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_stream_in *s, uint32_t n,
                                                               const uint8_t *arena, const SlotState *slots,
                                                               uint32_t cap, uint32_t *counts, uint32_t *offs,
@@ -489,24 +492,25 @@ __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_strea
                                                               tlsrec_batch_rec *recs, uint32_t max_records,
                                                               tlsrec_batch_res *res)
 {
+    constexpr int RX_CH = CH, RX_CONNS_G = RX_THREADS / G, RX_TILE = RX_CH * RX_CONNS_G;
     __shared__ uint32_t sh_tile, sh_cnt[RX_TILE], sh_off[RX_TILE];
-    const int tid = threadIdx.x, lane = tid & 63, q = tid & (RG - 1), g = tid / RG;
+    const int tid = threadIdx.x, lane = tid & 63, q = tid & (G - 1), g = tid / G;
     const uint32_t tile = claim_tile(tctr, &sh_tile);
     const uint32_t i0 = tile * RX_TILE;
     unsigned long long b = 0;
     for (int c = 0; c < RX_CH; c++) {
-        const uint32_t i = i0 + (uint32_t) (c * RX_CONNS + g);
+        const uint32_t i = i0 + (uint32_t) (c * RX_CONNS_G + g);
         uint32_t cnt = 0;
         if (i < n) {
             const tlsrec_stream_in si = s[i];
-            const HdrStop st = group_walk(arena + si.off, si.len, lane, false, &cnt,
+            const HdrStop st = group_walk<G>(arena + si.off, si.len, lane, false, &cnt,
                                           [&](uint32_t, const RxHdr &h, uint32_t) { b += h.dlen; });
             if (q == 0) {
                 counts[i] = cnt;
                 stops[i] = st;
             }
         }
-        if (q == 0) sh_cnt[c * RX_CONNS + g] = cnt;
+        if (q == 0) sh_cnt[c * RX_CONNS_G + g] = cnt;
     }
     wave_add_bytes(bytes, b);
     __syncthreads();
@@ -539,15 +543,15 @@ __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_strea
     }
     if (!recs) return;
     for (int c = 0; c < RX_CH; c++) {
-        const uint32_t i = i0 + (uint32_t) (c * RX_CONNS + g);
-        const uint32_t cnt = sh_cnt[c * RX_CONNS + g], off = sh_off[c * RX_CONNS + g];
+        const uint32_t i = i0 + (uint32_t) (c * RX_CONNS_G + g);
+        const uint32_t cnt = sh_cnt[c * RX_CONNS_G + g], off = sh_off[c * RX_CONNS_G + g];
         if (i >= n || !cnt) continue;                     /* group-uniform */
         const tlsrec_stream_in si = s[i];
         const bool tls13 = slot_minor(slots, cap, si.slot) == 4;
         const uint64_t seq0 = be64(si.in_ctr);
         tlsrec_batch_rec *out = recs + off;
         uint32_t c2;
-        group_walk(arena + si.off, si.len, lane, tls13, &c2, [&](uint32_t k, const RxHdr &h, uint32_t ccs_before) {
+        group_walk<G>(arena + si.off, si.len, lane, tls13, &c2, [&](uint32_t k, const RxHdr &h, uint32_t ccs_before) {
             if (off + k >= max_records) return;
             tlsrec_batch_rec d;
             memset(&d, 0, sizeof(d));
@@ -1518,6 +1522,37 @@ static int prefill_env(void)
     const char *e = getenv("TLSREC_RX_PREFILL");
     return (e && atoi(e) == 0) ? 0 : 1;
 }
+/* lanes per connection of the receive header walk: the records a
+ * connection can hold on average by the caller's capacity (max_records /
+ * connections) -- 4, 8 or 16; TLSREC_RX_RG forces one */
+static int rx_group(uint32_t n, uint32_t max_records)
+{
+    const char *e = getenv("TLSREC_RX_RG");
+    if (e) {
+        const int g = atoi(e);
+        if (g == 4 || g == 8 || g == 16) return g;
+    }
+    const uint64_t per = n ? ((uint64_t) max_records + n - 1) / n : 16;
+    return per <= 4 ? 4 : (per <= 8 ? 8 : 16);
+}
+
+template <int G>
+static void launch_rx_count(uint32_t n, hipStream_t st, const tlsrec_stream_in *s, const uint8_t *arena,
+                            uint32_t *counts, HdrStop *stops, unsigned long long *bytes)
+{
+    hipLaunchKernelGGL(in_count_group_kernel<G>, dim3((n + 1 + RX_THREADS / G - 1) / (RX_THREADS / G)),
+                       dim3(RX_THREADS), 0, st, s, n, arena, counts, stops, bytes);
+}
+
+template <int G>
+static void launch_rx_emit(uint32_t n, hipStream_t st, const tlsrec_stream_in *s, const uint8_t *arena,
+                           const uint32_t *offs, const SlotState *slots, uint32_t cap, tlsrec_batch_rec *recs,
+                           uint32_t max_records, tlsrec_batch_res *res)
+{
+    hipLaunchKernelGGL(in_emit_group_kernel<G>, dim3((n + RX_THREADS / G - 1) / (RX_THREADS / G)), dim3(RX_THREADS),
+                       0, st, s, n, arena, offs, slots, cap, recs, max_records, res);
+}
+
 static bool fused_stream_env(void)
 {
     const char *e = getenv("TLSREC_RX_FUSED_STREAM");
@@ -1678,22 +1713,40 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
     const uint32_t cap = tlsrec_keytab_capacity(kt);
     Scratch sc;
     const bool fused = fused_stream_env() && groupwalk_env();
-    const uint32_t tiles = blocks(nstreams, RX_TILE);
+    /* one pass: G lanes per connection, tiles of 512 connections (G = 4:
+     * two chunks of 128) or 128 (G = 16: eight chunks of 16) */
+    const int frg = rx_group(nstreams, max_records);
+    const uint32_t ftile = frg == 4 ? 2u * 64u : (frg == 8 ? 4u * 32u : 8u * 16u);
+    const uint32_t tiles = blocks(nstreams, ftile);
     int r = scratch_alloc(sc, nstreams, st, fused ? tiles : 0u);
     uint32_t total = 0, avg = 0;
     const bool gw = groupwalk_env();
     if (r == 0 && fused) {
         /* count, scan and emit in one pass (descriptors up to max_records) */
-        hipLaunchKernelGGL(in_frame_kernel, dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
-                           (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
-                           sc.tctr, recs, (recs && res) ? max_records : 0u, res);
+        if (frg == 4)
+            hipLaunchKernelGGL((in_frame_kernel<4, 2>), dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
+                               (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
+                               sc.tctr, recs, (recs && res) ? max_records : 0u, res);
+        else if (frg == 8)
+            hipLaunchKernelGGL((in_frame_kernel<8, 4>), dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
+                               (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
+                               sc.tctr, recs, (recs && res) ? max_records : 0u, res);
+        else
+            hipLaunchKernelGGL((in_frame_kernel<16, 8>), dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
+                               (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
+                               sc.tctr, recs, (recs && res) ? max_records : 0u, res);
         r = hipGetLastError() == hipSuccess ? fetch_total(sc, nstreams, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else if (r == 0) {
-        if (gw)
-            hipLaunchKernelGGL(in_count_group_kernel, dim3(blocks(nstreams + 1, RX_CONNS)), dim3(RX_THREADS), 0, st,
-                               streams, nstreams, (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
-        else
+        const int rg = rx_group(nstreams, max_records);
+        if (gw) {
+            if (rg == 4)
+                launch_rx_count<4>(nstreams, st, streams, (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
+            else if (rg == 8)
+                launch_rx_count<8>(nstreams, st, streams, (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
+            else
+                launch_rx_count<16>(nstreams, st, streams, (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
+        } else
             hipLaunchKernelGGL(in_count_kernel, dim3(blocks(nstreams + 1, 256)), dim3(256), 0, st, streams, nstreams,
                                (const uint8_t *) arena, sc.counts, sc.stops, sc.bytes);
         uint64_t seq = 0;
@@ -1701,10 +1754,15 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
         /* the descriptors are emitted while the host collects the totals
          * (r06; at most max_records of them: the check follows) */
         if (r == 0 && recs && res) {
-            if (gw)
-                hipLaunchKernelGGL(in_emit_group_kernel, dim3(blocks(nstreams, RX_CONNS)), dim3(RX_THREADS), 0, st,
-                                   streams, nstreams, (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records,
-                                   res);
+            if (gw && rg == 4)
+                launch_rx_emit<4>(nstreams, st, streams, (const uint8_t *) arena, sc.offs, slots, cap, recs,
+                                  max_records, res);
+            else if (gw && rg == 8)
+                launch_rx_emit<8>(nstreams, st, streams, (const uint8_t *) arena, sc.offs, slots, cap, recs,
+                                  max_records, res);
+            else if (gw)
+                launch_rx_emit<16>(nstreams, st, streams, (const uint8_t *) arena, sc.offs, slots, cap, recs,
+                                   max_records, res);
             else
                 hipLaunchKernelGGL(in_emit_kernel, dim3(blocks(nstreams, 256)), dim3(256), 0, st, streams, nstreams,
                                    (const uint8_t *) arena, sc.offs, slots, cap, recs, max_records, res);

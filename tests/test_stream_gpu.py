@@ -154,15 +154,17 @@ def test_encrypt_then_decrypt_many_connections():
     c.close()
 
 
-FRAMINGS = [("1", "1", "1"), ("1", "1", "0"), ("0", "0", "0")]
-FRAMING_IDS = ["one-pass", "groupwalk-3-kernels", "r05-framing"]
+FRAMINGS = [("1", "1", "1", "16"), ("1", "1", "0", "16"), ("1", "1", "0", "8"), ("1", "1", "0", "4"),
+            ("0", "0", "0", "16")]
+FRAMING_IDS = ["one-pass", "groupwalk-16", "groupwalk-8", "groupwalk-4", "r05-framing"]
 
 
 def _framing(monkeypatch, fr):
-    gw, grouped, fused = fr
+    gw, grouped, fused, rg = fr
     monkeypatch.setenv("TLSREC_RX_GROUPWALK", gw)       # the r06 lane-group walks or the r05 one-lane walks,
     monkeypatch.setenv("TLSREC_GROUPED", grouped)       # with and without the bucket pass,
-    monkeypatch.setenv("TLSREC_RX_FUSED_STREAM", fused) # count / scan / emit as one pass (look-back) or three kernels
+    monkeypatch.setenv("TLSREC_RX_FUSED_STREAM", fused) # count / scan / emit as one pass (look-back) or three kernels,
+    monkeypatch.setenv("TLSREC_RX_RG", rg)              # 16, 8 or 4 lanes per connection in the walk
 
 
 @pytest.mark.parametrize("fr", FRAMINGS, ids=FRAMING_IDS)
