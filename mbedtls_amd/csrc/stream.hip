@@ -101,6 +101,11 @@ __device__ __forceinline__ void wave_add_bytes(unsigned long long *sum, unsigned
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(sum + (blockIdx.x % BYTES_SPREAD) * BYTES_STRIDE, v);
 }
 
+/* the host-mapped mailbox of the batch totals (totals_kernel, r06) */
+struct TotMbox {
+    uint64_t total, bytes, seq, pad;
+};
+
 /* ---------------- receive ---------------------------------------------- */
 struct HdrStop {
     int32_t status;           /* header error that stopped the walk, 0 = out of bytes */
@@ -429,17 +434,20 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
  * tiles per round trip (64 per round, one wave, measured 234 us for 16 K
  * tiles of a 1 M-record stream batch). */
 template <int NT>
-__device__ uint32_t tile_lookback(unsigned long long *status, uint32_t tile, uint32_t agg)
+__device__ uint32_t tile_lookback(unsigned long long *status, uint32_t tile, uint32_t agg, uint32_t aux = 0,
+                                  uint32_t *aux_excl = nullptr)
 {
-    __shared__ uint32_t sh_fp[NT / 64], sh_sum[NT / 64];
+    /* status word: flag (bits 62-63) | records (bits 32-61) | aux (bits 0-31,
+     * the DTLS kernel's bytes in 64-B units): both prefix sums travel in one
+     * atomic word, so no fence orders them with other memory */
+    __shared__ uint32_t sh_fp[NT / 64], sh_sum[NT / 64], sh_aux[NT / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0)
-        __hip_atomic_store(status + tile, (tile == 0 ? TS_INC : TS_AGG) | agg, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (tile == 0) return 0;
-    uint32_t excl = 0;
+        __hip_atomic_store(status + tile, (tile == 0 ? TS_INC : TS_AGG) | ((unsigned long long) agg << 32) | aux,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0, xaux = 0;
     int64_t base = (int64_t) tile - 1;
-    for (;;) {
+    for (; tile != 0;) {
         const int64_t t = base - tid;
         const unsigned long long v = t >= 0 ? __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                             : TS_INC;   /* before tile 0: an inclusive prefix of 0 */
@@ -454,17 +462,27 @@ __device__ uint32_t tile_lookback(unsigned long long *status, uint32_t tile, uin
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        const uint32_t ws = wave_sum_u32((uint32_t) tid <= fp ? (uint32_t) v : 0u);
-        if (lane == 0) sh_sum[wave] = ws;
+        const bool in = (uint32_t) tid <= fp;
+        const uint32_t ws = wave_sum_u32(in ? (uint32_t) (v >> 32) & 0x3fffffffu : 0u);
+        const uint32_t wa = wave_sum_u32(in ? (uint32_t) v : 0u);
+        if (lane == 0) {
+            sh_sum[wave] = ws;
+            sh_aux[wave] = wa;
+        }
         __syncthreads();
 #pragma unroll
-        for (int w = 0; w < NT / 64; w++) excl += sh_sum[w];
+        for (int w = 0; w < NT / 64; w++) {
+            excl += sh_sum[w];
+            xaux += sh_aux[w];
+        }
         __syncthreads();                                 /* sh_fp / sh_sum reused next round */
         if (fp < (uint32_t) NT) break;
         base -= NT;
     }
-    if (tid == 0)
-        __hip_atomic_store(status + tile, TS_INC | (uint32_t) (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && tile != 0)
+        __hip_atomic_store(status + tile, TS_INC | ((unsigned long long) (excl + agg) << 32) | (uint32_t) (xaux + aux),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (aux_excl) *aux_excl = xaux;
     return excl;
 }
 
@@ -1038,7 +1056,8 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                                                                 uint32_t cap, uint32_t *counts, uint32_t *offs,
                                                                 unsigned long long *bytes, unsigned long long *tstat,
                                                                 uint32_t *tctr, tlsrec_batch_rec *recs,
-                                                                uint32_t max_records, tlsrec_batch_res *res)
+                                                                uint32_t max_records, tlsrec_batch_res *res,
+                                                                TotMbox *mb, uint64_t mseq)
 {
     __shared__ uint32_t sh_tile, sh_wsum[DG_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1061,6 +1080,14 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
         counts[i] = cnt;
     }
     wave_add_bytes(bytes, b);
+    /* the tile's bytes (64-B units) ride in the look-back's status word */
+    __shared__ unsigned long long sh_b[DG_THREADS / 64];
+    {
+        unsigned long long wb = b;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) wb += __shfl_xor(wb, o);
+        if (lane == 0) sh_b[wave] = wb;
+    }
     /* the tile's exclusive scan: within waves by shuffles, across waves in LDS */
     uint32_t incl = cnt;
 #pragma unroll
@@ -1070,11 +1097,24 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
     }
     if (lane == 63) sh_wsum[wave] = incl;
     __syncthreads();
-    const uint32_t excl = tile_lookback<DG_THREADS>(tstat, tile, sh_wsum[0] + sh_wsum[1] + sh_wsum[2] + sh_wsum[3]);
+    const uint32_t agg = sh_wsum[0] + sh_wsum[1] + sh_wsum[2] + sh_wsum[3];
+    const uint32_t aux = (uint32_t) ((sh_b[0] + sh_b[1] + sh_b[2] + sh_b[3]) >> 6);
+    uint32_t aux_excl = 0;
+    const uint32_t excl = tile_lookback<DG_THREADS>(tstat, tile, agg, aux, &aux_excl);
     uint32_t off = excl + incl - cnt;
     for (int w = 0; w < wave; w++) off += sh_wsum[w];
     if (i < n) offs[i] = off;
     if (i + 1 == n) offs[n] = off + cnt;                  /* the scan's sentinel: the batch total */
+    /* the last tile's prefix covers every tile: it hands the totals to the
+     * host now, while the other tiles still emit (r06; the byte total in
+     * 64-B units per tile, exact enough for the mean record size that steers
+     * the AEAD launch; mb = null: the host reads the totals afterwards) */
+    if (mb && tile == gridDim.x - 1 && tid == 0) {
+        mb->total = excl + agg;
+        mb->bytes = (unsigned long long) (aux_excl + aux) << 6;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(&mb->seq, mseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (!ok || !cnt || !recs) return;
     const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
     uint32_t k = off;
@@ -1467,10 +1507,6 @@ __global__ void dtls_out_finish_kernel(const tlsrec_stream_out *s, uint32_t n, c
  * descriptor emit) still run.  (The copies cost 4 us each with a 20 us gap
  * between them, and the launch after the synchronize another 30 us, per
  * receive call; profiles/r06/ab/mailbox/.) */
-struct TotMbox {
-    uint64_t total, bytes, seq, pad;
-};
-
 __global__ void __launch_bounds__(64) totals_kernel(const uint32_t *total_p, const unsigned long long *spread,
                                                     TotMbox *mb, uint64_t seq)
 {
@@ -1607,27 +1643,39 @@ static bool mailbox_env(void)
     return !(e && atoi(e) == 0);
 }
 
-/* queue the totals kernel: offs[n] and the byte counters to the mailbox;
- * *seq = the value collect_totals waits for (0: the copy path, nothing queued) */
-static int publish_totals(Scratch &sc, uint32_t n, hipStream_t st, uint64_t *seq)
+/* the calling thread's mailbox (device pointer) and the next sequence
+ * number; null with the copy path (TLSREC_RX_MAILBOX=0) or no mailbox */
+static TotMbox *mailbox_next(uint64_t *seq)
 {
     *seq = 0;
-    if (!mailbox_env()) return 0;
+    if (!mailbox_env()) return nullptr;
     Mailbox &m = t_mbox;
     if (!m.h) {
         void *h = nullptr, *d = nullptr;
         if (hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
-            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+            return nullptr;
         memset(h, 0, 256);
         if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
             hipHostFree(h);
-            return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+            return nullptr;
         }
         m.h = (TotMbox *) h;
         m.d = (TotMbox *) d;
     }
     *seq = ++m.seq;
-    hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, st, sc.offs + n, sc.bytes, m.d, *seq);
+    return m.d;
+}
+
+/* queue the totals kernel: offs[n] and the byte counters to the mailbox;
+ * *seq = the value collect_totals waits for (0: the copy path, nothing queued) */
+static int publish_totals(Scratch &sc, uint32_t n, hipStream_t st, uint64_t *seq)
+{
+    TotMbox *mb = mailbox_next(seq);
+    if (!mb) {
+        *seq = 0;
+        return 0;
+    }
+    hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, st, sc.offs + n, sc.bytes, mb, *seq);
     return hipGetLastError() == hipSuccess ? 0 : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
 }
 
@@ -1888,11 +1936,19 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     uint32_t total = 0, avg = 0;
     if (r == 0 && fused) {
         /* count, scan and emit in one pass (descriptors up to max_records) */
+        uint64_t seq = 0;
+#ifndef TLSREC_DTLS_LASTTILE_MB
+#define TLSREC_DTLS_LASTTILE_MB 1
+#endif
+        /* the frame kernel's last tile writes the totals into the mailbox
+         * (r06; 0 in A/B builds: the totals kernel after the frame kernel) */
+        TotMbox *mb = TLSREC_DTLS_LASTTILE_MB ? mailbox_next(&seq) : nullptr;
         hipLaunchKernelGGL(dtls_frame_kernel, dim3(tiles), dim3(DG_THREADS), 0, st, conns, nconns, dgrams, ndgrams,
                            (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.bytes, sc.tstat, sc.tctr,
-                           recs, (recs && res) ? max_records : 0u, res);
-        r = hipGetLastError() == hipSuccess ? fetch_total(sc, nconns, st, &total, &avg)
-                                            : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+                           recs, (recs && res) ? max_records : 0u, res, mb, seq);
+        if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
+        else if (mb) r = collect_totals(sc, nconns, st, seq, &total, &avg);
+        else r = fetch_total(sc, nconns, st, &total, &avg);
     } else if (r == 0) {
         hipLaunchKernelGGL(dtls_count_kernel, dim3(blocks(nconns + 1, 256)), dim3(256), 0, st, conns, nconns, dgrams,
                            ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.bytes);
