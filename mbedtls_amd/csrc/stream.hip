@@ -24,6 +24,7 @@
  * plaintext into its record slot (one wave per record).
  */
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -1695,6 +1696,9 @@ static int collect_totals(Scratch &sc, uint32_t n, hipStream_t st, uint64_t seq,
                 if (q == hipSuccess && __atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) != seq)
                     return TLSREC_ERR_SSL_HW_ACCEL_FAILED;
             }
+            /* queued behind long work on the stream: stop holding the CPU
+             * after ~100 us of spinning */
+            if (it > 65536) sched_yield();
         }
         *total = (uint32_t) __atomic_load_n(&h->total, __ATOMIC_RELAXED);
         bytes = __atomic_load_n(&h->bytes, __ATOMIC_RELAXED);
