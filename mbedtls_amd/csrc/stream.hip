@@ -501,9 +501,13 @@ __device__ __forceinline__ uint32_t claim_tile(uint32_t *ctr, uint32_t *sh)
  * the tile), so 1 M records of 4-record streams make 2 K tiles, not 16 K.
  * Writes counts, stops, offs (offs[n] = the batch's record count) and the
  * descriptors (at most max_records of them). */
-/* G lanes per connection (as in_count_group_kernel), CH chunks per tile */
-template <int G, int CH>
-__global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_stream_in *s, uint32_t n,
+/* G lanes per connection (as in_count_group_kernel), CH chunks per tile, NT
+ * threads per workgroup */
+#ifndef TLSREC_RX_FRAME_NT
+#define TLSREC_RX_FRAME_NT 512
+#endif
+template <int G, int CH, int NT>
+__global__ __launch_bounds__(NT) void in_frame_kernel(const tlsrec_stream_in *s, uint32_t n,
                                                               const uint8_t *arena, const SlotState *slots,
                                                               uint32_t cap, uint32_t *counts, uint32_t *offs,
                                                               HdrStop *stops, unsigned long long *bytes,
@@ -511,7 +515,8 @@ __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_strea
                                                               tlsrec_batch_rec *recs, uint32_t max_records,
                                                               tlsrec_batch_res *res)
 {
-    constexpr int RX_CH = CH, RX_CONNS_G = RX_THREADS / G, RX_TILE = RX_CH * RX_CONNS_G;
+    constexpr int RX_CH = CH, RX_CONNS_G = NT / G, RX_TILE = RX_CH * RX_CONNS_G;
+    static_assert(RX_TILE <= NT && RX_TILE <= 128 * 2, "tile scan");
     __shared__ uint32_t sh_tile, sh_cnt[RX_TILE], sh_off[RX_TILE];
     const int tid = threadIdx.x, lane = tid & 63, q = tid & (G - 1), g = tid / G;
     const uint32_t tile = claim_tile(tctr, &sh_tile);
@@ -551,7 +556,7 @@ __global__ __launch_bounds__(RX_THREADS) void in_frame_kernel(const tlsrec_strea
     for (int w = 0; w < RX_TW; w++) agg += sh_off[w];
     uint32_t wpre = 0;
     for (int w = 0; w < (tid >> 6) && w < RX_TW; w++) wpre += sh_off[w];
-    const uint32_t excl = tile_lookback<RX_THREADS>(tstat, tile, agg);
+    const uint32_t excl = tile_lookback<NT>(tstat, tile, agg);
     __syncthreads();                                      /* every thread has read the wave totals */
     if (tid < RX_TILE) sh_off[tid] = excl + wpre + incl - sh_cnt[tid];
     __syncthreads();
@@ -1775,18 +1780,21 @@ extern "C" int tlsrec_stream_decrypt(const tlsrec_keytab *kt, const tlsrec_strea
     const bool gw = groupwalk_env();
     if (r == 0 && fused) {
         /* count, scan and emit in one pass (descriptors up to max_records) */
+        /* tiles of 128 connections: one chunk of 128 at 4 lanes (512 threads),
+         * or chunks of 64 / 32 at 8 / 16 lanes */
+        constexpr int FNT = TLSREC_RX_FRAME_NT;
         if (frg == 4)
-            hipLaunchKernelGGL((in_frame_kernel<4, 2>), dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
+            hipLaunchKernelGGL((in_frame_kernel<4, 512 / FNT, FNT>), dim3(tiles), dim3(FNT), 0, st, streams, nstreams,
                                (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
                                sc.tctr, recs, (recs && res) ? max_records : 0u, res);
         else if (frg == 8)
-            hipLaunchKernelGGL((in_frame_kernel<8, 4>), dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
-                               (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
-                               sc.tctr, recs, (recs && res) ? max_records : 0u, res);
+            hipLaunchKernelGGL((in_frame_kernel<8, 1024 / FNT, FNT>), dim3(tiles), dim3(FNT), 0, st, streams,
+                               nstreams, (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes,
+                               sc.tstat, sc.tctr, recs, (recs && res) ? max_records : 0u, res);
         else
-            hipLaunchKernelGGL((in_frame_kernel<16, 8>), dim3(tiles), dim3(RX_THREADS), 0, st, streams, nstreams,
-                               (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes, sc.tstat,
-                               sc.tctr, recs, (recs && res) ? max_records : 0u, res);
+            hipLaunchKernelGGL((in_frame_kernel<16, 2048 / FNT, FNT>), dim3(tiles), dim3(FNT), 0, st, streams,
+                               nstreams, (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.stops, sc.bytes,
+                               sc.tstat, sc.tctr, recs, (recs && res) ? max_records : 0u, res);
         r = hipGetLastError() == hipSuccess ? fetch_total(sc, nstreams, st, &total, &avg)
                                             : TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     } else if (r == 0) {
