@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Markdown table of one round's bench rows (the JSON lines tools/gpu_r06.sh
 rows writes, copied to profiles/<round>/rows/):
-    python profiles/rows_table.py profiles/r05/rows"""
+    python profiles/rows_table.py profiles/r06/rows"""
 import glob
 import json
 import os

@@ -123,7 +123,7 @@ def test_pair_small_lane_model():
     """the paired passes' lanes per record for small records (engine.hip
     tlsrec__gcm_pair_small_l, a host function: no GPU needed) -- the round-fill
     model picks the lane count that measured best at every records-per-key
-    point of the r05 sweep (profiles/r05/small_rpk/)"""
+    point of the r05 sweep (profiles/archive/r05/small_rpk/)"""
     import ctypes
     from mbedtls_amd import _abi
     f = _abi.load().tlsrec__gcm_pair_small_l
