@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                                                                 unsigned long long *bytes, unsigned long long *tstat,
                                                                 uint32_t *tctr, tlsrec_batch_rec *recs,
                                                                 uint32_t max_records, tlsrec_batch_res *res,
-                                                                TotMbox *mb, uint64_t mseq)
+                                                                TotMbox *mb, uint64_t mseq, uint32_t *dgst)
 {
     __shared__ uint32_t sh_tile, sh_wsum[DG_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1121,12 +1121,16 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __hip_atomic_store(&mb->seq, mseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (!ok || !cnt || !recs) return;
+    if (!ok) return;
+    /* the emit walk also leaves each datagram's summary for the in-order
+     * finish -- its records and how its walk stopped (dgst[d] = records |
+     * stop << 24) -- so the finish reads 4 B per datagram and the records'
+     * descriptors instead of the datagrams' header lines again (r06) */
     const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
-    uint32_t k = off;
+    uint32_t k = off, d = ci.first_dgram, kd = off;
     dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
                          [&](uint64_t base, const DtlsHdr &h, const uint8_t *p) {
-                             if (k < max_records) {
+                             if (recs && k < max_records) {
                                  tlsrec_batch_rec r;
                                  memset(&r, 0, sizeof(r));
                                  r.buf_off = base + h.pos;                  /* rec->buf = the header (:3715-3716) */
@@ -1146,7 +1150,12 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                              }
                              k++;
                          },
-                         [](int32_t) {}, [] {});
+                         [&](int32_t stop) {
+                             if (dgst) dgst[d] = (k - kd) | ((uint32_t) stop << 24);
+                             d++;
+                             kd = k;
+                         },
+                         [] {});
 }
 
 /* ssl_get_next_record over each connection's datagrams in arrival order, on
@@ -1175,7 +1184,8 @@ template <bool PRE>
 __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsrec_dgram *dg, uint32_t ndg,
                                 uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
                                 const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
-                                const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
+                                const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres,
+                                const uint32_t *dgst)
 {
     const tlsrec_dtls_in ci = c[i];
     ReplayWindow w = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
@@ -1290,6 +1300,40 @@ __device__ void dtls_finish_one(uint32_t i, const tlsrec_dtls_in *c, const tlsre
     };
     if (!dtls_conn_ok(ci, ndg, slots, cap)) {
         st = TLSREC_ERR_SSL_BAD_INPUT_DATA;
+    } else if (PRE && dgst) {
+        /* the frame kernel's datagram summaries; each record's epoch and
+         * sequence number from its descriptor (ctr, :3683-3687), loaded with
+         * its slot and result DGF_U records at a time into the queue */
+        uint32_t kq = first;
+        uint64_t qc[DGF_U];
+        auto refill = [&]() __attribute__((always_inline)) {
+            kb = kq;
+#pragma unroll
+            for (int u = 0; u < DGF_U; u++) {
+                if (kq + u < first + nrec) {
+                    const uint4 a = load16(reinterpret_cast<const uint8_t *>(recs + kq + u) + 16);   /* data_len, slot, ctr */
+                    ps[u] = a.y;
+                    qc[u] = (uint64_t) a.z | ((uint64_t) a.w << 32);
+                    pr[u] = res[kq + u];
+                }
+            }
+            kq += DGF_U;
+        };
+        for (uint32_t d = ci.first_dgram; d < ci.first_dgram + ci.ndgram; d++) {
+            const uint32_t u = dgst[d];
+            for (uint32_t r = 0; r < (u & 0xffffffu); r++) {
+                if (k - kb >= (uint32_t) DGF_U || k == first) refill();
+                const uint64_t c8 = qc[0];       /* ctr bytes 0..7, little-endian */
+#pragma unroll
+                for (int v = 0; v + 1 < DGF_U; v++) qc[v] = qc[v + 1];
+                const uint32_t epoch = ((uint32_t) (c8 & 0xff) << 8) | (uint32_t) ((c8 >> 8) & 0xff);
+                uint64_t seq = 0;
+#pragma unroll
+                for (int b = 2; b < 8; b++) seq = (seq << 8) | ((c8 >> (8 * b)) & 0xff);
+                onrec(epoch, seq);
+            }
+            ondgram((int32_t) (u >> 24));
+        }
     } else if constexpr (PRE) {
         dtls_conn_walk<DGF_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
                              [&](uint64_t, const DtlsHdr &, const uint8_t *p) { hdr_rec(p); }, ondgram, prefetch);
@@ -1317,10 +1361,11 @@ template <bool PRE>
 __global__ void dtls_finish_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsrec_dgram *dg, uint32_t ndg,
                                    uint8_t *arena, const uint32_t *offs, const uint32_t *counts,
                                    const SlotState *slots, uint32_t cap, const tlsrec_batch_rec *recs,
-                                   const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres)
+                                   const tlsrec_batch_res *res, int32_t *disp, tlsrec_dtls_in_res *cres,
+                                   const uint32_t *dgst)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dtls_finish_one<PRE>(i, c, dg, ndg, arena, offs, counts, slots, cap, recs, res, disp, cres);
+    if (i < n) dtls_finish_one<PRE>(i, c, dg, ndg, arena, offs, counts, slots, cap, recs, res, disp, cres, dgst);
 }
 
 /* send: one record per datagram */
@@ -1946,6 +1991,8 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     const uint32_t tiles = blocks(nconns, DG_THREADS);
     int r = scratch_alloc(sc, nconns, st, fused ? tiles : 0u);
     uint32_t total = 0, avg = 0;
+    tlsrec_scratch_lease dgl = { nullptr, nullptr };
+    uint32_t *dgst = nullptr;
     if (r == 0 && fused) {
         /* count, scan and emit in one pass (descriptors up to max_records) */
         uint64_t seq = 0;
@@ -1955,9 +2002,11 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
         /* the frame kernel's last tile writes the totals into the mailbox
          * (r06; 0 in A/B builds: the totals kernel after the frame kernel) */
         TotMbox *mb = TLSREC_DTLS_LASTTILE_MB ? mailbox_next(&seq) : nullptr;
+        /* the datagram summaries for the finish (none: it walks the headers) */
+        if (ndgrams && tlsrec__scratch_acquire(st, 2, (size_t) ndgrams * 4, &dgl) == 0) dgst = (uint32_t *) dgl.mem;
         hipLaunchKernelGGL(dtls_frame_kernel, dim3(tiles), dim3(DG_THREADS), 0, st, conns, nconns, dgrams, ndgrams,
                            (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.bytes, sc.tstat, sc.tctr,
-                           recs, (recs && res) ? max_records : 0u, res, mb, seq);
+                           recs, (recs && res) ? max_records : 0u, res, mb, seq, dgst);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         else if (mb) r = collect_totals(sc, nconns, st, seq, &total, &avg);
         else r = fetch_total(sc, nconns, st, &total, &avg);
@@ -1979,12 +2028,14 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
     if (r == 0) {
         if (fused)
             hipLaunchKernelGGL(dtls_finish_kernel<true>, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns,
-                               dgrams, ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
+                               dgrams, ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres, dgst);
         else
             hipLaunchKernelGGL(dtls_finish_kernel<false>, dim3(blocks(nconns, 256)), dim3(256), 0, st, conns, nconns,
-                               dgrams, ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres);
+                               dgrams, ndgrams, arena, sc.offs, sc.counts, slots, cap, recs, res, disp, cres,
+                               (const uint32_t *) nullptr);
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
     }
+    if (dgl.mem) tlsrec__scratch_release(&dgl);
     tlsrec__scratch_release(&sc.lease);
     if (r == 0 && nrecords) *nrecords = total;
     return r;
