@@ -1052,10 +1052,13 @@ __global__ void dtls_emit_kernel(const tlsrec_dtls_in *c, uint32_t n, const tlsr
 
 /* dtls_count_kernel + scan + dtls_emit_kernel in one pass (in_frame_kernel's
  * tile look-back), one lane per connection, DG_THREADS connections per tile,
- * datagrams walked DG_U at a time; the emit walk reads the headers the count
- * walk has just brought into L2.  Descriptors beyond max_records are not
- * written. */
+ * datagrams walked DG_U at a time.  Descriptors beyond max_records are not
+ * written.  S > 0: the count walk keeps each lane's first S records' header
+ * fields in LDS (24 B each) and the emit builds those descriptors from there,
+ * without a second walk over the header lines (r06; a connection with more
+ * records walks again). */
 constexpr int DG_THREADS = 256;
+template <int S>
 __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtls_in *c, uint32_t n,
                                                                 const tlsrec_dgram *dg, uint32_t ndg,
                                                                 const uint8_t *arena, const SlotState *slots,
@@ -1066,6 +1069,8 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                                                                 TotMbox *mb, uint64_t mseq, uint32_t *dgst)
 {
     __shared__ uint32_t sh_tile, sh_wsum[DG_THREADS / 64];
+    constexpr int SS = S > 0 ? S : 1;
+    __shared__ uint2 st_off[SS][DG_THREADS], st_ctr[SS][DG_THREADS], st_meta[SS][DG_THREADS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t tile = claim_tile(tctr, &sh_tile);
     const uint32_t i = tile * DG_THREADS + (uint32_t) tid;
@@ -1076,13 +1081,30 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
     if (i < n) {
         ci = c[i];
         ok = dtls_conn_ok(ci, ndg, slots, cap);
-        if (ok)
+        if (ok) {
+            uint32_t d = ci.first_dgram, kd = 0;
             dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
-                                 [&](uint64_t, const DtlsHdr &h, const uint8_t *) {
+                                 [&](uint64_t base, const DtlsHdr &h, const uint8_t *p) {
+                                     if (S > 0 && cnt < (uint32_t) S) {
+                                         const uint64_t bo = base + h.pos;
+                                         st_off[cnt][tid] = make_uint2((uint32_t) bo, (uint32_t) (bo >> 32));
+                                         st_ctr[cnt][tid] = make_uint2(
+                                             p[3] | (uint32_t) p[4] << 8 | (uint32_t) p[5] << 16 | (uint32_t) p[6] << 24,
+                                             p[7] | (uint32_t) p[8] << 8 | (uint32_t) p[9] << 16 | (uint32_t) p[10] << 24);
+                                         st_meta[cnt][tid] = make_uint2(h.data_len | h.data_offset << 16,
+                                                                        p[0] | (uint32_t) p[1] << 8 | (uint32_t) p[2] << 16 |
+                                                                            h.cid_len << 24);
+                                     }
                                      cnt++;
                                      b += h.data_len;
                                  },
-                                 [](int32_t) {}, [] {});
+                                 [&](int32_t stop) {         /* S > 0: the datagram summaries here */
+                                     if (S > 0 && dgst) dgst[d] = (cnt - kd) | ((uint32_t) stop << 24);
+                                     d++;
+                                     kd = cnt;
+                                 },
+                                 [] {});
+        }
         counts[i] = cnt;
     }
     wave_add_bytes(bytes, b);
@@ -1127,6 +1149,32 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
      * stop << 24) -- so the finish reads 4 B per datagram and the records'
      * descriptors instead of the datagrams' header lines again (r06) */
     const ReplayWindow w0 = { ci.window_top, ci.window, (ci.flags & TLSREC_DTLS_ANTI_REPLAY) != 0 };
+    if (S > 0 && cnt <= (uint32_t) S) {             /* every record's fields are in LDS (this lane's own) */
+        if (!recs) return;
+        for (uint32_t j = 0; j < cnt && off + j < max_records; j++) {
+            const uint2 o = st_off[j][tid], cc = st_ctr[j][tid], m = st_meta[j][tid];
+            tlsrec_batch_rec r;
+            memset(&r, 0, sizeof(r));
+            r.buf_off = o.x | (uint64_t) o.y << 32;             /* rec->buf = the header (:3715-3716) */
+            r.data_len = m.x & 0xffffu;
+            r.data_offset = m.x >> 16;
+            r.buf_len = r.data_offset + r.data_len;
+            memcpy(r.ctr, &cc, 8);                              /* explicit epoch + sequence number (:3683-3687) */
+            r.type = (uint8_t) m.y;
+            r.ver[0] = (uint8_t) (m.y >> 8);
+            r.ver[1] = (uint8_t) (m.y >> 16);
+            r.cid_len = (uint8_t) (m.y >> 24);
+            r.cid_off[0] = 11;                                  /* the CID follows the sequence number */
+            const uint32_t epoch = (cc.x & 0xffu) << 8 | ((cc.x >> 8) & 0xffu);
+            const uint64_t s48 = (uint64_t) ((cc.x >> 16) & 0xffu) << 40 | (uint64_t) (cc.x >> 24) << 32 |
+                                 (uint64_t) (cc.y & 0xffu) << 24 | ((cc.y >> 8) & 0xffu) << 16 |
+                                 ((cc.y >> 16) & 0xffu) << 8 | (cc.y >> 24);
+            r.slot = (epoch == ci.in_epoch && w0.fresh_s(s48)) ? ci.slot : NO_SLOT;
+            recs[off + j] = r;
+            guard_result(&res[off + j]);
+        }
+        return;
+    }
     uint32_t k = off, d = ci.first_dgram, kd = off;
     dtls_conn_walk<DG_U>(ci.first_dgram, ci.first_dgram + ci.ndgram, dg, arena, ci.cid_len,
                          [&](uint64_t base, const DtlsHdr &h, const uint8_t *p) {
@@ -1151,7 +1199,7 @@ __global__ __launch_bounds__(DG_THREADS) void dtls_frame_kernel(const tlsrec_dtl
                              k++;
                          },
                          [&](int32_t stop) {
-                             if (dgst) dgst[d] = (k - kd) | ((uint32_t) stop << 24);
+                             if (S == 0 && dgst) dgst[d] = (k - kd) | ((uint32_t) stop << 24);
                              d++;
                              kd = k;
                          },
@@ -1602,6 +1650,13 @@ static bool fused_env(void)
     const char *e = getenv("TLSREC_RX_FUSED");
     return !(e && atoi(e) == 0);
 }
+/* TLSREC_DTLS_STASH=0: the DTLS frame kernel's emit walks the headers again
+ * instead of reading the count walk's LDS copy (A/B runs) */
+static bool dtls_stash_env(void)
+{
+    const char *e = getenv("TLSREC_DTLS_STASH");
+    return !(e && atoi(e) == 0);
+}
 /* TLSREC_RX_PREFILL=0: the receive batch runs its guard kernel although the
  * emit kernels wrote the guard results (A/B runs) */
 static int prefill_env(void)
@@ -2004,9 +2059,17 @@ extern "C" int tlsrec_dtls_decrypt(const tlsrec_keytab *kt, const tlsrec_dtls_in
         TotMbox *mb = TLSREC_DTLS_LASTTILE_MB ? mailbox_next(&seq) : nullptr;
         /* the datagram summaries for the finish (none: it walks the headers) */
         if (ndgrams && tlsrec__scratch_acquire(st, 2, (size_t) ndgrams * 4, &dgl) == 0) dgst = (uint32_t *) dgl.mem;
-        hipLaunchKernelGGL(dtls_frame_kernel, dim3(tiles), dim3(DG_THREADS), 0, st, conns, nconns, dgrams, ndgrams,
-                           (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.bytes, sc.tstat, sc.tctr,
-                           recs, (recs && res) ? max_records : 0u, res, mb, seq, dgst);
+        /* LDS for the records of a connection of mean size (4 / 16 records:
+         * 24 / 96 KiB per workgroup); TLSREC_DTLS_STASH=0: the emit walks the
+         * headers again */
+        const uint32_t per = nconns ? (uint32_t) ((ndgrams + nconns - 1) / nconns) : 0;
+#define TLSREC_DTLS_FRAME(S_) hipLaunchKernelGGL(dtls_frame_kernel<S_>, dim3(tiles), dim3(DG_THREADS), 0, st, conns, \
+                           nconns, dgrams, ndgrams, (const uint8_t *) arena, slots, cap, sc.counts, sc.offs, sc.bytes, \
+                           sc.tstat, sc.tctr, recs, (recs && res) ? max_records : 0u, res, mb, seq, dgst)
+        if (!dtls_stash_env() || per > 16) TLSREC_DTLS_FRAME(0);
+        else if (per > 4) TLSREC_DTLS_FRAME(16);
+        else TLSREC_DTLS_FRAME(4);
+#undef TLSREC_DTLS_FRAME
         if (hipGetLastError() != hipSuccess) r = TLSREC_ERR_SSL_HW_ACCEL_FAILED;
         else if (mb) r = collect_totals(sc, nconns, st, seq, &total, &avg);
         else r = fetch_total(sc, nconns, st, &total, &avg);
